@@ -1,0 +1,549 @@
+/* ora_search.c -- TEST INFRASTRUCTURE ONLY (see ora.h).
+ *
+ * Plain-C restatement of the reference's order-graph search:
+ *   SparseParentList             score_cache/sparse_parent_list.cpp:20-55
+ *   StaticPatternDatabase        heuristic/static_pattern_database.cpp:82-247
+ *   Node / CompareNodeStar       base/node.h:24-135
+ *   PriorityQueue + heap         priority_queue/priority_queue.cpp:36-64,
+ *                                priority_queue/priority_queue-inl.h:19-234
+ *   run_astar_on_one_scc         astar/astar_main.cpp:216-546
+ *   reconstructSolution/outputs  astar_main.cpp:140-212,505-533
+ *   astar() driver               astar_main.cpp:548-644
+ *   Skeleton components          base/skeleton.cpp:187-230
+ */
+#define _GNU_SOURCE
+#include "ora.h"
+#include "ora_internal.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct { vs_t set; float cost; int64_t idx; } spl_entry;
+
+typedef struct {
+    int64_t count;
+    vs_t *parents;
+    float *scores;
+} spl_t;
+
+typedef struct {
+    vs_t group;
+    int size;
+    int *bitpos;     /* group bit positions, ascending */
+    float *pd;       /* 2^size, indexed by pext(R, group) */
+    uint8_t *present;
+} pdb_group;
+
+struct ora_search {
+    int n;
+    spl_t *spl;
+    int best_index; /* SparseParentList::bestIndex (stateful) */
+    int pd_count;
+    vs_t ancestors, scc;
+    pdb_group *groups;
+};
+
+static int cmp_spl(const void *a, const void *b) {
+    const spl_entry *x = (const spl_entry *)a, *y = (const spl_entry *)b;
+    if (x->cost < y->cost) return -1;
+    if (x->cost > y->cost) return 1;
+    /* pinned tie-break: file line order */
+    return x->idx < y->idx ? -1 : (x->idx > y->idx ? 1 : 0);
+}
+
+ora_search *ora_search_create(int n, const int64_t *offsets,
+                              const ora_varset *sets, const float *costs) {
+    ora_search *s = (ora_search *)calloc(1, sizeof(*s));
+    s->n = n;
+    s->spl = (spl_t *)calloc((size_t)n, sizeof(spl_t));
+    for (int v = 0; v < n; v++) {
+        int64_t c = offsets[v + 1] - offsets[v];
+        spl_entry *e = (spl_entry *)malloc(sizeof(spl_entry) * (size_t)(c ? c : 1));
+        /* ScoreCache::putScore overwrites duplicate parent sets: keep the
+         * last value at the first position (FloatMap semantics). */
+        omap seen;
+        omap_init(&seen, (size_t)c + 1);
+        int64_t m = 0;
+        for (int64_t i = 0; i < c; i++) {
+            uint64_t pos;
+            vs_t st = sets[offsets[v] + i];
+            if (omap_get(&seen, st, &pos)) { e[pos].cost = costs[offsets[v] + i]; continue; }
+            omap_put(&seen, st, (uint64_t)m);
+            e[m].set = st; e[m].cost = costs[offsets[v] + i]; e[m].idx = i; m++;
+        }
+        omap_free(&seen);
+        qsort(e, (size_t)m, sizeof(spl_entry), cmp_spl);
+        s->spl[v].count = m;
+        s->spl[v].parents = (vs_t *)malloc(sizeof(vs_t) * (size_t)(m ? m : 1));
+        s->spl[v].scores = (float *)malloc(sizeof(float) * (size_t)(m ? m : 1));
+        for (int64_t i = 0; i < m; i++) { s->spl[v].parents[i] = e[i].set; s->spl[v].scores[i] = e[i].cost; }
+        free(e);
+    }
+    return s;
+}
+
+static void free_groups(ora_search *s) {
+    if (!s->groups) return;
+    for (int g = 0; g < s->pd_count; g++) {
+        free(s->groups[g].bitpos); free(s->groups[g].pd); free(s->groups[g].present);
+    }
+    free(s->groups);
+    s->groups = NULL;
+}
+
+void ora_search_free(ora_search *s) {
+    if (!s) return;
+    for (int v = 0; v < s->n; v++) { free(s->spl[v].parents); free(s->spl[v].scores); }
+    free(s->spl);
+    free_groups(s);
+    free(s);
+}
+
+/* SparseParentList::getScore (sparse_parent_list.cpp:44-55) */
+static float spl_get(ora_search *s, int v, vs_t pars, int64_t *best) {
+    const spl_t *l = &s->spl[v];
+    int64_t i;
+    for (i = 0; i < l->count; i++)
+        if ((pars & l->parents[i]) == l->parents[i]) break;
+    *best = i;
+    if (i == l->count) return FLT_MAX;
+    return l->scores[i];
+}
+
+float ora_bestscore(ora_search *s, int v, ora_varset S, ora_varset *parents) {
+    int64_t b;
+    float c = spl_get(s, v, S, &b);
+    if (parents) *parents = (b < s->spl[v].count) ? s->spl[v].parents[b] : 0;
+    return c;
+}
+
+/* ---- static pattern database ------------------------------------------ */
+static int64_t pext_group(const pdb_group *g, vs_t R) {
+    int64_t r = 0;
+    for (int i = 0; i < g->size; i++)
+        if ((R >> g->bitpos[i]) & 1ULL) r |= 1LL << i;
+    return r;
+}
+static vs_t pdep_group(const pdb_group *g, int64_t r) {
+    vs_t R = 0;
+    for (int i = 0; i < g->size; i++)
+        if ((r >> i) & 1) R |= 1ULL << g->bitpos[i];
+    return R;
+}
+
+/* createPatternDatabase + expand (static_pattern_database.cpp:176-247).
+ * Layers are dense arrays over R = group \ key; keys are visited in
+ * ascending R order (the reference iterates a boost::unordered_map; the
+ * value is order-independent whenever all costs are <= 0). */
+static void create_pdb(ora_search *s, vs_t allVariables, pdb_group *g) {
+    const int64_t full = 1LL << g->size;
+    float *prev = (float *)calloc((size_t)full, sizeof(float));
+    uint8_t *prevp = (uint8_t *)calloc((size_t)full, 1);
+    float *cur = (float *)calloc((size_t)full, sizeof(float));
+    uint8_t *curp = (uint8_t *)calloc((size_t)full, 1);
+    g->pd = (float *)calloc((size_t)full, sizeof(float));
+    g->present = (uint8_t *)calloc((size_t)full, 1);
+    /* previousLayer[allVariables] = 0; R = group \ allVariables (empty) */
+    int64_t r0 = pext_group(g, g->group & ~allVariables);
+    prev[r0] = 0.0f; prevp[r0] = 1;
+    for (int layer = 0; layer <= g->size; layer++) {
+        memset(cur, 0, sizeof(float) * (size_t)full);
+        memset(curp, 0, (size_t)full);
+        for (int64_t r = 0; r < full; r++) {
+            if (!prevp[r]) continue;
+            const vs_t key = allVariables & ~pdep_group(g, r);
+            const float value = prev[r];
+            /* expand(key, value, ...) */
+            for (int leaf = 0; leaf < s->n; leaf++) {
+                if (!((key >> leaf) & 1ULL) || !((g->group >> leaf) & 1ULL)) continue;
+                const vs_t parentChoices = key | s->ancestors;
+                int64_t b;
+                const float the_score = spl_get(s, leaf, parentChoices, &b);
+                const float newG = the_score + value;
+                const vs_t nk = key ^ (1ULL << leaf);
+                const int64_t nr = pext_group(g, g->group & ~nk);
+                const float oldG = curp[nr] ? cur[nr] : 0.0f;
+                curp[nr] = 1;
+                if (oldG == 0 || newG < oldG) cur[nr] = newG;
+                else cur[nr] = oldG;
+            }
+            /* pattern = variableSet & ~key & ~ancestors */
+            const vs_t pattern = g->group & ~key & ~s->ancestors;
+            const int64_t pr = pext_group(g, pattern);
+            g->pd[pr] = value; g->present[pr] = 1;
+        }
+        float *t = prev; prev = cur; cur = t;
+        uint8_t *tp = prevp; prevp = curp; curp = tp;
+    }
+    for (int64_t r = 0; r < full; r++) {
+        if (!prevp[r]) continue;
+        const vs_t key = allVariables & ~pdep_group(g, r);
+        const int64_t pr = pext_group(g, g->group & ~key);
+        g->pd[pr] = prev[r]; g->present[pr] = 1;
+    }
+    free(prev); free(prevp); free(cur); free(curp);
+}
+
+/* StaticPatternDatabase::initialize(spgs) (static_pattern_database.cpp:82-134) */
+int ora_pdb_build(ora_search *s, int pd_count, ora_varset ancestors, ora_varset scc) {
+    free_groups(s);
+    if (pd_count < 1) return -1;
+    s->pd_count = pd_count;
+    s->ancestors = ancestors;
+    s->scc = scc;
+    s->groups = (pdb_group *)calloc((size_t)pd_count, sizeof(pdb_group));
+    const vs_t allVariables = scc;
+    int remainingCount = popc64(scc);
+    int var = scc ? __builtin_ctzll(scc) : -1; /* VARSET_FIND_FIRST_SET */
+    const int pds = (int)ceil((float)remainingCount / pd_count);
+    int x = 0;
+    for (int pd_i = 0; pd_i < pd_count; pd_i++) {
+        vs_t group = 0;
+        int sz;
+        for (sz = 0; sz < pds && x < remainingCount; sz++) {
+            group |= 1ULL << var;
+            /* VARSET_FIND_NEXT_SET: index + ffsl(vs >> (index+1)) */
+            vs_t rest = (var + 1 < 64) ? (scc >> (var + 1)) : 0;
+            var = var + (rest ? (__builtin_ctzll(rest) + 1) : 0);
+            ++x;
+        }
+        pdb_group *g = &s->groups[pd_i];
+        g->group = group;
+        g->size = sz;
+        g->bitpos = (int *)malloc(sizeof(int) * (size_t)(sz ? sz : 1));
+        int t = 0;
+        for (int b = 0; b < 64 && t < sz; b++)
+            if ((group >> b) & 1ULL) g->bitpos[t++] = b;
+        create_pdb(s, allVariables, g);
+    }
+    return 0;
+}
+
+/* StaticPatternDatabase::h (static_pattern_database.cpp:145-174) */
+float ora_pdb_h(ora_search *s, ora_varset S, int *complete) {
+    float h = 0;
+    const vs_t mask = (s->n >= 64) ? ~0ULL : ((1ULL << s->n) - 1ULL);
+    const vs_t remaining = (~S) & mask;
+    for (int pd_i = 0; pd_i < s->pd_count; pd_i++) {
+        const pdb_group *g = &s->groups[pd_i];
+        const vs_t vs = g->group & remaining;
+        const int64_t r = pext_group(g, vs);
+        if (!g->present[r]) return FLT_MAX / 64.0f;
+        if (vs == remaining) {
+            if (complete) *complete = 1;
+            return g->pd[r];
+        }
+        h += g->pd[r];
+    }
+    return h;
+}
+
+int ora_pdb_groups(ora_search *s, ora_varset *groups, int max_groups) {
+    for (int g = 0; g < s->pd_count && g < max_groups; g++) groups[g] = s->groups[g].group;
+    return s->pd_count;
+}
+
+float ora_pdb_value(ora_search *s, int g, ora_varset R) {
+    const pdb_group *gr = &s->groups[g];
+    return gr->pd[pext_group(gr, R & gr->group)];
+}
+
+/* ---- Node / heap -------------------------------------------------------- */
+typedef struct {
+    float g, h;
+    vs_t sub;
+    uint8_t leaf;
+    int pqPos;
+} node_t;
+
+typedef struct {
+    node_t **a;
+    int64_t size, cap;
+    int hang;
+} heap_t;
+
+/* CompareNodeStar (node.h:124-135): true if a has LOWER priority than b */
+static inline int cns(const node_t *a, const node_t *b) {
+    volatile float fa = a->g + a->h;
+    volatile float fb = b->g + b->h;
+    volatile float diff = fa - fb;
+    if (fabsf(diff) < FLT_EPSILON) {
+        int la = popc64(a->sub) & 0xff, lb = popc64(b->sub) & 0xff;
+        return (lb - la) > 0;
+    }
+    return diff > 0;
+}
+
+static void hp_push_hole(heap_t *H, int64_t hole, int64_t top, node_t *value) {
+    int64_t parent = (hole - 1) / 2;
+    while (hole > top && cns(H->a[parent], value)) {
+        H->a[hole] = H->a[parent];
+        H->a[hole]->pqPos = (int)hole;
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    H->a[hole] = value;
+    value->pqPos = (int)hole;
+}
+
+static void hp_push(heap_t *H, node_t *n) {
+    if (H->size == H->cap) {
+        H->cap = H->cap ? H->cap * 2 : 1024;
+        H->a = (node_t **)realloc(H->a, sizeof(node_t *) * (size_t)H->cap);
+    }
+    H->a[H->size++] = n;
+    hp_push_hole(H, H->size - 1, 0, n);
+}
+
+static void hp_adjust(heap_t *H, int64_t hole, int64_t len, node_t *value) {
+    const int64_t top = hole;
+    int64_t second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (cns(H->a[second], H->a[second - 1])) second--;
+        H->a[hole] = H->a[second];
+        H->a[hole]->pqPos = (int)hole;
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        H->a[hole] = H->a[second - 1];
+        H->a[hole]->pqPos = (int)hole;
+        hole = second - 1;
+    }
+    hp_push_hole(H, hole, top, value);
+}
+
+static node_t *hp_pop(heap_t *H) {
+    node_t *ret = H->a[0];
+    const int64_t last = H->size - 1;
+    node_t *value = H->a[last];
+    H->a[last] = H->a[0];
+    hp_adjust(H, 0, last, value);
+    H->size--;
+    return ret;
+}
+
+static void hp_update(heap_t *H, node_t *n) {
+    const int64_t pos = n->pqPos;
+    const int64_t parent = (pos - 1) / 2;
+    node_t *value = H->a[pos];
+    if (pos > 0 && cns(H->a[parent], value)) {
+        /* __up_heap */
+        int64_t par = (pos - 1) / 2, index = pos;
+        while (index > 0 && cns(H->a[par], value)) {
+            H->a[index] = H->a[par];
+            H->a[index]->pqPos = (int)index;
+            index = par;
+            par = (par - 1) / 2;
+        }
+        if (pos != index) { H->a[index] = value; value->pqPos = (int)index; }
+    } else {
+        /* __down_heap, including its left-only descent and missing pqPos
+         * update of the moved value (priority_queue-inl.h:176-208). */
+        const int64_t len = H->size;
+        int64_t index = pos, left = 2 * index + 1, right = 2 * index + 2, largest = len;
+        int64_t guard = 0;
+        while (index < len) {
+            if ((right >= len) || ((left < len) && cns(H->a[right], H->a[left]))) largest = left;
+            if (largest < len && cns(value, H->a[largest])) {
+                if (largest == index) { H->hang = 1; break; } /* reference loops forever here */
+                H->a[index] = H->a[largest];
+                H->a[largest]->pqPos = (int)index;
+                index = largest;
+                left = index * 2 + 1;
+                right = index * 2 + 2;
+            } else break;
+            if (++guard > 128) { H->hang = 1; break; }
+        }
+        if (pos != index) H->a[index] = value;
+    }
+}
+
+/* ---- A* ------------------------------------------------------------------ */
+typedef struct {
+    node_t *blocks[4096];
+    int nblocks;
+    int64_t used;
+} pool_t;
+#define POOL_BLOCK (1 << 16)
+static node_t *pool_new(pool_t *p) {
+    int64_t b = p->used / POOL_BLOCK, o = p->used % POOL_BLOCK;
+    if (b >= p->nblocks) {
+        if (p->nblocks >= 4096) { fprintf(stderr, "oracle A*: node pool exhausted\n"); abort(); }
+        p->blocks[p->nblocks++] = (node_t *)malloc(sizeof(node_t) * POOL_BLOCK);
+    }
+    p->used++;
+    return &p->blocks[b][o];
+}
+static void pool_free(pool_t *p) {
+    for (int i = 0; i < p->nblocks; i++) free(p->blocks[i]);
+    p->nblocks = 0; p->used = 0;
+}
+
+/* connected components (skeleton.cpp:187-230) in discovery order */
+static int components(const vs_t *edges, int n, vs_t *out) {
+    int nc = 0;
+    vs_t visited = 0;
+    for (int v = 0; v < n; v++) {
+        if ((visited >> v) & 1ULL) continue;
+        vs_t comp = 0;
+        /* explore_one_scc: DFS over ascending neighbour index */
+        int stack[64], it[64], sp = 0;
+        stack[sp] = v; it[sp] = 0; sp++;
+        visited |= 1ULL << v; comp |= 1ULL << v;
+        while (sp > 0) {
+            int cur = stack[sp - 1];
+            int i = it[sp - 1];
+            for (; i < n; i++) {
+                if ((visited >> i) & 1ULL) continue;
+                if ((edges[cur] >> i) & 1ULL) break;
+            }
+            if (i < n) {
+                it[sp - 1] = i + 1;
+                visited |= 1ULL << i; comp |= 1ULL << i;
+                stack[sp] = i; it[sp] = 0; sp++;
+            } else sp--;
+        }
+        out[nc++] = comp;
+    }
+    return nc;
+}
+
+static int run_astar_one(ora_search *s, const vs_t *edges, int skeleton_good,
+                         vs_t ancestors, vs_t the_scc, vs_t *vpar, int *order,
+                         float *goal_cost, int64_t *expanded, char *net_text,
+                         int64_t net_cap, int *hang) {
+    const int n = s->n;
+    omap generated;
+    omap_init(&generated, 1 << 12);
+    pool_t pool;
+    memset(&pool, 0, sizeof pool);
+    heap_t open;
+    memset(&open, 0, sizeof open);
+
+    /* VARSET_FIND_NEXT_SET(the_scc, 0) = 0 + ffsl(the_scc >> 1) */
+    const vs_t r1 = the_scc >> 1;
+    node_t *root = pool_new(&pool);
+    root->g = 0.0f; root->h = 0.0f; root->sub = ancestors;
+    root->leaf = (uint8_t)(r1 ? __builtin_ctzll(r1) + 1 : 0);
+    root->pqPos = 0;
+    hp_push(&open, root);
+
+    node_t *goal = NULL;
+    const vs_t allVariables = ancestors | the_scc;
+    const float upperBound = FLT_MAX;
+    int64_t nodesExpanded = 0;
+    while (open.size > 0) {
+        node_t *u = hp_pop(&open);
+        nodesExpanded++;
+        const vs_t variables = u->sub;
+        if (variables == allVariables) { goal = u; break; }
+        if (u->g + u->h > upperBound) break;
+        u->pqPos = -2;
+        for (int leaf = 0; leaf < n; leaf++) {
+            if ((variables >> leaf) & 1ULL) continue;
+            if (!((the_scc >> leaf) & 1ULL)) continue;
+            if (skeleton_good && variables != 0) {
+                if ((variables & edges[leaf]) == 0) continue;
+            }
+            const vs_t nv = variables | (1ULL << leaf);
+            uint64_t idx;
+            node_t *succ = NULL;
+            if (omap_get(&generated, nv, &idx)) succ = (node_t *)(uintptr_t)idx;
+            if (succ == NULL) {
+                int64_t b;
+                const float leaf_score = spl_get(s, leaf, nv, &b);
+                const float g = u->g + leaf_score;
+                int complete = 0;
+                const float h = ora_pdb_h(s, nv, &complete);
+                succ = pool_new(&pool);
+                succ->g = g; succ->h = h; succ->sub = nv; succ->leaf = (uint8_t)leaf; succ->pqPos = 0;
+                hp_push(&open, succ);
+                omap_put(&generated, nv, (uint64_t)(uintptr_t)succ);
+                continue;
+            }
+            if (succ->pqPos == -2) continue;
+            int64_t b;
+            const float g = u->g + spl_get(s, leaf, variables, &b);
+            if (g < succ->g) {
+                succ->leaf = (uint8_t)leaf;
+                succ->g = g;
+                hp_update(&open, succ);
+            }
+        }
+    }
+    *expanded += nodesExpanded;
+    if (open.hang) *hang = 1;
+    int ok = 0;
+    if (goal) {
+        ok = 1;
+        /* reconstructSolution (astar_main.cpp:140-166) */
+        int *total = (int *)calloc((size_t)n, sizeof(int));
+        vs_t *opt = (vs_t *)calloc((size_t)n, sizeof(vs_t));
+        vs_t remaining = goal->sub;
+        node_t *current = goal;
+        const int count = popc64(the_scc);
+        for (int i = 0; i < count && current; i++) {
+            const int leaf = current->leaf;
+            total[count - 1 - i] = leaf;
+            int64_t b;
+            (void)spl_get(s, leaf, remaining, &b);
+            opt[count - 1 - i] = (b < s->spl[leaf].count) ? s->spl[leaf].parents[b] : 0;
+            remaining ^= 1ULL << leaf;
+            uint64_t idx;
+            current = omap_get(&generated, remaining, &idx) ? (node_t *)(uintptr_t)idx : NULL;
+        }
+        /* netFile (astar_main.cpp:192-212) */
+        if (net_text && net_cap > 0) {
+            int64_t len = 0;
+            len += snprintf(net_text + len, (size_t)(net_cap - len), "NumVars %d\n", n);
+            for (int v = 0; v < n && len < net_cap; v++) {
+                len += snprintf(net_text + len, (size_t)(net_cap - len), "Var %d, parents", total[v] + 1);
+                for (int i = 0; i < n && len < net_cap; i++)
+                    if ((opt[v] >> i) & 1ULL) len += snprintf(net_text + len, (size_t)(net_cap - len), ", %d", i + 1);
+                if (len < net_cap) len += snprintf(net_text + len, (size_t)(net_cap - len), "\n");
+            }
+        }
+        /* netFile.csv parent matrix (astar_main.cpp:505-533) */
+        for (int v = 0; v < n; v++) vpar[v] = 0;
+        for (int v = 0; v < n; v++) vpar[total[v]] = opt[v];
+        for (int v = 0; v < n; v++) order[v] = total[v];
+        *goal_cost = goal->g;
+        free(total);
+        free(opt);
+    }
+    omap_free(&generated);
+    pool_free(&pool);
+    free(open.a);
+    return ok;
+}
+
+int ora_astar(ora_search *s, const ora_varset *edges, int pd_count,
+              ora_varset *vpar, int *order, float *goal_cost,
+              int64_t *expanded, char *net_text, int64_t net_cap) {
+    const int n = s->n;
+    const vs_t all = (n >= 64) ? ~0ULL : ((1ULL << n) - 1ULL);
+    /* astar(): heuristic over all variables, ancestors empty (:590-611) */
+    if (ora_pdb_build(s, pd_count, 0ULL, all) != 0) return -1;
+    vs_t comps[64];
+    int nc;
+    int skeleton_good = edges != NULL;
+    if (edges) nc = components(edges, n, comps);
+    else { comps[0] = all; nc = 1; }
+    *expanded = 0;
+    int fail = 0, hang = 0;
+    for (int i = 0; i < n; i++) { vpar[i] = 0; order[i] = 0; }
+    *goal_cost = 0.0f;
+    if (net_text && net_cap > 0) net_text[0] = 0;
+    for (int c = 0; c < nc; c++) {
+        if (!run_astar_one(s, edges, skeleton_good, 0ULL, comps[c], vpar, order,
+                           goal_cost, expanded, net_text, net_cap, &hang))
+            fail = 1;
+    }
+    if (hang) return 2;
+    return fail;
+}
