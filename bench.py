@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X cBIC-score hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2] [--mode weak|shard]
+
+One step = one full cBIC scoring pass (every parent set of size <= k of every
+variable through the layer-synchronous HIP scorer, stored-set rule and
+dominance recursion included) over inputs already resident in HBM.
+
+--mode weak (default): every rank scores the whole configuration on its own
+    synthetic dataset (seed 9200 + rank): a batch of independent structure-
+    learning problems, per-GPU work fixed as N grows, no collective in the
+    data path.
+--mode shard: one dataset, variables striped over ranks (score_main.cpp:136-139)
+    and the per-variable (set, score) lists exchanged with one RCCL
+    all_gather inside the timed step; strong scaling.
+
+Rank 0 prints one JSON line.  cpu_baseline = the CPU oracle (a faithful C
+restatement that solves each OLS over all N rows like the reference) timed on
+a bounded sample on this host, rank 0 at N=1 only.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "urlearning-cpp_amd"))
+
+import synth  # noqa: E402
+import ulg  # noqa: E402
+
+METRIC = "cBIC parent-set scores/sec + A* expansions/sec, n=25 full skeleton"
+CONFIGS = {
+    "c2": dict(n=20, N=10000, k=4, lam=2.0),
+    "c3": dict(n=25, N=10000, k=6, lam=2.0),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return ws, rank, local
+
+
+def cpu_baseline(cfg, X, target_s=15.0):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    oracle.build()
+    n, k, lam = cfg["n"], cfg["k"], cfg["lam"]
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1))
+    nvars = min(n, threads)
+    variables = list(range(nvars))
+    cands = [(1 << n) - 1] * n
+    ds = oracle.Dataset(X)
+    t0 = time.perf_counter()
+    probe_frac = 0.002
+    c0 = oracle.score_sample(ds, lam, variables, cands, k, probe_frac, threads)
+    dt0 = time.perf_counter() - t0
+    frac = min(1.0, probe_frac * target_s / max(dt0, 1e-3))
+    t0 = time.perf_counter()
+    c = oracle.score_sample(ds, lam, variables, cands, k, frac, threads)
+    dt = time.perf_counter() - t0
+    return {"value": c / dt, "unit": "parent-set scores/s", "cores": threads, "kind": "port",
+            "sample": f"CPU oracle (C restatement, per-set OLS over all N rows) on {nvars} of {n} variables, "
+                      f"first {frac:.4f} of every layer 1..{k} in Gosper order: {c} parent sets in {dt:.2f} s "
+                      f"on {threads} threads"}
+
+
+def roofline(ctx, cfg, per_launch_sets):
+    """Dominant kernel = the layer-k 'rest' launch (sets without variable 0)."""
+    k = cfg["k"]
+    name = f"score_layer_{k}_rest"
+    p = ctx.profile_get(name)
+    if p is None:
+        return None, None
+    sets = per_launch_sets
+    # compulsory HBM bytes per scored set = 4 (k direct-subset score reads) + 4 (score write)
+    bytes_per_set = 4 * (k + 1)
+    achieved = sets * bytes_per_set / (p["avg_ms"] * 1e-3) / 1e9
+    flops_per_set = 2 * k ** 3 / 3 + 2 * k * k + 2 * k
+    return ({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": name,
+             "avg_launch_ms": p["avg_ms"], "launches": p["count"], "sets_per_launch": sets,
+             "bytes_per_set": bytes_per_set,
+             "fp64_flops_per_set": flops_per_set,
+             "fp64_tflops": sets * flops_per_set / (p["avg_ms"] * 1e-3) / 1e12}, p)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--mode", default="weak", choices=["weak", "shard"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    cfg = CONFIGS[args.config]
+    n, N, k, lam = cfg["n"], cfg["N"], cfg["k"], cfg["lam"]
+
+    import torch
+    dist = None
+    if ws > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=ws)
+
+    seed = 9200 + (rank if args.mode == "weak" else 0)
+    X, _ = synth.gaussian_sem(n, N, seed)
+    ctx = ulg.Context(local)
+    ctx.load(X, lam)
+    cands_all = [(1 << n) - 1] * n
+    if args.mode == "shard":
+        variables = [v for v in range(n) if v % ws == rank]
+    else:
+        variables = list(range(n))
+    cands = [cands_all[v] for v in variables]
+    units_rank = len(variables) * sum(math.comb(n - 1, L) for L in range(k + 1))
+
+    def step():
+        stored, scored = ctx.score(variables, cands, k)
+        if args.mode == "shard" and ws > 1:
+            # one RCCL all_gather of the per-variable (set, score) lists
+            cnt = torch.tensor([stored], dtype=torch.int64, device="cuda")
+            cnts = [torch.zeros_like(cnt) for _ in range(ws)]
+            dist.all_gather(cnts, cnt)
+            mx = int(max(int(c.item()) for c in cnts))
+            sets_t = torch.empty(max(stored, 1), dtype=torch.int64, device="cuda")
+            sc_t = torch.empty(max(stored, 1), dtype=torch.float32, device="cuda")
+            off_t = torch.empty(len(variables) + 1, dtype=torch.int64, device="cuda")
+            ctx.fetch_device(sets_t.data_ptr(), sc_t.data_ptr(), off_t.data_ptr())
+            packed = torch.zeros(mx, 3, dtype=torch.int32, device="cuda")
+            if stored:
+                packed[:stored, 0:2] = sets_t[:stored].view(torch.int32).view(stored, 2)
+                packed[:stored, 2] = sc_t[:stored].view(torch.int32)
+            out = torch.empty(ws * mx, 3, dtype=torch.int32, device="cuda")
+            dist.all_gather_into_tensor(out, packed)
+        return scored
+
+    for _ in range(args.warmup):
+        step()
+    ctx.profile(True)
+    ctx.profile_reset()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    scored_total = 0
+    for _ in range(args.steps):
+        scored_total += step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    ctx.profile(False)
+    elapsed = t1 - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        u = torch.tensor([scored_total], dtype=torch.float64, device="cuda")
+        dist.all_reduce(u, op=dist.ReduceOp.SUM)
+        scored_all = float(u.item())
+    else:
+        scored_all = float(scored_total)
+
+    # sets in one launch of the dominant kernel (layer k, sets without variable 0)
+    per_launch = sum(math.comb(n - 1 - 1, k) for v in variables if v != 0) + (math.comb(n - 1, k) if 0 in variables else 0)
+    roof, _ = roofline(ctx, cfg, per_launch)
+    kernels = ctx.profile_dump()
+
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": scored_all / elapsed,
+            "unit": "parent-set scores/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak" if args.mode == "weak" else "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": f"synthetic: seeded linear-Gaussian SEM (synth.gaussian_sem, seed {9200}+rank), "
+                    f"full n x n skeleton",
+            "config": {"workload": f"C3 cBIC scoring: n={n}, N={N}, max-parents k={k}, lambda={lam}, full skeleton, "
+                                   f"all {n} variables per {'GPU' if args.mode == 'weak' else 'job'}",
+                       "config_id": args.config, "mode": args.mode,
+                       "parent_sets_per_step_per_rank": units_rank},
+            "roofline": roof,
+            "kernel_ms_total": {kk: round(vv["total_ms"], 4) for kk, vv in kernels.items()},
+        }
+        if ws == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(cfg, X)
+        print(json.dumps(res))
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,118 @@
+/*
+ * ulg.h -- C ABI of the MI355X-native URLearning hot path (libulg.so).
+ *
+ * Drop-in boundary for the reference's plugin points on the
+ * cBIC-score + order-graph-search path (ninalu/urlearning-cpp, paths
+ * relative to urlearning/):
+ *
+ *   ulg_cbic_load        replaces BIC_OLS_Function::BIC_OLS_Function
+ *                        (scoring_function/BIC_OLS.cpp:30-123): data load,
+ *                        centring/scaling, Gram matrix (the reference's
+ *                        printed corr_mat = Z'Z/N, :105).
+ *   ulg_cbic_score       replaces ScoreCalculator::calculateScores
+ *                        (scoring_function/score_calculator.h:35,
+ *                        score_calculator.cpp:33-135) driving
+ *                        ScoringFunction::calculateScore (scoring_function.h:16-23,
+ *                        BIC_OLS.cpp:174-389) for a batch of variables; the
+ *                        stored-set rule and the find_best_subset_score
+ *                        dominance recursion are reproduced exactly.
+ *   ulg_cbic_fetch       hands the stored FloatMap contents back (what
+ *                        scoringThread prints, score/score_main.cpp:173-203).
+ *   ulg_bestscore_*      replaces bestscorecalculators::BestScoreCalculator
+ *                        (score_cache/best_score_calculator.h:16-26) with the
+ *                        list calculator's semantics
+ *                        (score_cache/sparse_parent_list.cpp:20-55).
+ *   ulg_pdb_*            replaces heuristics::StaticPatternDatabase
+ *                        (heuristic/static_pattern_database.cpp:82-247).
+ *   ulg_astar            replaces run_astar_on_one_scc
+ *                        (astar/astar_main.cpp:216-546).
+ *
+ * Conventions (mirroring the reference's): the caller owns host buffers;
+ * device memory is owned by the context; hot calls report errors by an int
+ * status (0 = ok) and ulg_last_error(); one context per host thread and per
+ * GPU (one process per GPU for multi-GPU runs).  varsets are uint64 bit
+ * masks (bit i = variable i), as in typedefs.h:647-755.  Scores are the
+ * .pss "score" (higher is better); costs are A* costs (= -score after the
+ * .pss "%f" round trip, score_cache.cpp:151).
+ */
+#ifndef ULG_H
+#define ULG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ulg_ctx ulg_ctx;
+
+#define ULG_OK 0
+#define ULG_ERR_ARG 1
+#define ULG_ERR_HIP 2
+#define ULG_ERR_STATE 3
+#define ULG_ERR_UNSUPPORTED 4
+
+/* Largest parent-set size the HIP scorer handles (compile-time unrolled
+ * Cholesky + dominance recursion per layer). */
+#define ULG_MAX_PARENTS_GPU 8
+
+/* ---- context --------------------------------------------------------- */
+/* One device per context: ndev must be 1 (multi-GPU = one process per GPU). */
+int ulg_create(const int *device_ids, int ndev, ulg_ctx **out);
+void ulg_destroy(ulg_ctx *ctx);
+const char *ulg_last_error(const ulg_ctx *ctx);
+/* Library build identifier ("gfx950 ..."). */
+const char *ulg_version(void);
+
+/* ---- cBIC scoring (BIC_OLS.cpp, score_calculator.cpp) ----------------- */
+/* data_colmajor: N x n doubles, column-major (column j = variable j), as
+ * Armadillo holds raw_data.  n <= 63.  Normalises each column to zero mean
+ * and unit sample variance (N-1) and builds the FP64 Gram matrix Z'Z on the
+ * device (MFMA f64). */
+int ulg_cbic_load(ulg_ctx *ctx, const double *data_colmajor, int64_t N, int n,
+                  double lambda);
+/* Copy the device Gram matrix Z'Z (n x n, row-major) to host. */
+int ulg_cbic_gram(ulg_ctx *ctx, double *gram_out);
+
+/* Score all parent sets of size <= max_parents within each variable's
+ * candidate set (candidates[i] for variable vars[i]; the variable's own bit
+ * is ignored).  Runs the layer-synchronous HIP scorer; results stay on the
+ * device until ulg_cbic_fetch.  *total_stored = number of stored sets,
+ * *total_scored = number of parent sets evaluated (incl. empty sets). */
+int ulg_cbic_score(ulg_ctx *ctx, const int *vars, int nv,
+                   const uint64_t *candidates, int max_parents,
+                   int64_t *total_stored, int64_t *total_scored);
+/* Copy the stored sets out.  offsets[nv+1]; variable vars[i] owns
+ * [offsets[i], offsets[i+1]); within a variable, sets are ordered by
+ * (|set|, set value) -- the reference's Gosper insertion order.
+ * device_ptrs = 1: sets/scores/offsets are device pointers (e.g. torch
+ * tensors on this context's device); 0: host pointers. */
+int ulg_cbic_fetch(ulg_ctx *ctx, uint64_t *sets, float *scores,
+                   int64_t *offsets, int device_ptrs);
+/* Convenience: ulg_cbic_score + ulg_cbic_fetch to host buffers of
+ * capacity cap entries; returns ULG_ERR_ARG if cap is too small. */
+int ulg_cbic_score_vars(ulg_ctx *ctx, const int *vars, int nv,
+                        const uint64_t *candidates, int max_parents,
+                        uint64_t *sets, float *scores, int64_t *offsets,
+                        int64_t cap);
+
+/* The .pss "%f" + atof round trip the A* input goes through
+ * (score_main.cpp:191, score_cache.cpp:151), computed exactly on the
+ * device: cost = float(-1 * strtod(printf("%f", score))). */
+int ulg_quantize_costs(ulg_ctx *ctx, const float *scores, float *costs,
+                       int64_t count);
+
+/* ---- profiling (per-kernel HIP-event timing on the context stream) ---- */
+int ulg_profile_enable(ulg_ctx *ctx, int on);
+/* Average duration (ms) and launch count of kernels whose name matches
+ * `name` exactly, since the last reset.  Returns ULG_ERR_ARG if none. */
+int ulg_profile_get(ulg_ctx *ctx, const char *name, double *avg_ms,
+                    int64_t *count, double *total_ms);
+/* Writes a newline-separated "name count total_ms" listing into buf. */
+int ulg_profile_dump(ulg_ctx *ctx, char *buf, int64_t cap);
+int ulg_profile_reset(ulg_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

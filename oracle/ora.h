@@ -70,6 +70,13 @@ int64_t ora_score_variable(const ora_dataset *ds, double lambda, int v,
                            ora_varset candidates, int max_parents,
                            ora_varset *sets, float *scores, int64_t cap);
 
+/* Same, with an alternative evaluation schedule (sched = 1: per layer, sets
+ * containing variable 0 first, then the rest, each phase in reverse Gosper
+ * order) -- used to validate the GPU's two-launch layer schedule. */
+int64_t ora_score_variable_sched(const ora_dataset *ds, double lambda, int v,
+                                 ora_varset candidates, int max_parents, int sched,
+                                 ora_varset *sets, float *scores, int64_t cap);
+
 /* All variables, T threads striped by v % T (score_main.cpp:132-207).
  * candidates[v] is the candidate set of v (2-hop skeleton neighbourhood).
  * Output per variable v occupies [offsets[v], offsets[v+1]) of sets/scores;
@@ -79,6 +86,12 @@ int ora_score_all(const ora_dataset *ds, double lambda,
                   const ora_varset *candidates, int max_parents, int threads,
                   const int64_t *cap_per_var, ora_varset *sets, float *scores,
                   int64_t *offsets);
+
+/* Bounded CPU-baseline sample (bench.py): variables vlist striped over T
+ * threads, each layer cut to its first ceil(frac*|layer|) Gosper sets.
+ * Returns the number of parent sets scored. */
+int64_t ora_score_sample(const ora_dataset *ds, double lambda, const int *vlist, int nvl,
+                         const ora_varset *candidates, int max_parents, double frac, int threads);
 
 /* 2-hop candidate set N(v) U N(N(v)) from skeleton rows
  * (score_main.cpp:146-153); edges==NULL means no skeleton (all bits). */

@@ -385,7 +385,7 @@ static int cmp_entry(const void *a, const void *b) {
 static int64_t score_variable_ws(const ora_dataset *ds, double lambda, int v,
                                  vs_t candidates, int max_parents,
                                  ora_varset *sets, float *scores, int64_t cap,
-                                 ols_ws *w) {
+                                 ols_ws *w, int sched, double frac, int64_t *nscored) {
     const int n = ds->n;
     omap cache, checked;
     omap_init(&cache, 1024);
@@ -393,6 +393,7 @@ static int64_t score_variable_ws(const ora_dataset *ds, double lambda, int v,
     /* empty set first; stored because score (-0.0f) < 1 (:56-61) */
     float sc = calculate_score(ds, lambda, v, 0ULL, &cache, &checked, w);
     if (sc < 1) omap_put(&cache, 0ULL, f2u(sc));
+    if (nscored) (*nscored)++;
     int nbr[64];
     int nn = 0;
     for (int i = 0; i < n; i++)
@@ -401,16 +402,54 @@ static int64_t score_variable_ws(const ora_dataset *ds, double lambda, int v,
         vs_t compact = 0;
         for (int i = 0; i < layer; i++) compact |= 1ULL << i;
         const vs_t max = (nn >= 64) ? ~0ULL : (1ULL << nn);
-        while (compact < max) {
-            vs_t vars = 0;
-            for (int i = 0; i < nn; i++)
-                if ((compact >> i) & 1ULL) vars |= 1ULL << nbr[i];
-            if (!((vars >> v) & 1ULL)) {
-                float s = calculate_score(ds, lambda, v, vars, &cache, &checked, w);
-                if (s < 0) omap_put(&cache, vars, f2u(s));
+        /* bounded-sample timing mode (bench.py cpu_baseline): only the first
+         * ceil(frac * |layer|) sets of each layer in Gosper order */
+        int64_t budget = INT64_MAX;
+        if (frac < 1.0) {
+            double c = 1.0;
+            const int m = nn - (int)((candidates >> v) & 1ULL);
+            for (int i = 1; i <= layer; i++) c = c * (double)(m - layer + i) / (double)i;
+            budget = (int64_t)ceil(frac * c);
+        }
+        if (sched == 0) {
+            while (compact < max && budget > 0) {
+                vs_t vars = 0;
+                for (int i = 0; i < nn; i++)
+                    if ((compact >> i) & 1ULL) vars |= 1ULL << nbr[i];
+                if (!((vars >> v) & 1ULL)) {
+                    float s = calculate_score(ds, lambda, v, vars, &cache, &checked, w);
+                    if (s < 0) omap_put(&cache, vars, f2u(s));
+                    if (nscored) (*nscored)++;
+                    budget--;
+                }
+                compact = next_permutation(compact);
+                if (compact == 0) break;
             }
-            compact = next_permutation(compact);
-            if (compact == 0) break;
+        } else {
+            /* Validation schedule for the GPU's two-launch layers:
+             * sets containing variable 0 first, then the rest, each phase in
+             * REVERSE Gosper order. */
+            int64_t cnt = 0, capl = 1024;
+            vs_t *lay = (vs_t *)malloc(sizeof(vs_t) * (size_t)capl);
+            while (compact < max) {
+                vs_t vars = 0;
+                for (int i = 0; i < nn; i++)
+                    if ((compact >> i) & 1ULL) vars |= 1ULL << nbr[i];
+                if (!((vars >> v) & 1ULL)) {
+                    if (cnt == capl) { capl *= 2; lay = (vs_t *)realloc(lay, sizeof(vs_t) * (size_t)capl); }
+                    lay[cnt++] = vars;
+                }
+                compact = next_permutation(compact);
+                if (compact == 0) break;
+            }
+            for (int phase = 0; phase < 2; phase++)
+                for (int64_t i = cnt - 1; i >= 0; i--) {
+                    const int has0 = (int)(lay[i] & 1ULL);
+                    if ((phase == 0) != has0) continue;
+                    float s = calculate_score(ds, lambda, v, lay[i], &cache, &checked, w);
+                    if (s < 0) omap_put(&cache, lay[i], f2u(s));
+                }
+            free(lay);
         }
     }
     /* output sorted by (|set|, set) == the reference's insertion order */
@@ -435,7 +474,7 @@ int64_t ora_score_variable(const ora_dataset *ds, double lambda, int v,
                            ora_varset candidates, int max_parents,
                            ora_varset *sets, float *scores, int64_t cap) {
     ols_ws w = {0};
-    int64_t r = score_variable_ws(ds, lambda, v, candidates, max_parents, sets, scores, cap, &w);
+    int64_t r = score_variable_ws(ds, lambda, v, candidates, max_parents, sets, scores, cap, &w, 0, 1.0, NULL);
     free(w.X); free(w.Y); free(w.tmp);
     return r;
 }
@@ -460,15 +499,21 @@ typedef struct {
     float *scores;
     int64_t *counts;
     int err;
+    double frac;
+    int64_t nscored;
+    const int *vlist;
+    int nvl;
 } thr_arg;
 
 static void *score_thread(void *p) {
     thr_arg *a = (thr_arg *)p;
     ols_ws w = {0};
-    for (int v = 0; v < a->ds->n; v++) {
-        if (v % a->threads != a->tid) continue; /* score_main.cpp:136-139 */
+    const int nl = a->vlist ? a->nvl : a->ds->n;
+    for (int vi = 0; vi < nl; vi++) {
+        const int v = a->vlist ? a->vlist[vi] : vi;
+        if (vi % a->threads != a->tid) continue; /* score_main.cpp:136-139 */
         int64_t c = score_variable_ws(a->ds, a->lambda, v, a->cands[v], a->max_parents,
-                                      a->sets + a->base[v], a->scores + a->base[v], a->cap[v], &w);
+                                      a->sets + a->base[v], a->scores + a->base[v], a->cap[v], &w, 0, a->frac, &a->nscored);
         if (c < 0) a->err = 1;
         a->counts[v] = c;
     }
@@ -489,7 +534,7 @@ int ora_score_all(const ora_dataset *ds, double lambda,
     pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
     thr_arg *args = (thr_arg *)calloc((size_t)threads, sizeof(thr_arg));
     for (int t = 0; t < threads; t++) {
-        thr_arg a = {ds, lambda, candidates, max_parents, threads, t, cap_per_var, base, sets, scores, counts, 0};
+        thr_arg a = {ds, lambda, candidates, max_parents, threads, t, cap_per_var, base, sets, scores, counts, 0, 1.0, 0, NULL, 0};
         args[t] = a;
         pthread_create(&th[t], NULL, score_thread, &args[t]);
     }
@@ -517,4 +562,46 @@ float ora_quantize_cost(float score) {
     snprintf(buf, sizeof buf, "%f", (double)score);
     float cost = -1 * atof(buf);
     return cost;
+}
+
+int64_t ora_score_variable_sched(const ora_dataset *ds, double lambda, int v,
+                                 ora_varset candidates, int max_parents, int sched,
+                                 ora_varset *sets, float *scores, int64_t cap) {
+    ols_ws w = {0};
+    int64_t r = score_variable_ws(ds, lambda, v, candidates, max_parents, sets, scores, cap, &w, sched, 1.0, NULL);
+    free(w.X); free(w.Y); free(w.tmp);
+    return r;
+}
+
+/* Bounded CPU-baseline sample: variables vlist[0..nvl) striped over T
+ * threads, each layer truncated to its first ceil(frac * |layer|) sets in
+ * Gosper order.  Returns the number of parent sets scored. */
+int64_t ora_score_sample(const ora_dataset *ds, double lambda, const int *vlist, int nvl,
+                         const ora_varset *candidates, int max_parents, double frac, int threads) {
+    const int n = ds->n;
+    if (threads < 1) threads = 1;
+    int64_t *cap = (int64_t *)malloc(sizeof(int64_t) * (size_t)n);
+    int64_t *base = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n + 1));
+    int64_t *counts = (int64_t *)calloc((size_t)n, sizeof(int64_t));
+    base[0] = 0;
+    for (int v = 0; v < n; v++) {
+        const int m = popc64(candidates[v] & ~(1ULL << v));
+        double c = 1.0, tot = 1.0;
+        for (int L = 1; L <= max_parents && L <= m; L++) { c = c * (double)(m - L + 1) / (double)L; tot += ceil(frac * c); }
+        cap[v] = (int64_t)tot + 1;
+        base[v + 1] = base[v] + cap[v];
+    }
+    ora_varset *sets = (ora_varset *)malloc(sizeof(ora_varset) * (size_t)base[n]);
+    float *scores = (float *)malloc(sizeof(float) * (size_t)base[n]);
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
+    thr_arg *args = (thr_arg *)calloc((size_t)threads, sizeof(thr_arg));
+    for (int t = 0; t < threads; t++) {
+        thr_arg a = {ds, lambda, candidates, max_parents, threads, t, cap, base, sets, scores, counts, 0, frac, 0, vlist, nvl};
+        args[t] = a;
+        pthread_create(&th[t], NULL, score_thread, &args[t]);
+    }
+    int64_t tot = 0;
+    for (int t = 0; t < threads; t++) { pthread_join(th[t], NULL); tot += args[t].nscored; }
+    free(cap); free(base); free(counts); free(sets); free(scores); free(th); free(args);
+    return tot;
 }

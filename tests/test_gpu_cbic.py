@@ -1,0 +1,139 @@
+"""GPU parity tests of the cBIC scorer (libulg.so on cuda:0) against the CPU
+oracle.  Bar: the stored parent-set lists are identical (index work,
+bit-exact); scores agree within 1e-6 relative (north_star tolerance; the
+oracle solves each OLS over all N rows, the GPU through the Gram matrix)."""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import load_fig
+import synth
+
+pytestmark = pytest.mark.gpu
+
+REL_TOL = 1e-6
+
+
+def _compare_lists(o_offs, o_sets, o_scores, g_offs, g_sets, g_scores, variables, ctx=""):
+    assert len(o_offs) == len(g_offs), ctx
+    for i, v in enumerate(variables):
+        a = o_sets[o_offs[i]:o_offs[i + 1]]
+        b = g_sets[g_offs[i]:g_offs[i + 1]]
+        if not np.array_equal(a, b):
+            sa, sb = set(int(x) for x in a), set(int(x) for x in b)
+            raise AssertionError(f"{ctx} variable {v}: stored sets differ: only oracle {sorted(sa - sb)[:8]}, "
+                                 f"only gpu {sorted(sb - sa)[:8]} ({len(a)} vs {len(b)})")
+        sa = o_scores[o_offs[i]:o_offs[i + 1]].astype(np.float64)
+        sb = g_scores[g_offs[i]:g_offs[i + 1]].astype(np.float64)
+        err = np.abs(sa - sb) / np.maximum(np.abs(sa), 1.0)
+        assert err.max(initial=0.0) <= REL_TOL, f"{ctx} variable {v}: max rel score error {err.max()}"
+
+
+def _oracle_lists(oracle, X, lam, variables, cands, k):
+    ds = oracle.Dataset(X)
+    offs = [0]
+    sets, scores = [], []
+    for v, c in zip(variables, cands):
+        s, sc = ds.score_variable(lam, v, c, k)
+        sets.append(s)
+        scores.append(sc)
+        offs.append(offs[-1] + len(s))
+    return np.array(offs), np.concatenate(sets), np.concatenate(scores)
+
+
+def test_gram_matches_numpy(ulg_ctx):
+    X, _ = synth.gaussian_sem(21, 7000, 9100)
+    ulg_ctx.load(X, 2.0)
+    G = ulg_ctx.gram()
+    Z = (X - X.mean(0)) / X.std(0, ddof=1)
+    ref = Z.T @ Z
+    assert np.allclose(G, ref, rtol=1e-11, atol=1e-8 * len(X))
+    # asymmetric check: individual off-diagonal entries, not just symmetry
+    assert abs(G[3, 17] - ref[3, 17]) <= 1e-9 * len(X)
+    assert np.allclose(G, G.T, rtol=0, atol=1e-9 * len(X))
+
+
+@pytest.mark.parametrize("fig", [1, 2])
+@pytest.mark.parametrize("lam", [0.5, 1.0, 2.0])
+def test_fig_scores_match_oracle(ulg_ctx, oracle_built, fig, lam):
+    X = load_fig(fig)
+    n = X.shape[1]
+    variables = list(range(n))
+    cands = [(1 << n) - 1] * n
+    ulg_ctx.load(X, lam)
+    g = ulg_ctx.score_all(variables, cands, 3)
+    o = _oracle_lists(oracle_built, X, lam, variables, cands, 3)
+    _compare_lists(*o, *g, variables, ctx=f"fig{fig} lam={lam}")
+
+
+@pytest.mark.parametrize("seed,n,N,k", [(9200, 10, 3000, 4), (9201, 12, 2000, 6), (9202, 9, 1500, 8),
+                                        (9203, 14, 1000, 3), (9204, 8, 800, 7)])
+def test_synthetic_full_skeleton_matches_oracle(ulg_ctx, oracle_built, seed, n, N, k):
+    X, _ = synth.gaussian_sem(n, N, seed)
+    variables = list(range(n))
+    cands = [(1 << n) - 1] * n
+    ulg_ctx.load(X, 2.0)
+    g = ulg_ctx.score_all(variables, cands, k)
+    o = _oracle_lists(oracle_built, X, 2.0, variables, cands, k)
+    _compare_lists(*o, *g, variables, ctx=f"seed {seed}")
+
+
+def test_sparse_skeleton_and_variable_subset(ulg_ctx, oracle_built):
+    """2-hop candidate sets from a sparse skeleton; a permuted subset of the
+    variables; variable 0 both inside and outside the candidate lists."""
+    import ulg
+    n = 16
+    X, W = synth.gaussian_sem(n, 2500, 9210)
+    rows = synth.true_skeleton_edges(W, extra_frac=0.1, seed=3)
+    cands_all = ulg.candidates_from_edges(rows, n)
+    variables = [7, 0, 13, 2, 9]
+    cands = [cands_all[v] for v in variables]
+    ulg_ctx.load(X, 1.0)
+    g = ulg_ctx.score_all(variables, cands, 4)
+    o = _oracle_lists(oracle_built, X, 1.0, variables, cands, 4)
+    _compare_lists(*o, *g, variables, ctx="sparse")
+
+
+def test_quantize_matches_oracle(ulg_ctx, oracle_built):
+    rng = np.random.default_rng(7)
+    vals = np.concatenate([rng.normal(0, 3e4, 20000), rng.normal(0, 1, 20000), rng.normal(0, 1e-5, 5000),
+                           [0.0078125, 0.0234375, -0.0078125, -1e-9, 1e-9, 0.0, -0.0, 5e-7, -5e-7, 3e38, -3e38,
+                            1e-40, np.inf, -np.inf]]).astype(np.float32)
+    got = ulg_ctx.quantize(vals)
+    exp = np.array([oracle_built.quantize(float(x)) for x in vals], dtype=np.float32)
+    assert got.tobytes() == exp.tobytes()
+
+
+def test_c2_properties_full_size(ulg_ctx, oracle_built):
+    """BASELINE config C2 (n=20, N=10k, k=4, full skeleton) at full size:
+    size-independent properties on every variable, oracle parity on two."""
+    n, N, k = 20, 10000, 4
+    X, _ = synth.gaussian_sem(n, N, 9200)
+    variables = list(range(n))
+    cands = [(1 << n) - 1] * n
+    ulg_ctx.load(X, 2.0)
+    stored, scored = ulg_ctx.score(variables, cands, k)
+    assert scored == n * sum(math.comb(n - 1, L) for L in range(k + 1)) == 100720
+    offs, sets, scores = ulg_ctx.fetch(stored)
+    assert offs[0] == 0 and offs[-1] == stored
+    for v in range(n):
+        s = sets[offs[v]:offs[v + 1]]
+        assert int(s[0]) == 0 and np.float32(scores[offs[v]]).tobytes() == np.float32(-0.0).tobytes()
+        keys = [(bin(int(x)).count("1"), int(x)) for x in s]
+        assert keys == sorted(keys) and len(set(keys)) == len(keys)
+        assert all(not ((int(x) >> v) & 1) and bin(int(x)).count("1") <= k for x in s)
+    assert np.isfinite(scores).all()
+    for v in (0, 11):
+        o = _oracle_lists(oracle_built, X, 2.0, [v], [cands[v]], k)
+        g = (np.array([0, offs[v + 1] - offs[v]]), sets[offs[v]:offs[v + 1]], scores[offs[v]:offs[v + 1]])
+        _compare_lists(*o, *g, [v], ctx="C2")
+
+
+def test_rescoring_is_deterministic(ulg_ctx):
+    X, _ = synth.gaussian_sem(15, 4000, 9220)
+    ulg_ctx.load(X, 2.0)
+    a = ulg_ctx.score_all(list(range(15)), [(1 << 15) - 1] * 15, 5)
+    b = ulg_ctx.score_all(list(range(15)), [(1 << 15) - 1] * 15, 5)
+    for x, y in zip(a, b):
+        assert x.tobytes() == y.tobytes()

@@ -1,0 +1,852 @@
+// cbic.hip -- continuous-BIC parent-set scoring on MI355X (gfx950).
+//
+// Reference path (ninalu/urlearning-cpp, urlearning/):
+//   BIC_OLS_Function ctor          scoring_function/BIC_OLS.cpp:30-123
+//   calculateScoreAndBeta          BIC_OLS.cpp:277-389 (mlpack OLS, no intercept)
+//   calculateScore                 BIC_OLS.cpp:174-276 (store / prune rule)
+//   find_best_subset_score         BIC_OLS.cpp:125-172 (dominance recursion)
+//   calculateScores_internal       score_calculator.cpp:54-135 (layers, Gosper)
+//
+// Design (MI355X-first):
+//   * the data is normalised once and the FP64 Gram matrix G = Z'Z is built
+//     with v_mfma_f64_16x16x4_f64 (the only dense contraction on the path);
+//   * every parent set is then one lane: gather G[P,P], G[P,v] from LDS,
+//     k x k Cholesky in registers, RSS = G[v,v] - |L^-1 b|^2;
+//   * the dominance recursion (whose result depends on the reference's
+//     zero-padded parent vector and XOR-toggle) is replayed
+//     exactly on per-lane bitsets over subsets of P u {variable 0};
+//   * a layer is two launches -- sets that contain variable 0, then the rest
+//      -- which reproduces the sequential Gosper order;
+//   * every (variable, layer) owns a dense float slab indexed by the colex
+//     rank of the set inside the variable's candidate list (= the Gosper
+//     enumeration index), holding the stored score or an absent sentinel.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "ulg_internal.h"
+
+using namespace ulg;
+
+namespace {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBlock = 256;
+constexpr int kGramRows = 1024;  // rows of Z per Gram wave (split-K chunk)
+
+__device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
+__device__ __forceinline__ float absent_f() { return __uint_as_float(kAbsentBits); }
+
+// ------------------------------------------------------------------------
+// Normalisation (BIC_OLS.cpp:66-97): x - mean, divided by the sample std
+// (N-1) of the centred column.  Deterministic tree reductions.
+// ------------------------------------------------------------------------
+__device__ double block_sum(double v, double *red) {
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int s = kBlock / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    double r = red[0];
+    __syncthreads();
+    return r;
+}
+
+__global__ void __launch_bounds__(kBlock) colstats_kernel(const double *raw, int64_t N, double *stat) {
+    __shared__ double red[kBlock];
+    const double *x = raw + (int64_t)blockIdx.x * N;
+    double s = 0.0;
+    for (int64_t i = threadIdx.x; i < N; i += kBlock) s += x[i];
+    const double mean = block_sum(s, red) / (double)N;
+    // arma::var(x - mean): two-pass with the compensation term
+    double s2 = 0.0;
+    for (int64_t i = threadIdx.x; i < N; i += kBlock) s2 += x[i] - mean;
+    const double m2 = block_sum(s2, red) / (double)N;
+    double a2 = 0.0, a3 = 0.0;
+    for (int64_t i = threadIdx.x; i < N; i += kBlock) {
+        const double t = m2 - (x[i] - mean);
+        a2 += t * t;
+        a3 += t;
+    }
+    a2 = block_sum(a2, red);
+    a3 = block_sum(a3, red);
+    if (threadIdx.x == 0) {
+        const double var = N > 1 ? (a2 - a3 * a3 / (double)N) / (double)(N - 1) : 0.0;
+        stat[2 * blockIdx.x] = mean;
+        stat[2 * blockIdx.x + 1] = sqrt(var);
+    }
+}
+
+// Z row-major N x npad (padded columns zero): lanes of a wave read one row.
+__global__ void __launch_bounds__(kBlock) normalise_kernel(const double *raw, int64_t N, int n, int npad,
+                                                           const double *stat, double *z) {
+    const int64_t idx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (idx >= N * npad) return;
+    const int64_t r = idx / npad;
+    const int c = (int)(idx % npad);
+    double v = 0.0;
+    if (c < n) v = (raw[(int64_t)c * N + r] - stat[2 * c]) / stat[2 * c + 1];
+    z[idx] = v;
+}
+
+// G = Z'Z on v_mfma_f64_16x16x4_f64.  One wave per (16x16 tile, row chunk).
+// A[i][k] = Z[r0+k][I0+i], B[k][j] = Z[r0+k][J0+j]; lane l holds
+// i = j = l & 15, k = l >> 4.  D: col = l & 15, row = (l >> 4) + 4 * reg.
+__global__ void __launch_bounds__(64) gram_mfma_kernel(const double *z, int64_t N, int npad, int tiles,
+                                                       double *partials) {
+    const int chunk = blockIdx.x;
+    const int tile = blockIdx.y;
+    const int I0 = (tile / tiles) * 16, J0 = (tile % tiles) * 16;
+    const int lane = threadIdx.x;
+    const int i = lane & 15, k = lane >> 4;
+    const int64_t rb = (int64_t)chunk * kGramRows;
+    const int64_t re = rb + kGramRows < N ? rb + kGramRows : N;
+    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int64_t r0 = rb; r0 < re; r0 += 4) {
+        const int64_t r = r0 + k;
+        double a = 0.0, b = 0.0;
+        if (r < re) {
+            a = z[r * npad + I0 + i];
+            b = z[r * npad + J0 + i];
+        }
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    }
+    double *out = partials + ((int64_t)chunk * tiles * tiles + tile) * 256;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+        const int row = (lane >> 4) + 4 * reg;
+        out[row * 16 + (lane & 15)] = acc[reg];
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) gram_reduce_kernel(const double *partials, int chunks, int tiles, int n,
+                                                             double *gram) {
+    const int idx = blockIdx.x * kBlock + threadIdx.x;
+    if (idx >= n * n) return;
+    const int r = idx / n, c = idx % n;
+    const int tile = (r / 16) * tiles + (c / 16);
+    const int e = (r % 16) * 16 + (c % 16);
+    double s = 0.0;
+    for (int ch = 0; ch < chunks; ++ch) s += partials[((int64_t)ch * tiles * tiles + tile) * 256 + e];
+    gram[idx] = s;
+}
+
+// ------------------------------------------------------------------------
+// Combinatorics on compact candidate indices.  colex rank of a sorted set
+// {a_1 < ... < a_L} is sum_j C(a_j, j): Gosper's next-permutation walks
+// exactly this order (typedefs.h:692-697), so rank == enumeration index.
+// ------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t B(const uint32_t *binom, int a, int k) { return binom[a * kBinomK + k]; }
+
+__device__ __forceinline__ uint64_t unrank_colex(uint64_t r, int l, int U, const uint32_t *binom) {
+    uint64_t mask = 0;
+    int c = U - 1;
+    for (int i = l; i >= 1; --i) {
+        while (c >= 0 && (uint64_t)B(binom, c, i) > r) --c;
+        mask |= 1ull << c;
+        r -= B(binom, c, i);
+        --c;
+    }
+    return mask;
+}
+
+__device__ __forceinline__ uint64_t rank_colex(uint64_t mask, const uint32_t *binom) {
+    uint64_t r = 0;
+    int j = 0;
+    while (mask) {
+        const int a = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        ++j;
+        r += B(binom, a, j);
+    }
+    return r;
+}
+
+// Per-lane bitset over the subsets of (P u {var 0}) in local numbering.
+template <int W>
+struct Bits {
+    uint64_t w[W];
+    __device__ __forceinline__ void clear() {
+#pragma unroll
+        for (int j = 0; j < W; ++j) w[j] = 0;
+    }
+    __device__ __forceinline__ bool test(uint32_t i) const {
+        uint64_t x = w[0];
+#pragma unroll
+        for (int j = 1; j < W; ++j) x = ((int)(i >> 6) == j) ? w[j] : x;
+        return (x >> (i & 63)) & 1ull;
+    }
+    __device__ __forceinline__ void set(uint32_t i) {
+        const uint64_t bit = 1ull << (i & 63);
+#pragma unroll
+        for (int j = 0; j < W; ++j) w[j] |= ((int)(i >> 6) == j) ? bit : 0ull;
+    }
+};
+
+// find_best_subset_score (BIC_OLS.cpp:125-172) replayed on local masks.
+// pv: M entries of 4 bits (local bit numbers; entries past the filled ones
+// are 0 == variable 0, the zero-initialised arma::uvec of SURVEY N3).  Only
+// WHICH cached keys are visited matters: the return value is the max over
+// their cached values (and 0), so the recursion records them in `visited`.
+template <int M, int W>
+__device__ __forceinline__ void best_subset(uint32_t T, uint32_t pv, const Bits<W> &present, Bits<W> &checked,
+                                            Bits<W> &visited) {
+#pragma nounroll
+    for (int idx = 0; idx < M; ++idx) {
+        const uint32_t u = (pv >> (4 * idx)) & 15u;
+        const uint32_t T2 = T ^ (1u << u);
+        if (checked.test(T2)) continue;
+        if (present.test(T2)) {
+            visited.set(T2);
+            continue;
+        }
+        if constexpr (M > 1) {
+            uint32_t npv = 0;
+            int j = 0;
+#pragma nounroll
+            for (int i = 0; i < M; ++i) {
+                const uint32_t pi = (pv >> (4 * i)) & 15u;
+                if (pi == u) continue;
+                npv |= pi << (4 * j);
+                ++j;
+                best_subset<M - 1, W>(T2, npv, present, checked, visited);
+                checked.set(T2);
+            }
+        }
+    }
+}
+
+struct ScoreArgs {
+    const double *gram;      // n x n row-major
+    const uint32_t *binom;   // [64][kBinomK]
+    const uint8_t *cand;     // [nv][64] compact index -> variable
+    const int *meta;         // [nv][4]: variable, m, var0in, -
+    const uint64_t *tbl_off; // [nv*S + 1] start of (vi, layer) slab
+    const uint64_t *work;    // [nv + 1] prefix of this launch's sets
+    float *table;
+    double N;
+    double lambda;
+    int n, nv, S;
+};
+
+// LDS carve: gram | binom | work | tbl_off   (all offsets 16-B aligned)
+struct LdsLayout {
+    int gram, binom, work, toff, total;
+};
+__host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
+__host__ __device__ inline LdsLayout lds_layout(int n, int nv, int S) {
+    LdsLayout l;
+    l.gram = 0;
+    l.binom = align16(l.gram + n * n * 8);
+    l.work = align16(l.binom + 64 * kBinomK * 4);
+    l.toff = align16(l.work + (nv + 1) * 8);
+    l.total = align16(l.toff + (nv * S + 1) * 8);
+    return l;
+}
+
+template <int L, int PHASE>  // PHASE 0: sets containing variable 0; 1: the rest
+__global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const LdsLayout lay = lds_layout(a.n, a.nv, a.S);
+    double *g = reinterpret_cast<double *>(smem + lay.gram);
+    uint32_t *binom = reinterpret_cast<uint32_t *>(smem + lay.binom);
+    uint64_t *work = reinterpret_cast<uint64_t *>(smem + lay.work);
+    uint64_t *toff = reinterpret_cast<uint64_t *>(smem + lay.toff);
+    for (int i = threadIdx.x; i < a.n * a.n; i += kBlock) g[i] = a.gram[i];
+    for (int i = threadIdx.x; i < 64 * kBinomK; i += kBlock) binom[i] = a.binom[i];
+    for (int i = threadIdx.x; i <= a.nv; i += kBlock) work[i] = a.work[i];
+    for (int i = threadIdx.x; i <= a.nv * a.S; i += kBlock) toff[i] = a.tbl_off[i];
+    __syncthreads();
+
+    const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (gid >= work[a.nv]) return;
+    int lo = 0, hi = a.nv;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (work[mid] <= gid) lo = mid; else hi = mid;
+    }
+    const int vi = lo;
+    const int v = a.meta[vi * 4 + 0];
+    const int m = a.meta[vi * 4 + 1];
+    const bool z = a.meta[vi * 4 + 2] != 0;
+    const uint64_t r = gid - work[vi];
+
+    uint64_t cm;  // compact mask of P over the variable's candidate list
+    if (PHASE == 0) cm = (unrank_colex(r, L - 1, m - 1, binom) << 1) | 1ull;
+    else if (z) cm = unrank_colex(r, L, m - 1, binom) << 1;
+    else cm = unrank_colex(r, L, m, binom);
+    const uint64_t rankP = rank_colex(cm, binom);
+
+    // parent variables in ascending order (== BIC_OLS parent_vec order)
+    const uint8_t *cl = a.cand + vi * 64;
+    int gv[L];
+    {
+        uint64_t rem = cm;
+#pragma unroll
+        for (int i = 0; i < L; ++i) {
+            const int b = __builtin_ctzll(rem);
+            rem &= rem - 1;
+            gv[i] = cl[b];
+        }
+    }
+
+    // ---- OLS via the Gram matrix: Cholesky of G[P,P], y = L^-1 G[P,v] ----
+    double Lm[L][L];
+    double y[L];
+    const int n = a.n;
+#pragma unroll
+    for (int i = 0; i < L; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) Lm[i][j] = g[gv[i] * n + gv[j]];
+#pragma unroll
+    for (int i = 0; i < L; ++i) y[i] = g[gv[i] * n + v];
+    const double cvv = g[v * n + v];
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+        double s = Lm[j][j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) s -= Lm[j][k] * Lm[j][k];
+        const double d = sqrt(s);
+        Lm[j][j] = d;
+        const double inv = 1.0 / d;
+#pragma unroll
+        for (int i = j + 1; i < L; ++i) {
+            double t = Lm[i][j];
+#pragma unroll
+            for (int k = 0; k < j; ++k) t -= Lm[i][k] * Lm[j][k];
+            Lm[i][j] = t * inv;
+        }
+    }
+    double yy = 0.0;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        double t = y[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) t -= Lm[i][k] * y[k];
+        t = t / Lm[i][i];
+        y[i] = t;
+        yy += t * t;
+    }
+    const double rss = cvv - yy;
+    // BIC_OLS.cpp:366  num_err*log(error_L2) + lambda*log(num_err)*k - 0
+    const double the_score = a.N * log(rss / a.N) + a.lambda * log(a.N) * (double)L - 0.0;
+    const float ts = (float)the_score;
+
+    float out;
+    if (ts >= 0.0f) {
+        // returned -ts; the caller stores it iff it is < 0 (score_calculator.cpp:111)
+        const float s = -ts;
+        out = (s < 0.0f) ? s : absent_f();
+    } else {
+        constexpr int W = (L + 1) <= 6 ? 1 : (1 << ((L + 1) - 6));
+        const bool v0inP = z && (cm & 1ull);
+        const uint64_t E = z ? (cm & ~1ull) : cm;
+        uint64_t cpack = 0;  // local bit -> compact index, 6 bits each (bit 0 -> 0)
+        {
+            uint64_t rem = E;
+#pragma unroll
+            for (int i = 1; i <= L; ++i) {
+                if (rem) {
+                    const uint64_t b = (uint64_t)__builtin_ctzll(rem);
+                    rem &= rem - 1;
+                    cpack |= b << (6 * i);
+                }
+            }
+        }
+        const uint32_t Plocal = v0inP ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
+        const int q = v0inP ? L : L + 1;
+        const uint64_t vbase = (uint64_t)vi * a.S;
+
+        // presence of every candidate key in the cache as it stands now
+        Bits<W> present;
+        present.clear();
+        const uint32_t full = 1u << q;
+#pragma nounroll
+        for (uint32_t t = 1; t < full; ++t) {
+            const int pc = __builtin_popcount(t);
+            bool cand = pc <= L && t != Plocal && (z || !(t & 1u));
+            if (pc == L) cand = cand && PHASE == 1 && (t & 1u);
+            if (!cand) continue;
+            uint64_t rk = 0;
+            uint32_t rem = t;
+            int j = 0;
+            while (rem) {
+                const int lb = __builtin_ctz(rem);
+                rem &= rem - 1;
+                ++j;
+                rk += B(binom, (int)((cpack >> (6 * lb)) & 63ull), j);
+            }
+            const float val = a.table[toff[vbase + pc] + rk];
+            if (fbits(val) != kAbsentBits) present.set(t);
+        }
+
+        Bits<W> checked, visited;
+        checked.clear();
+        visited.clear();
+        checked.set(0u);  // checked.insert(empty_set)
+        uint32_t pvtop = 0;
+#pragma unroll
+        for (int i = 0; i < L; ++i) pvtop |= (uint32_t)(i + (v0inP ? 0 : 1)) << (4 * i);
+        best_subset<L, W>(Plocal, pvtop, present, checked, visited);
+
+        float best = 0.0f;
+#pragma unroll
+        for (int wj = 0; wj < W; ++wj) {
+            uint64_t x = visited.w[wj];
+            while (x) {
+                const uint32_t t = (uint32_t)(wj * 64 + __builtin_ctzll(x));
+                x &= x - 1;
+                uint64_t rk = 0;
+                uint32_t rem = t;
+                int j = 0;
+                while (rem) {
+                    const int lb = __builtin_ctz(rem);
+                    rem &= rem - 1;
+                    ++j;
+                    rk += B(binom, (int)((cpack >> (6 * lb)) & 63ull), j);
+                }
+                const float val = a.table[toff[vbase + __builtin_popcount(t)] + rk];
+                if (val > best) best = val;
+            }
+        }
+        // BIC_OLS.cpp:234: best_subset_score + bic_threshold >= -the_score
+        out = ((double)best + 0.0 >= (double)(-ts)) ? absent_f() : -ts;
+    }
+    a.table[toff[(uint64_t)vi * a.S + L] + rankP] = out;
+}
+
+__global__ void empty_set_kernel(const uint64_t *tbl_off, int nv, int S, float *table) {
+    const int vi = blockIdx.x * blockDim.x + threadIdx.x;
+    if (vi < nv) table[tbl_off[(uint64_t)vi * S]] = -0.0f;  // cache[empty] = -0.0f (BIC_OLS.cpp:249)
+}
+
+// ---- compaction of the slabs into (set, score) lists ------------------------
+constexpr int kSlotsPerThread = 4;
+constexpr int kSlotsPerBlock = kBlock * kSlotsPerThread;
+
+__global__ void __launch_bounds__(kBlock) count_kernel(const float *table, uint64_t total, uint64_t *blk) {
+    __shared__ uint32_t red[kBlock];
+    const uint64_t base = (uint64_t)blockIdx.x * kSlotsPerBlock + threadIdx.x * kSlotsPerThread;
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < kSlotsPerThread; ++j) {
+        const uint64_t s = base + j;
+        if (s < total && fbits(table[s]) != kAbsentBits) ++c;
+    }
+    red[threadIdx.x] = c;
+    __syncthreads();
+    for (int s = kBlock / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) blk[blockIdx.x] = red[0];
+}
+
+// exclusive scan of nb block counts in place, total in blk[nb]; one block.
+__global__ void __launch_bounds__(1024) scan_kernel(uint64_t *blk, int64_t nb) {
+    __shared__ uint64_t part[1024];
+    const int64_t per = (nb + 1023) / 1024;
+    const int64_t b0 = threadIdx.x * per, b1 = b0 + per < nb ? b0 + per : nb;
+    uint64_t s = 0;
+    for (int64_t i = b0; i < b1; ++i) s += blk[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t acc = 0;
+        for (int i = 0; i < 1024; ++i) {
+            const uint64_t t = part[i];
+            part[i] = acc;
+            acc += t;
+        }
+        blk[nb] = acc;
+    }
+    __syncthreads();
+    uint64_t acc = part[threadIdx.x];
+    for (int64_t i = b0; i < b1; ++i) {
+        const uint64_t t = blk[i];
+        blk[i] = acc;
+        acc += t;
+    }
+}
+
+struct WriteArgs {
+    const float *table;
+    const uint64_t *blk;
+    const uint64_t *tbl_off;
+    const int *meta;
+    const uint8_t *cand;
+    const uint32_t *binom;
+    uint64_t total;
+    int nv, S;
+    uint64_t *sets;
+    float *scores;
+    int64_t *offsets;
+};
+
+__global__ void __launch_bounds__(kBlock) write_kernel(WriteArgs a) {
+    __shared__ uint32_t pre[kBlock];
+    __shared__ uint32_t binom[64 * kBinomK];
+    for (int i = threadIdx.x; i < 64 * kBinomK; i += kBlock) binom[i] = a.binom[i];
+    const uint64_t base = (uint64_t)blockIdx.x * kSlotsPerBlock + threadIdx.x * kSlotsPerThread;
+    uint32_t c = 0;
+    float vals[kSlotsPerThread];
+#pragma unroll
+    for (int j = 0; j < kSlotsPerThread; ++j) {
+        const uint64_t s = base + j;
+        vals[j] = s < a.total ? a.table[s] : absent_f();
+        if (fbits(vals[j]) != kAbsentBits) ++c;
+    }
+    pre[threadIdx.x] = c;
+    __syncthreads();
+    // Hillis-Steele inclusive scan over 256 counts
+    for (int off = 1; off < kBlock; off <<= 1) {
+        const uint32_t t = (int)threadIdx.x >= off ? pre[threadIdx.x - off] : 0u;
+        __syncthreads();
+        pre[threadIdx.x] += t;
+        __syncthreads();
+    }
+    uint64_t pos = a.blk[blockIdx.x] + pre[threadIdx.x] - c;
+    const int nseg = a.nv * a.S;
+#pragma unroll
+    for (int j = 0; j < kSlotsPerThread; ++j) {
+        if (fbits(vals[j]) == kAbsentBits) continue;
+        const uint64_t s = base + j;
+        int lo = 0, hi = nseg;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (a.tbl_off[mid] <= s) lo = mid; else hi = mid;
+        }
+        const int vi = lo / a.S, L = lo % a.S;
+        const int m = a.meta[vi * 4 + 1];
+        const uint64_t cm = unrank_colex(s - a.tbl_off[lo], L, m, binom);
+        uint64_t gs = 0;
+        uint64_t rem = cm;
+        while (rem) {
+            const int b = __builtin_ctzll(rem);
+            rem &= rem - 1;
+            gs |= 1ull << a.cand[vi * 64 + b];
+        }
+        a.sets[pos] = gs;
+        a.scores[pos] = vals[j];
+        if (L == 0) a.offsets[vi] = (int64_t)pos;
+        ++pos;
+    }
+}
+
+__global__ void set_total_kernel(const uint64_t *blk, int64_t nb, int nv, int64_t *offsets) {
+    offsets[nv] = (int64_t)blk[nb];
+}
+
+// ---- "%f" + atof round trip (score_main.cpp:191 / score_cache.cpp:151) -----
+// D = round-half-even(|x| * 10^6) exactly in integers (glibc printf is exact
+// with ties to even); strtod of D/10^6 is the correctly rounded double
+// quotient; cost = float(-1 * that).
+__device__ __forceinline__ float quantize_one(float x) {
+    const uint32_t u = __float_as_uint(x);
+    const uint32_t ex = (u >> 23) & 0xffu;
+    const bool neg = (u >> 31) != 0;
+    if (ex == 0xffu) return -x;  // inf -> -inf, nan stays nan
+    uint64_t M;
+    int E;
+    if (ex == 0) { M = u & 0x7fffffu; E = -149; }
+    else { M = (u & 0x7fffffu) | 0x800000u; E = (int)ex - 150; }
+    double mag;
+    if (E >= 0) {
+        mag = (double)fabsf(x);  // x * 10^6 is an integer: printed exactly
+    } else {
+        const int sh = -E;
+        const uint64_t num = M * 1000000ull;  // < 2^44
+        uint64_t D;
+        if (sh >= 64) D = 0;
+        else {
+            D = num >> sh;
+            const uint64_t rem = num & ((1ull << sh) - 1ull);
+            const uint64_t half = 1ull << (sh - 1);
+            if (rem > half || (rem == half && (D & 1ull))) ++D;
+        }
+        mag = (double)D / 1000000.0;
+    }
+    const double val = neg ? -mag : mag;
+    return (float)(-1.0 * val);
+}
+
+__global__ void quantize_kernel(const float *in, float *out, int64_t count) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < count) out[i] = quantize_one(in[i]);
+}
+
+using KernelFn = void (*)(ScoreArgs);
+template <int L>
+KernelFn pick(int phase) {
+    return phase == 0 ? score_layer_kernel<L, 0> : score_layer_kernel<L, 1>;
+}
+KernelFn layer_kernel(int L, int phase) {
+    switch (L) {
+        case 1: return pick<1>(phase);
+        case 2: return pick<2>(phase);
+        case 3: return pick<3>(phase);
+        case 4: return pick<4>(phase);
+        case 5: return pick<5>(phase);
+        case 6: return pick<6>(phase);
+        case 7: return pick<7>(phase);
+        case 8: return pick<8>(phase);
+        default: return nullptr;
+    }
+}
+static_assert(kMaxL == 8, "layer_kernel dispatch covers layers 1..8");
+
+const char *kLayerNames[2][kMaxL + 1] = {
+    {"", "score_layer_1_var0", "score_layer_2_var0", "score_layer_3_var0", "score_layer_4_var0",
+     "score_layer_5_var0", "score_layer_6_var0", "score_layer_7_var0", "score_layer_8_var0"},
+    {"", "score_layer_1_rest", "score_layer_2_rest", "score_layer_3_rest", "score_layer_4_rest",
+     "score_layer_5_rest", "score_layer_6_rest", "score_layer_7_rest", "score_layer_8_rest"}};
+
+}  // namespace
+
+extern "C" {
+
+int ulg_cbic_load(ulg_ctx *c, const double *data, int64_t N, int n, double lambda) {
+    if (!c || !data || N < 2 || n < 1 || n > kMaxVars) return set_err(c, ULG_ERR_ARG, "ulg_cbic_load: bad arguments");
+    ULG_HIP(c, hipSetDevice(c->device));
+    c->loaded = false;
+    c->scored = false;
+    c->n = n;
+    c->N = N;
+    c->lambda = lambda;
+    c->npad = (n + 15) / 16 * 16;
+    const int tiles = c->npad / 16;
+    const int chunks = (int)((N + kGramRows - 1) / kGramRows);
+    int rc;
+    if ((rc = ensure(c, c->raw, (size_t)(N * n))) || (rc = ensure(c, c->z, (size_t)(N * c->npad))) ||
+        (rc = ensure(c, c->gram, (size_t)(n * n))) || (rc = ensure(c, c->colstat, (size_t)(2 * n))) ||
+        (rc = ensure(c, c->partials, (size_t)chunks * tiles * tiles * 256)))
+        return rc;
+    ULG_HIP(c, hipMemcpyAsync(c->raw.p, data, sizeof(double) * (size_t)(N * n), hipMemcpyHostToDevice, c->stream));
+    prof_begin(c, "colstats");
+    colstats_kernel<<<n, kBlock, 0, c->stream>>>(c->raw.p, N, c->colstat.p);
+    prof_end(c);
+    const int64_t tot = N * c->npad;
+    prof_begin(c, "normalise");
+    normalise_kernel<<<(unsigned)((tot + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(c->raw.p, N, n, c->npad,
+                                                                                         c->colstat.p, c->z.p);
+    prof_end(c);
+    prof_begin(c, "gram_mfma_f64");
+    gram_mfma_kernel<<<dim3(chunks, tiles * tiles), 64, 0, c->stream>>>(c->z.p, N, c->npad, tiles, c->partials.p);
+    prof_end(c);
+    prof_begin(c, "gram_reduce");
+    gram_reduce_kernel<<<(n * n + kBlock - 1) / kBlock, kBlock, 0, c->stream>>>(c->partials.p, chunks, tiles, n,
+                                                                               c->gram.p);
+    prof_end(c);
+    ULG_HIP(c, hipGetLastError());
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    c->loaded = true;
+    return ULG_OK;
+}
+
+int ulg_cbic_gram(ulg_ctx *c, double *out) {
+    if (!c || !out) return ULG_ERR_ARG;
+    if (!c->loaded) return set_err(c, ULG_ERR_STATE, "ulg_cbic_gram: no data loaded");
+    ULG_HIP(c, hipSetDevice(c->device));
+    ULG_HIP(c, hipMemcpy(out, c->gram.p, sizeof(double) * (size_t)(c->n * c->n), hipMemcpyDeviceToHost));
+    return ULG_OK;
+}
+
+int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidates, int max_parents,
+                   int64_t *total_stored, int64_t *total_scored) {
+    if (!c) return ULG_ERR_ARG;
+    if (!c->loaded) return set_err(c, ULG_ERR_STATE, "ulg_cbic_score: call ulg_cbic_load first");
+    if (!vars || !candidates || nv < 1 || nv > c->n) return set_err(c, ULG_ERR_ARG, "ulg_cbic_score: bad variable list");
+    ULG_HIP(c, hipSetDevice(c->device));
+    const int n = c->n;
+    uint64_t seen = 0;
+    for (int i = 0; i < nv; ++i) {
+        if (vars[i] < 0 || vars[i] >= n || ((seen >> vars[i]) & 1ull))
+            return set_err(c, ULG_ERR_ARG, "ulg_cbic_score: variables must be distinct and < n");
+        seen |= 1ull << vars[i];
+    }
+    const uint64_t allmask = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+    if (max_parents < 1 || max_parents > n - 1) max_parents = n - 1;
+    // per-variable candidate lists (the variable itself never enters a set,
+    // score_calculator.cpp:100)
+    std::vector<uint8_t> cand((size_t)nv * 64, 0);
+    std::vector<int> meta((size_t)nv * 4, 0);
+    std::vector<int> mv(nv);
+    int kmax = 0;
+    for (int i = 0; i < nv; ++i) {
+        const uint64_t C = candidates[i] & allmask & ~(1ull << vars[i]);
+        int m = 0;
+        for (int b = 0; b < n; ++b)
+            if ((C >> b) & 1ull) cand[(size_t)i * 64 + m++] = (uint8_t)b;
+        mv[i] = m;
+        meta[i * 4 + 0] = vars[i];
+        meta[i * 4 + 1] = m;
+        meta[i * 4 + 2] = (C & 1ull) ? 1 : 0;  // variable 0 is a candidate (compact index 0)
+        kmax = std::max(kmax, std::min(m, max_parents));
+    }
+    if (kmax > kMaxL)
+        return set_err(c, ULG_ERR_UNSUPPORTED,
+                       "ulg_cbic_score: parent sets larger than ULG_MAX_PARENTS_GPU (8) are not supported");
+    const int S = kmax + 1;
+    // slab offsets: (vi, L) -> start, final sentinel = total slots
+    std::vector<uint64_t> toff((size_t)nv * S + 1);
+    uint64_t acc = 0;
+    int64_t scored = 0;
+    for (int i = 0; i < nv; ++i)
+        for (int L = 0; L < S; ++L) {
+            toff[(size_t)i * S + L] = acc;
+            const uint64_t cnt = (L <= max_parents) ? binom64(mv[i], L) : 0;
+            acc += cnt;
+            scored += (int64_t)cnt;
+        }
+    toff[(size_t)nv * S] = acc;
+    const uint64_t total_slots = acc;
+    // per launch work prefixes: [L][phase][nv+1]
+    std::vector<uint64_t> work((size_t)(kmax + 1) * 2 * (nv + 1), 0);
+    for (int L = 1; L <= kmax; ++L)
+        for (int ph = 0; ph < 2; ++ph) {
+            uint64_t *w = &work[((size_t)L * 2 + ph) * (nv + 1)];
+            uint64_t s = 0;
+            for (int i = 0; i < nv; ++i) {
+                w[i] = s;
+                const bool z = meta[i * 4 + 2] != 0;
+                uint64_t cnt;
+                if (L > max_parents) cnt = 0;
+                else if (ph == 0) cnt = z ? binom64(mv[i] - 1, L - 1) : 0;
+                else cnt = z ? binom64(mv[i] - 1, L) : binom64(mv[i], L);
+                s += cnt;
+            }
+            w[nv] = s;
+        }
+    int rc;
+    if ((rc = ensure(c, c->table, total_slots)) || (rc = ensure(c, c->d_tbl_off, toff.size())) ||
+        (rc = ensure(c, c->d_work, work.size())) || (rc = ensure(c, c->d_cand, cand.size())) ||
+        (rc = ensure(c, c->d_meta, meta.size())))
+        return rc;
+    ULG_HIP(c, hipMemcpyAsync(c->d_tbl_off.p, toff.data(), toff.size() * 8, hipMemcpyHostToDevice, c->stream));
+    ULG_HIP(c, hipMemcpyAsync(c->d_work.p, work.data(), work.size() * 8, hipMemcpyHostToDevice, c->stream));
+    ULG_HIP(c, hipMemcpyAsync(c->d_cand.p, cand.data(), cand.size(), hipMemcpyHostToDevice, c->stream));
+    ULG_HIP(c, hipMemcpyAsync(c->d_meta.p, meta.data(), meta.size() * 4, hipMemcpyHostToDevice, c->stream));
+
+    prof_begin(c, "empty_set");
+    empty_set_kernel<<<(nv + 63) / 64, 64, 0, c->stream>>>(c->d_tbl_off.p, nv, S, c->table.p);
+    prof_end(c);
+    ScoreArgs sa;
+    sa.gram = c->gram.p;
+    sa.binom = c->d_binom.p;
+    sa.cand = c->d_cand.p;
+    sa.meta = c->d_meta.p;
+    sa.tbl_off = c->d_tbl_off.p;
+    sa.table = c->table.p;
+    sa.N = (double)c->N;
+    sa.lambda = c->lambda;
+    sa.n = n;
+    sa.nv = nv;
+    sa.S = S;
+    const LdsLayout lay = lds_layout(n, nv, S);
+    for (int L = 1; L <= kmax; ++L)
+        for (int ph = 0; ph < 2; ++ph) {
+            const uint64_t *w = &work[((size_t)L * 2 + ph) * (nv + 1)];
+            const uint64_t cnt = w[nv];
+            if (cnt == 0) continue;
+            sa.work = c->d_work.p + ((size_t)L * 2 + ph) * (nv + 1);
+            const uint64_t blocks = (cnt + kBlock - 1) / kBlock;
+            if (blocks > 0x7fffffffull) return set_err(c, ULG_ERR_UNSUPPORTED, "ulg_cbic_score: layer too large");
+            prof_begin(c, kLayerNames[ph][L]);
+            hipLaunchKernelGGL(layer_kernel(L, ph), dim3((unsigned)blocks), dim3(kBlock), (size_t)lay.total, c->stream, sa);
+            prof_end(c);
+        }
+    ULG_HIP(c, hipGetLastError());
+
+    // compaction
+    const int64_t nb = (int64_t)((total_slots + kSlotsPerBlock - 1) / kSlotsPerBlock);
+    if ((rc = ensure(c, c->d_blk, (size_t)nb + 1))) return rc;
+    prof_begin(c, "count_stored");
+    count_kernel<<<(unsigned)nb, kBlock, 0, c->stream>>>(c->table.p, total_slots, c->d_blk.p);
+    prof_end(c);
+    prof_begin(c, "scan_stored");
+    scan_kernel<<<1, 1024, 0, c->stream>>>(c->d_blk.p, nb);
+    prof_end(c);
+    uint64_t stored = 0;
+    ULG_HIP(c, hipMemcpyAsync(&stored, c->d_blk.p + nb, 8, hipMemcpyDeviceToHost, c->stream));
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    if ((rc = ensure(c, c->out_sets, stored)) || (rc = ensure(c, c->out_scores, stored)) ||
+        (rc = ensure(c, c->out_offsets, (size_t)nv + 1)))
+        return rc;
+    WriteArgs wa;
+    wa.table = c->table.p;
+    wa.blk = c->d_blk.p;
+    wa.tbl_off = c->d_tbl_off.p;
+    wa.meta = c->d_meta.p;
+    wa.cand = c->d_cand.p;
+    wa.binom = c->d_binom.p;
+    wa.total = total_slots;
+    wa.nv = nv;
+    wa.S = S;
+    wa.sets = c->out_sets.p;
+    wa.scores = c->out_scores.p;
+    wa.offsets = c->out_offsets.p;
+    prof_begin(c, "write_stored");
+    write_kernel<<<(unsigned)nb, kBlock, 0, c->stream>>>(wa);
+    prof_end(c);
+    set_total_kernel<<<1, 1, 0, c->stream>>>(c->d_blk.p, nb, nv, c->out_offsets.p);
+    ULG_HIP(c, hipGetLastError());
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+
+    c->nv = nv;
+    c->kmax = kmax;
+    c->vars.assign(vars, vars + nv);
+    c->m = mv;
+    c->tbl_off = toff;
+    c->total_slots = (int64_t)total_slots;
+    c->total_stored = (int64_t)stored;
+    c->total_scored = scored;
+    c->scored = true;
+    if (total_stored) *total_stored = (int64_t)stored;
+    if (total_scored) *total_scored = scored;
+    return ULG_OK;
+}
+
+int ulg_cbic_fetch(ulg_ctx *c, uint64_t *sets, float *scores, int64_t *offsets, int device_ptrs) {
+    if (!c) return ULG_ERR_ARG;
+    if (!c->scored) return set_err(c, ULG_ERR_STATE, "ulg_cbic_fetch: nothing scored");
+    ULG_HIP(c, hipSetDevice(c->device));
+    const hipMemcpyKind k = device_ptrs ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    const size_t cnt = (size_t)c->total_stored;
+    if (sets && cnt) ULG_HIP(c, hipMemcpyAsync(sets, c->out_sets.p, cnt * 8, k, c->stream));
+    if (scores && cnt) ULG_HIP(c, hipMemcpyAsync(scores, c->out_scores.p, cnt * 4, k, c->stream));
+    if (offsets) ULG_HIP(c, hipMemcpyAsync(offsets, c->out_offsets.p, (size_t)(c->nv + 1) * 8, k, c->stream));
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    return ULG_OK;
+}
+
+int ulg_cbic_score_vars(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidates, int max_parents,
+                        uint64_t *sets, float *scores, int64_t *offsets, int64_t cap) {
+    int64_t stored = 0;
+    int rc = ulg_cbic_score(c, vars, nv, candidates, max_parents, &stored, nullptr);
+    if (rc) return rc;
+    if (stored > cap) return set_err(c, ULG_ERR_ARG, "ulg_cbic_score_vars: output capacity too small");
+    return ulg_cbic_fetch(c, sets, scores, offsets, 0);
+}
+
+int ulg_quantize_costs(ulg_ctx *c, const float *scores, float *costs, int64_t count) {
+    if (!c || count < 0 || (count > 0 && (!scores || !costs))) return ULG_ERR_ARG;
+    if (count == 0) return ULG_OK;
+    ULG_HIP(c, hipSetDevice(c->device));
+    int rc;
+    if ((rc = ensure(c, c->qbuf_in, (size_t)count)) || (rc = ensure(c, c->qbuf_out, (size_t)count))) return rc;
+    ULG_HIP(c, hipMemcpyAsync(c->qbuf_in.p, scores, (size_t)count * 4, hipMemcpyHostToDevice, c->stream));
+    prof_begin(c, "quantize");
+    quantize_kernel<<<(unsigned)((count + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(c->qbuf_in.p, c->qbuf_out.p,
+                                                                                       count);
+    prof_end(c);
+    ULG_HIP(c, hipMemcpyAsync(costs, c->qbuf_out.p, (size_t)count * 4, hipMemcpyDeviceToHost, c->stream));
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    return ULG_OK;
+}
+
+}  // extern "C"

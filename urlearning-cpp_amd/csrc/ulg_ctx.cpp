@@ -1,0 +1,156 @@
+// ulg_ctx.cpp -- context lifecycle, errors, profiling for libulg.so.
+#include <cstdio>
+#include <cstring>
+
+#include "ulg_internal.h"
+
+namespace ulg {
+
+int set_err(ulg_ctx *c, int code, const std::string &msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+const std::vector<uint32_t> &host_binom() {
+    static std::vector<uint32_t> t = [] {
+        std::vector<uint32_t> b(64 * kBinomK, 0);
+        for (int a = 0; a < 64; ++a)
+            for (int k = 0; k < kBinomK; ++k) {
+                uint64_t v = binom64(a, k);
+                b[a * kBinomK + k] = v > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)v;
+            }
+        return b;
+    }();
+    return t;
+}
+
+uint64_t binom64(int a, int b) {
+    if (b < 0 || b > a) return 0;
+    if (b > a - b) b = a - b;
+    unsigned __int128 r = 1;
+    for (int i = 1; i <= b; ++i) r = r * (unsigned)(a - b + i) / (unsigned)i;
+    return r > ~0ull ? ~0ull : (uint64_t)r;
+}
+
+void prof_begin(ulg_ctx *c, const char *name) {
+    if (!c->prof) return;
+    ProfRec r;
+    r.name = name;
+    (void)hipEventCreate(&r.start);
+    (void)hipEventCreate(&r.stop);
+    (void)hipEventRecord(r.start, c->stream);
+    c->pending.push_back(r);
+}
+
+void prof_end(ulg_ctx *c) {
+    if (!c->prof || c->pending.empty()) return;
+    (void)hipEventRecord(c->pending.back().stop, c->stream);
+}
+
+void prof_collect(ulg_ctx *c) {
+    for (auto &r : c->pending) {
+        float ms = 0.f;
+        if (hipEventSynchronize(r.stop) == hipSuccess && hipEventElapsedTime(&ms, r.start, r.stop) == hipSuccess)
+            c->prof_ms[r.name].push_back(ms);
+        (void)hipEventDestroy(r.start);
+        (void)hipEventDestroy(r.stop);
+    }
+    c->pending.clear();
+}
+
+}  // namespace ulg
+
+using namespace ulg;
+
+extern "C" {
+
+const char *ulg_version(void) { return "ulg 0.1 (HIP, gfx950/CDNA4)"; }
+
+int ulg_create(const int *device_ids, int ndev, ulg_ctx **out) {
+    if (!out) return ULG_ERR_ARG;
+    *out = nullptr;
+    if (ndev != 1 || !device_ids) return ULG_ERR_ARG;
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count <= 0) {
+        fprintf(stderr, "ulg_create: no HIP device available (%s)\n", hipGetErrorString(e));
+        return ULG_ERR_HIP;
+    }
+    if (device_ids[0] < 0 || device_ids[0] >= count) return ULG_ERR_ARG;
+    ulg_ctx *c = new ulg_ctx();
+    c->device = device_ids[0];
+    if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return ULG_ERR_HIP;
+    }
+    const auto &b = host_binom();
+    if (ensure(c, c->d_binom, b.size()) != ULG_OK ||
+        hipMemcpy(c->d_binom.p, b.data(), b.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+        delete c;
+        return ULG_ERR_HIP;
+    }
+    *out = c;
+    return ULG_OK;
+}
+
+void ulg_destroy(ulg_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    prof_collect(c);
+    release(c->raw); release(c->z); release(c->gram); release(c->partials); release(c->colstat);
+    release(c->table); release(c->d_tbl_off); release(c->d_work); release(c->d_blk);
+    release(c->d_cand); release(c->d_meta); release(c->d_binom);
+    release(c->out_sets); release(c->out_scores); release(c->out_offsets);
+    release(c->qbuf_in); release(c->qbuf_out);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char *ulg_last_error(const ulg_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int ulg_profile_enable(ulg_ctx *c, int on) {
+    if (!c) return ULG_ERR_ARG;
+    c->prof = on != 0;
+    return ULG_OK;
+}
+
+int ulg_profile_reset(ulg_ctx *c) {
+    if (!c) return ULG_ERR_ARG;
+    (void)hipStreamSynchronize(c->stream);
+    prof_collect(c);
+    c->prof_ms.clear();
+    return ULG_OK;
+}
+
+int ulg_profile_get(ulg_ctx *c, const char *name, double *avg_ms, int64_t *count, double *total_ms) {
+    if (!c || !name) return ULG_ERR_ARG;
+    (void)hipStreamSynchronize(c->stream);
+    prof_collect(c);
+    auto it = c->prof_ms.find(name);
+    if (it == c->prof_ms.end() || it->second.empty()) return ULG_ERR_ARG;
+    double t = 0;
+    for (double v : it->second) t += v;
+    if (avg_ms) *avg_ms = t / (double)it->second.size();
+    if (count) *count = (int64_t)it->second.size();
+    if (total_ms) *total_ms = t;
+    return ULG_OK;
+}
+
+int ulg_profile_dump(ulg_ctx *c, char *buf, int64_t cap) {
+    if (!c || !buf || cap <= 0) return ULG_ERR_ARG;
+    (void)hipStreamSynchronize(c->stream);
+    prof_collect(c);
+    int64_t len = 0;
+    buf[0] = 0;
+    for (auto &kv : c->prof_ms) {
+        double t = 0;
+        for (double v : kv.second) t += v;
+        int w = snprintf(buf + len, (size_t)(cap - len), "%s %zu %.6f\n", kv.first.c_str(), kv.second.size(), t);
+        if (w < 0 || len + w >= cap) break;
+        len += w;
+    }
+    return ULG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,117 @@
+// ulg_internal.h -- shared host-side state of the MI355X URLearning path.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/ulg.h"
+
+namespace ulg {
+
+constexpr int kMaxVars = 63;               // varset = uint64, bit 63 kept free
+constexpr int kMaxL = ULG_MAX_PARENTS_GPU;  // unrolled layers on the device
+constexpr int kBinomK = kMaxL + 2;          // binomial table columns C(a, 0..kBinomK-1)
+constexpr uint32_t kAbsentBits = 0xFFFFFFFFu;  // "not in the FloatMap" sentinel (a NaN payload)
+
+// Device buffer that only grows.
+template <typename T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t cap = 0;  // elements
+};
+
+struct ProfRec {
+    std::string name;
+    hipEvent_t start, stop;
+};
+
+}  // namespace ulg
+
+struct ulg_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // ---- data (BIC_OLS ctor) ----
+    int n = 0;
+    int64_t N = 0;
+    int npad = 0;
+    double lambda = 0.0;
+    bool loaded = false;
+    ulg::DevBuf<double> raw, z, gram, partials, colstat;
+
+    // ---- scoring state ----
+    int nv = 0;
+    int kmax = 0;
+    std::vector<int> vars;
+    std::vector<int> m;           // candidate count per batch variable
+    std::vector<uint64_t> tbl_off;  // [nv][kmax+2] flattened prefix of table slots
+    int64_t total_slots = 0;
+    int64_t total_stored = 0;
+    int64_t total_scored = 0;
+    bool scored = false;
+    ulg::DevBuf<float> table;
+    ulg::DevBuf<uint64_t> d_tbl_off, d_work, d_blk;
+    ulg::DevBuf<uint8_t> d_cand;  // [nv][64] compact index -> variable
+    ulg::DevBuf<int> d_meta;      // [nv][4]: var, m, var0in, pad
+    ulg::DevBuf<uint32_t> d_binom;
+    ulg::DevBuf<uint64_t> out_sets;
+    ulg::DevBuf<float> out_scores;
+    ulg::DevBuf<int64_t> out_offsets;
+
+    ulg::DevBuf<float> qbuf_in, qbuf_out;
+
+    // ---- profiling ----
+    bool prof = false;
+    std::vector<ulg::ProfRec> pending;
+    std::map<std::string, std::vector<double>> prof_ms;
+};
+
+namespace ulg {
+
+// error helpers -----------------------------------------------------------
+int set_err(ulg_ctx *c, int code, const std::string &msg);
+
+#define ULG_HIP(ctx, expr)                                                          \
+    do {                                                                            \
+        hipError_t e_ = (expr);                                                     \
+        if (e_ != hipSuccess)                                                       \
+            return ::ulg::set_err((ctx), ULG_ERR_HIP,                               \
+                                  std::string(#expr " failed: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+template <typename T>
+int ensure(ulg_ctx *c, DevBuf<T> &b, size_t elems) {
+    if (elems == 0) elems = 1;
+    if (b.cap >= elems) return ULG_OK;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    hipError_t e = hipMalloc(&b.p, elems * sizeof(T));
+    if (e != hipSuccess)
+        return set_err(c, ULG_ERR_HIP, std::string("hipMalloc failed: ") + hipGetErrorString(e));
+    b.cap = elems;
+    return ULG_OK;
+}
+
+template <typename T>
+void release(DevBuf<T> &b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+}
+
+// profiling: bracket a launch with events when enabled
+void prof_begin(ulg_ctx *c, const char *name);
+void prof_end(ulg_ctx *c);
+void prof_collect(ulg_ctx *c);  // after a stream sync
+
+// binomial table C(a, b), a < 64, b < kBinomK, clamped to uint32
+const std::vector<uint32_t> &host_binom();
+uint64_t binom64(int a, int b);
+
+}  // namespace ulg

@@ -1,0 +1,176 @@
+"""ctypes binding of libulg.so (include/ulg.h) -- the HIP hot path.
+
+This module is plumbing for tests, bench.py and scripts: every compute call
+goes through the C ABI into the gfx950 kernels.  There is no CPU fallback:
+if libulg.so is missing, or no HIP device is present, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libulg.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "ulg.h")
+
+_lib = None
+
+
+class ULGError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libulg.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ULGError(f"{LIB_PATH} not built: run __graft_entry__.build() or make -C urlearning-cpp_amd")
+        L = C.CDLL(LIB_PATH)
+        P, I, I64, D, F = C.c_void_p, C.c_int, C.c_int64, C.c_double, C.c_float
+        L.ulg_create.argtypes = [C.POINTER(I), I, C.POINTER(P)]
+        L.ulg_destroy.argtypes = [P]
+        L.ulg_last_error.argtypes = [P]
+        L.ulg_last_error.restype = C.c_char_p
+        L.ulg_version.restype = C.c_char_p
+        L.ulg_cbic_load.argtypes = [P, P, I64, I, D]
+        L.ulg_cbic_gram.argtypes = [P, P]
+        L.ulg_cbic_score.argtypes = [P, P, I, P, I, C.POINTER(I64), C.POINTER(I64)]
+        L.ulg_cbic_fetch.argtypes = [P, P, P, P, I]
+        L.ulg_cbic_score_vars.argtypes = [P, P, I, P, I, P, P, P, I64]
+        L.ulg_quantize_costs.argtypes = [P, P, P, I64]
+        L.ulg_profile_enable.argtypes = [P, I]
+        L.ulg_profile_get.argtypes = [P, C.c_char_p, C.POINTER(D), C.POINTER(I64), C.POINTER(D)]
+        L.ulg_profile_dump.argtypes = [P, C.c_char_p, I64]
+        L.ulg_profile_reset.argtypes = [P]
+        _lib = L
+    return _lib
+
+
+def header_symbols():
+    """Every function the C ABI header declares."""
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(ulg_[a-z0-9_]+)\s*\(", txt)))
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class Context:
+    """One ulg_ctx on one GPU (one process per GPU for multi-GPU work)."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        self._h = C.c_void_p()
+        dev = (C.c_int * 1)(device)
+        rc = L.ulg_create(dev, 1, C.byref(self._h))
+        if rc != 0:
+            raise ULGError(f"ulg_create(device={device}) failed with status {rc}")
+        self.device = device
+        self.n = None
+
+    def close(self):
+        if self._h:
+            lib().ulg_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = lib().ulg_last_error(self._h).decode()
+            raise ULGError(f"{what}: status {rc}: {msg}")
+
+    # ---- cBIC -------------------------------------------------------------
+    def load(self, data: np.ndarray, lam: float):
+        """data: N x n array (rows = records).  Stored column-major."""
+        x = np.asfortranarray(np.asarray(data, dtype=np.float64))
+        N, n = x.shape
+        flat = np.ascontiguousarray(x.T.reshape(-1))  # column-major flatten
+        self._check(lib().ulg_cbic_load(self._h, _ptr(flat), N, n, float(lam)), "ulg_cbic_load")
+        self.n = n
+        self.N = N
+
+    def gram(self) -> np.ndarray:
+        g = np.empty((self.n, self.n), dtype=np.float64)
+        self._check(lib().ulg_cbic_gram(self._h, _ptr(g)), "ulg_cbic_gram")
+        return g
+
+    def score(self, variables, candidates, max_parents: int):
+        """Returns (total_stored, total_scored); results stay on the GPU."""
+        v = np.ascontiguousarray(variables, dtype=np.int32)
+        c = np.ascontiguousarray(candidates, dtype=np.uint64)
+        st, sc = C.c_int64(), C.c_int64()
+        self._check(lib().ulg_cbic_score(self._h, _ptr(v), len(v), _ptr(c), int(max_parents),
+                                         C.byref(st), C.byref(sc)), "ulg_cbic_score")
+        self._nv = len(v)
+        return st.value, sc.value
+
+    def fetch(self, total_stored: int):
+        sets = np.empty(max(total_stored, 1), dtype=np.uint64)
+        scores = np.empty(max(total_stored, 1), dtype=np.float32)
+        offs = np.empty(self._nv + 1, dtype=np.int64)
+        self._check(lib().ulg_cbic_fetch(self._h, _ptr(sets), _ptr(scores), _ptr(offs), 0), "ulg_cbic_fetch")
+        return offs, sets[:total_stored], scores[:total_stored]
+
+    def fetch_device(self, sets_ptr: int, scores_ptr: int, offsets_ptr: int):
+        """Copy results into caller-owned device buffers (e.g. torch tensors)."""
+        self._check(lib().ulg_cbic_fetch(self._h, C.c_void_p(sets_ptr), C.c_void_p(scores_ptr),
+                                         C.c_void_p(offsets_ptr), 1), "ulg_cbic_fetch")
+
+    def score_all(self, variables, candidates, max_parents: int):
+        st, _ = self.score(variables, candidates, max_parents)
+        return self.fetch(st)
+
+    def quantize(self, scores: np.ndarray) -> np.ndarray:
+        s = np.ascontiguousarray(scores, dtype=np.float32)
+        out = np.empty_like(s)
+        self._check(lib().ulg_quantize_costs(self._h, _ptr(s), _ptr(out), s.size), "ulg_quantize_costs")
+        return out
+
+    # ---- profiling ----------------------------------------------------------
+    def profile(self, on: bool = True):
+        self._check(lib().ulg_profile_enable(self._h, 1 if on else 0), "ulg_profile_enable")
+
+    def profile_reset(self):
+        self._check(lib().ulg_profile_reset(self._h), "ulg_profile_reset")
+
+    def profile_get(self, name: str):
+        avg, tot = C.c_double(), C.c_double()
+        cnt = C.c_int64()
+        rc = lib().ulg_profile_get(self._h, name.encode(), C.byref(avg), C.byref(cnt), C.byref(tot))
+        if rc != 0:
+            return None
+        return {"avg_ms": avg.value, "count": cnt.value, "total_ms": tot.value}
+
+    def profile_dump(self) -> dict:
+        buf = C.create_string_buffer(1 << 16)
+        self._check(lib().ulg_profile_dump(self._h, buf, len(buf)), "ulg_profile_dump")
+        out = {}
+        for line in buf.value.decode().splitlines():
+            name, cnt, tot = line.split()
+            out[name] = {"count": int(cnt), "total_ms": float(tot)}
+        return out
+
+
+def candidates_from_edges(edges, n: int):
+    """2-hop candidate sets N(v) U N(N(v)) (score_main.cpp:146-153)."""
+    allm = (1 << n) - 1
+    if edges is None:
+        return [allm] * n
+    out = []
+    for v in range(n):
+        nb = int(edges[v])
+        for j in range(n):
+            if (int(edges[v]) >> j) & 1 and j != v:
+                nb |= int(edges[j])
+        out.append(nb)
+    return out
