@@ -102,6 +102,45 @@ int ulg_cbic_score_vars(ulg_ctx *ctx, const int *vars, int nv,
 int ulg_quantize_costs(ulg_ctx *ctx, const float *scores, float *costs,
                        int64_t count);
 
+/* ---- search side (best-score tables, pattern database, A*) ------------ */
+/* Load per-variable parent-set lists (file order within each variable;
+ * costs = A* costs, i.e. -1 * atof(score), score_cache.cpp:151) and build
+ * the best-score lattice tables on the device.  Duplicate sets within a
+ * variable must already be merged (ScoreCache::putScore semantics). */
+int ulg_search_load(ulg_ctx *ctx, int n, const int64_t *offsets,
+                    const uint64_t *sets, const float *costs);
+/* Same from the lists the last ulg_cbic_score produced in this context
+ * (every variable must have been scored); costs go through the device
+ * "%f" round trip (ulg_quantize_costs), lists stay on the device. */
+int ulg_search_from_scores(ulg_ctx *ctx);
+/* SparseParentList::getScore / getParents for count (variable, S) pairs:
+ * the cost of the first (cost, file-order) stored set that is a subset of
+ * S, or FLT_MAX if none; parents[i] gets that set (0 if none). */
+int ulg_bestscore_query(ulg_ctx *ctx, int64_t count, const int *vars,
+                        const uint64_t *S, float *costs, uint64_t *parents);
+/* StaticPatternDatabase with pd_count groups over scc (and ancestors);
+ * static_pattern_database.cpp:82-247.  astar() builds it over all
+ * variables with no ancestors. */
+int ulg_pdb_build(ulg_ctx *ctx, int pd_count, uint64_t ancestors,
+                  uint64_t scc);
+/* StaticPatternDatabase::h for count subnetworks S. */
+int ulg_pdb_query(ulg_ctx *ctx, int64_t count, const uint64_t *S, float *h,
+                  int *complete);
+
+#define ULG_ASTAR_EXACT 0 /* the reference's pop order: bit-exact DAG */
+#define ULG_ASTAR_GPU 1   /* layer-synchronous GPU order-graph search */
+/* astar() (astar_main.cpp:548-644): static PDB(pd_count) over all
+ * variables, one search per connected component of the skeleton
+ * (edges = n skeleton rows, bit j of row i = edge i-j, or NULL for no
+ * skeleton).  Outputs what netFile.csv holds -- vpar[v] = parent set of v
+ * (bit i set iff i -> v) -- the total ordering, the goal cost (g of the
+ * goal node) and the number of expanded nodes; net_text (if non-NULL)
+ * receives the netFile text.  Components are processed in order and each
+ * overwrites the outputs, as the reference does. */
+int ulg_astar(ulg_ctx *ctx, const uint64_t *edges, int pd_count, int mode,
+              uint64_t *vpar, int *order, float *goal_cost, int64_t *expanded,
+              char *net_text, int64_t net_cap);
+
 /* ---- profiling (per-kernel HIP-event timing on the context stream) ---- */
 int ulg_profile_enable(ulg_ctx *ctx, int on);
 /* Average duration (ms) and launch count of kernels whose name matches

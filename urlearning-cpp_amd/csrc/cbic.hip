@@ -24,7 +24,7 @@
 #include <cmath>
 #include <cstring>
 
-#include "ulg_internal.h"
+#include "search_internal.h"
 
 using namespace ulg;
 
@@ -539,42 +539,9 @@ __global__ void set_total_kernel(const uint64_t *blk, int64_t nb, int nv, int64_
     offsets[nv] = (int64_t)blk[nb];
 }
 
-// ---- "%f" + atof round trip (score_main.cpp:191 / score_cache.cpp:151) -----
-// D = round-half-even(|x| * 10^6) exactly in integers (glibc printf is exact
-// with ties to even); strtod of D/10^6 is the correctly rounded double
-// quotient; cost = float(-1 * that).
-__device__ __forceinline__ float quantize_one(float x) {
-    const uint32_t u = __float_as_uint(x);
-    const uint32_t ex = (u >> 23) & 0xffu;
-    const bool neg = (u >> 31) != 0;
-    if (ex == 0xffu) return -x;  // inf -> -inf, nan stays nan
-    uint64_t M;
-    int E;
-    if (ex == 0) { M = u & 0x7fffffu; E = -149; }
-    else { M = (u & 0x7fffffu) | 0x800000u; E = (int)ex - 150; }
-    double mag;
-    if (E >= 0) {
-        mag = (double)fabsf(x);  // x * 10^6 is an integer: printed exactly
-    } else {
-        const int sh = -E;
-        const uint64_t num = M * 1000000ull;  // < 2^44
-        uint64_t D;
-        if (sh >= 64) D = 0;
-        else {
-            D = num >> sh;
-            const uint64_t rem = num & ((1ull << sh) - 1ull);
-            const uint64_t half = 1ull << (sh - 1);
-            if (rem > half || (rem == half && (D & 1ull))) ++D;
-        }
-        mag = (double)D / 1000000.0;
-    }
-    const double val = neg ? -mag : mag;
-    return (float)(-1.0 * val);
-}
-
 __global__ void quantize_kernel(const float *in, float *out, int64_t count) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < count) out[i] = quantize_one(in[i]);
+    if (i < count) out[i] = quantize_score(in[i]);
 }
 
 using KernelFn = void (*)(ScoreArgs);

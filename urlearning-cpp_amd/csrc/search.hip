@@ -1,0 +1,429 @@
+// search.hip -- best-score lattice tables and the static pattern database on
+// MI355X, plus the device queries the search uses.
+//
+// Reference path (urlearning/):
+//   SparseParentList::initialize/getScore  score_cache/sparse_parent_list.cpp:20-55
+//   StaticPatternDatabase                  heuristic/static_pattern_database.cpp:82-247
+//
+// BestScore table (replaces the sorted-list linear scan): for variable v with
+// parent-set support D_v (union of its stored sets, m_v = |D_v|), a dense
+// table over all 2^m_v subsets S of D_v holds
+//     key(S) = min over stored sets P subset of S of (ordered(cost_P) << 32 | file_index_P)
+// i.e. exactly the first entry of the list sorted by (cost, file order) that
+// is a subset of S (SparseParentList with the pinned N7 tie-break).  It is
+// filled by a scatter of the stored sets and an in-place subset-min ("zeta")
+// transform: bits 0..13 inside 128 KiB LDS tiles, the remaining bits in a
+// second pass over strided tiles whose rows are 16 contiguous entries.  Both
+// passes stream the table once (HBM-bound).  Lookup: key = T_v[pext(S, D_v)].
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+
+#include "search_internal.h"
+
+using namespace ulg;
+
+namespace {
+
+constexpr int kB = 256;
+constexpr int kTileBits = 14;  // pass A: 2^14 u64 = 128 KiB LDS
+constexpr int kRowBits = 4;    // pass B rows: 16 contiguous u64 = 128 B
+constexpr int kColBits = 10;   // pass B: 2^10 rows x 16 = 2^14 u64
+
+__global__ void __launch_bounds__(kB) support_kernel(const uint64_t *sets, const int64_t *offsets, int n,
+                                                     unsigned long long *support) {
+    const int v = blockIdx.y;
+    const int64_t b = offsets[v], e = offsets[v + 1];
+    uint64_t acc = 0;
+    for (int64_t i = b + (int64_t)blockIdx.x * kB + threadIdx.x; i < e; i += (int64_t)gridDim.x * kB) acc |= sets[i];
+    // wave OR-reduction then one atomic per wave
+    for (int off = 32; off > 0; off >>= 1) acc |= __shfl_xor(acc, off);
+    if ((threadIdx.x & 63) == 0 && acc) atomicOr(&support[v], (unsigned long long)acc);
+}
+
+__global__ void __launch_bounds__(kB) scatter_kernel(const uint64_t *sets, const float *costs, const int64_t *offsets,
+                                                     int n, const uint64_t *support, const uint64_t *tb_off,
+                                                     uint64_t *table) {
+    const int v = blockIdx.y;
+    const int64_t b = offsets[v], e = offsets[v + 1];
+    const uint64_t D = support[v];
+    for (int64_t i = b + (int64_t)blockIdx.x * kB + threadIdx.x; i < e; i += (int64_t)gridDim.x * kB) {
+        const uint64_t idx = pext64(sets[i], D);
+        table[tb_off[v] + idx] = ((uint64_t)ordkey(costs[i]) << 32) | (uint64_t)(i - b);
+    }
+}
+
+// pass A: all subset bits inside a contiguous tile of 2^T entries.
+__global__ void __launch_bounds__(1024) zeta_tile_kernel(uint64_t *table, const uint64_t *tb_off, const int *tiles_prefix,
+                                                         const int *mbits, int nvar) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t *t = reinterpret_cast<uint64_t *>(smem);
+    // which variable / tile
+    int lo = 0, hi = nvar;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (tiles_prefix[mid] <= (int)blockIdx.x) lo = mid; else hi = mid;
+    }
+    const int v = lo;
+    const int m = mbits[v];
+    const int T = m < kTileBits ? m : kTileBits;
+    const uint64_t size = 1ull << T;
+    const uint64_t base = tb_off[v] + ((uint64_t)(blockIdx.x - tiles_prefix[v]) << T);
+    for (uint64_t i = threadIdx.x; i < size; i += 1024) t[i] = table[base + i];
+    __syncthreads();
+    for (int b = 0; b < T; ++b) {
+        const uint64_t bit = 1ull << b;
+        for (uint64_t p = threadIdx.x; p < (size >> 1); p += 1024) {
+            const uint64_t i = ((p >> b) << (b + 1)) | (p & (bit - 1));
+            const uint64_t a = t[i], c = t[i | bit];
+            if (a < c) t[i | bit] = a;
+        }
+        __syncthreads();
+    }
+    for (uint64_t i = threadIdx.x; i < size; i += 1024) table[base + i] = t[i];
+}
+
+// pass B: bits [bit_lo, bit_lo + G) over tiles of 2^G rows x 16 contiguous entries.
+struct ZetaBArgs {
+    uint64_t *table;
+    const uint64_t *tb_off;
+    const int *blocks_prefix;
+    const int *mbits;
+    int nvar;
+    int bit_lo;
+};
+__global__ void __launch_bounds__(1024) zeta_strided_kernel(ZetaBArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t *t = reinterpret_cast<uint64_t *>(smem);
+    int lo = 0, hi = a.nvar;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (a.blocks_prefix[mid] <= (int)blockIdx.x) lo = mid; else hi = mid;
+    }
+    const int v = lo;
+    const int m = a.mbits[v];
+    const int bit_lo = a.bit_lo;
+    const int G = std::min(kColBits, m - bit_lo);
+    const int nlow = bit_lo - kRowBits;
+    const uint64_t bid = blockIdx.x - a.blocks_prefix[v];
+    const uint64_t base = a.tb_off[v] + (((bid & ((1ull << nlow) - 1)) << kRowBits) | ((bid >> nlow) << (bit_lo + G)));
+    const int rows = 1 << G;
+    const int size = rows << kRowBits;
+    for (int e = threadIdx.x; e < size; e += 1024) {
+        const uint64_t hc = (uint64_t)(e >> kRowBits), lw = (uint64_t)(e & 15);
+        t[e] = a.table[base | (hc << bit_lo) | lw];
+    }
+    __syncthreads();
+    for (int j = 0; j < G; ++j) {
+        for (int p = threadIdx.x; p < (size >> 1); p += 1024) {
+            const int lw = p & 15, q = p >> 4;  // q indexes rows with bit j clear
+            const int r0 = ((q >> j) << (j + 1)) | (q & ((1 << j) - 1));
+            const int i0 = (r0 << kRowBits) | lw, i1 = ((r0 | (1 << j)) << kRowBits) | lw;
+            const uint64_t x = t[i0], y = t[i1];
+            if (x < y) t[i1] = x;
+        }
+        __syncthreads();
+    }
+    for (int e = threadIdx.x; e < size; e += 1024) {
+        const uint64_t hc = (uint64_t)(e >> kRowBits), lw = (uint64_t)(e & 15);
+        a.table[base | (hc << bit_lo) | lw] = t[e];
+    }
+}
+
+__global__ void __launch_bounds__(kB) cost_table_kernel(const uint64_t *table, uint64_t total, float *costs) {
+    const uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x;
+    if (i < total) costs[i] = key_cost(table[i]);
+}
+
+__global__ void __launch_bounds__(kB) query_kernel(SearchDev d, int64_t count, const int *vars, const uint64_t *S,
+                                                   float *costs, uint64_t *parents) {
+    const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (i >= count) return;
+    const int v = vars[i];
+    const uint64_t key = bs_key(d, v, S[i]);
+    costs[i] = key_cost(key);
+    parents[i] = (key == ~0ull) ? 0ull : d.sets[d.offsets[v] + (int64_t)(key & 0xffffffffull)];
+}
+
+__global__ void quantize_lists_kernel(const float *scores, float *costs, int64_t count) {
+    const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (i < count) costs[i] = quantize_score(scores[i]);
+}
+
+// ---- static pattern database ------------------------------------------------
+struct PdbBsArgs {
+    SearchDev d;
+    uint64_t group;
+    int s;
+    const int *bitpos;  // s entries
+    uint64_t scc, anc;
+    float *bsv;         // [2^s][s]
+};
+// bsv[R][j] = getScore(leaf = bitpos[j], (scc \ (R \ {leaf})) | ancestors) for leaf in R
+__global__ void __launch_bounds__(kB) pdb_bs_kernel(PdbBsArgs a) {
+    const uint64_t p = (uint64_t)blockIdx.x * kB + threadIdx.x;
+    const int s = a.s;
+    if (p >= ((uint64_t)s << (s - 1))) return;
+    const int j = (int)(p >> (s - 1));
+    const uint64_t rr = p & ((1ull << (s - 1)) - 1ull);
+    const uint64_t R = ((rr >> j) << (j + 1)) | (1ull << j) | (rr & ((1ull << j) - 1ull));
+    uint64_t Rg = 0;
+    for (int t = 0; t < s; ++t)
+        if ((R >> t) & 1ull) Rg |= 1ull << a.bitpos[t];
+    const int leaf = a.bitpos[j];
+    const uint64_t removed = Rg & ~(1ull << leaf);
+    const uint64_t choices = (a.scc & ~removed) | a.anc;
+    a.bsv[R * s + j] = key_cost(bs_key(a.d, leaf, choices));
+}
+
+// one layer of the reverse BFS (static_pattern_database.cpp:184-207):
+// pd[R] = fold over leaves l in R (descending, the oracle's key order) of
+//         newG = bs(l, ...) + pd[R \ l], kept if oldG == 0 || newG < oldG.
+__global__ void __launch_bounds__(kB) pdb_layer_kernel(const float *bsv, int s, int layer, float *pd) {
+    const uint64_t R = (uint64_t)blockIdx.x * kB + threadIdx.x;
+    if (R >= (1ull << s) || __popcll(R) != layer) return;
+    float cur = 0.0f;
+    for (int j = s - 1; j >= 0; --j) {
+        if (!((R >> j) & 1ull)) continue;
+        const float newG = bsv[R * s + j] + pd[R ^ (1ull << j)];
+        if (cur == 0 || newG < cur) cur = newG;
+    }
+    pd[R] = cur;
+}
+
+__global__ void __launch_bounds__(kB) pdb_query_kernel(SearchDev d, int64_t count, const uint64_t *S, float *h,
+                                                       int *complete) {
+    const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (i >= count) return;
+    int c = 0;
+    h[i] = pdb_h(d, S[i], &c);
+    complete[i] = c;
+}
+
+}  // namespace
+
+namespace ulg {
+
+int search_build_tables(ulg_ctx *c) {
+    SearchState &s = *c->search;
+    const int n = s.n;
+    int rc;
+    // support D_v
+    if ((rc = ensure(c, s.d_support, (size_t)n))) return rc;
+    ULG_HIP(c, hipMemsetAsync(s.d_support.p, 0, (size_t)n * 8, c->stream));
+    int64_t maxcnt = 1;
+    for (int v = 0; v < n; ++v) maxcnt = std::max<int64_t>(maxcnt, s.offsets[v + 1] - s.offsets[v]);
+    const unsigned gx = (unsigned)std::min<int64_t>((maxcnt + kB - 1) / kB, 4096);
+    prof_begin(c, "bs_support");
+    support_kernel<<<dim3(gx, n), kB, 0, c->stream>>>(s.d_sets.p, s.d_offsets.p, n,
+                                                     reinterpret_cast<unsigned long long *>(s.d_support.p));
+    prof_end(c);
+    s.support.assign(n, 0);
+    ULG_HIP(c, hipMemcpyAsync(s.support.data(), s.d_support.p, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    s.mbits.assign(n, 0);
+    s.tb_off.assign(n + 1, 0);
+    for (int v = 0; v < n; ++v) {
+        s.mbits[v] = __builtin_popcountll(s.support[v]);
+        s.tb_off[v + 1] = s.tb_off[v] + (1ull << s.mbits[v]);
+    }
+    const uint64_t total = s.tb_off[n];
+    s.table_entries = total;
+    if ((rc = ensure(c, s.d_table, total)) || (rc = ensure(c, s.d_tb_off, (size_t)n + 1)) ||
+        (rc = ensure(c, s.d_mbits, (size_t)n)))
+        return rc;
+    ULG_HIP(c, hipMemcpyAsync(s.d_tb_off.p, s.tb_off.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    ULG_HIP(c, hipMemcpyAsync(s.d_mbits.p, s.mbits.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+    prof_begin(c, "bs_fill");
+    ULG_HIP(c, hipMemsetAsync(s.d_table.p, 0xff, total * 8, c->stream));
+    prof_end(c);
+    prof_begin(c, "bs_scatter");
+    scatter_kernel<<<dim3(gx, n), kB, 0, c->stream>>>(s.d_sets.p, s.d_costs.p, s.d_offsets.p, n, s.d_support.p,
+                                                     s.d_tb_off.p, s.d_table.p);
+    prof_end(c);
+    // pass A tiles
+    std::vector<int> tiles_prefix(n + 1, 0), blocks_prefix(n + 1, 0);
+    for (int v = 0; v < n; ++v) {
+        const int m = s.mbits[v];
+        tiles_prefix[v + 1] = tiles_prefix[v] + (m <= kTileBits ? 1 : (1 << (m - kTileBits)));
+    }
+    if ((rc = ensure(c, s.d_prefix, (size_t)2 * (n + 1)))) return rc;
+    ULG_HIP(c, hipMemcpyAsync(s.d_prefix.p, tiles_prefix.data(), (size_t)(n + 1) * 4, hipMemcpyHostToDevice, c->stream));
+    const int maxm = *std::max_element(s.mbits.begin(), s.mbits.end());
+    const size_t ldsA = (size_t)8 << std::min(maxm, kTileBits);
+    ULG_HIP(c, hipFuncSetAttribute((const void *)zeta_tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(8 << kTileBits)));
+    prof_begin(c, "bs_zeta_tile");
+    zeta_tile_kernel<<<tiles_prefix[n], 1024, ldsA, c->stream>>>(s.d_table.p, s.d_tb_off.p, s.d_prefix.p, s.d_mbits.p, n);
+    prof_end(c);
+    ULG_HIP(c, hipGetLastError());
+    // pass B over the remaining high bits, kColBits at a time
+    ULG_HIP(c, hipFuncSetAttribute((const void *)zeta_strided_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(8 << (kColBits + kRowBits))));
+    for (int bit_lo = kTileBits; bit_lo < maxm; bit_lo += kColBits) {
+        std::fill(blocks_prefix.begin(), blocks_prefix.end(), 0);
+        for (int v = 0; v < n; ++v) {
+            const int m = s.mbits[v];
+            int nb = 0;
+            if (m > bit_lo) nb = 1 << (m - kRowBits - std::min(kColBits, m - bit_lo));
+            blocks_prefix[v + 1] = blocks_prefix[v] + nb;
+        }
+        if (blocks_prefix[n] == 0) break;
+        ULG_HIP(c, hipMemcpyAsync(s.d_prefix.p + (n + 1), blocks_prefix.data(), (size_t)(n + 1) * 4, hipMemcpyHostToDevice, c->stream));
+        ZetaBArgs za{s.d_table.p, s.d_tb_off.p, s.d_prefix.p + (n + 1), s.d_mbits.p, n, bit_lo};
+        const int G = std::min(kColBits, maxm - bit_lo);
+        prof_begin(c, "bs_zeta_strided");
+        zeta_strided_kernel<<<blocks_prefix[n], 1024, (size_t)8 << (G + kRowBits), c->stream>>>(za);
+        prof_end(c);
+        ULG_HIP(c, hipGetLastError());
+        // host copy of blocks_prefix must stay valid until the copy ran
+        ULG_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    s.tables_ready = true;
+    s.pdb_ready = false;
+    return ULG_OK;
+}
+
+int search_build_pdb(ulg_ctx *c, int pd_count, uint64_t ancestors, uint64_t scc) {
+    SearchState &s = *c->search;
+    if (!s.tables_ready) return set_err(c, ULG_ERR_STATE, "pattern database needs the best-score tables");
+    if (pd_count < 1 || pd_count > kMaxGroups) return set_err(c, ULG_ERR_ARG, "pd_count must be 1..8");
+    // groups: consecutive scc variables, ceil(|scc| / pd_count) each (static_pattern_database.cpp:95-120)
+    s.groups.clear();
+    const int remaining = __builtin_popcountll(scc);
+    const int pds = (int)std::ceil((float)remaining / pd_count);
+    int var = scc ? __builtin_ctzll(scc) : -1;
+    int x = 0;
+    for (int g = 0; g < pd_count; ++g) {
+        uint64_t grp = 0;
+        int sz;
+        for (sz = 0; sz < pds && x < remaining; ++sz) {
+            grp |= 1ull << var;
+            const uint64_t rest = (var + 1 < 64) ? (scc >> (var + 1)) : 0;
+            var = var + (rest ? (__builtin_ctzll(rest) + 1) : 0);
+            ++x;
+        }
+        s.groups.push_back(grp);
+    }
+    if (ancestors & scc) return set_err(c, ULG_ERR_UNSUPPORTED, "ancestors overlapping the search variables");
+    s.ancestors = ancestors;
+    s.scc = scc;
+    int rc;
+    size_t total = 0, maxbsv = 1;
+    s.pd_off.assign(pd_count + 1, 0);
+    for (int g = 0; g < pd_count; ++g) {
+        const int sz = __builtin_popcountll(s.groups[g]);
+        if (sz > 24) return set_err(c, ULG_ERR_UNSUPPORTED, "pattern-database group larger than 24 variables");
+        s.pd_off[g + 1] = s.pd_off[g] + (1ull << sz);
+        maxbsv = std::max(maxbsv, (size_t)sz << sz);
+    }
+    total = s.pd_off[pd_count];
+    if ((rc = ensure(c, s.d_pd, total)) || (rc = ensure(c, s.d_bsv, maxbsv)) || (rc = ensure(c, s.d_bitpos, 64)))
+        return rc;
+    ULG_HIP(c, hipMemsetAsync(s.d_pd.p, 0, total * 4, c->stream));
+    const SearchDev d = s.dev();
+    for (int g = 0; g < pd_count; ++g) {
+        const uint64_t grp = s.groups[g];
+        const int sz = __builtin_popcountll(grp);
+        if (sz == 0) continue;
+        std::vector<int> bitpos;
+        for (int b = 0; b < 64; ++b)
+            if ((grp >> b) & 1ull) bitpos.push_back(b);
+        ULG_HIP(c, hipMemcpyAsync(s.d_bitpos.p, bitpos.data(), bitpos.size() * 4, hipMemcpyHostToDevice, c->stream));
+        PdbBsArgs a{d, grp, sz, s.d_bitpos.p, scc, ancestors, s.d_bsv.p};
+        const uint64_t work = (uint64_t)sz << (sz - 1);
+        prof_begin(c, "pdb_bs");
+        pdb_bs_kernel<<<(unsigned)((work + kB - 1) / kB), kB, 0, c->stream>>>(a);
+        prof_end(c);
+        float *pd = s.d_pd.p + s.pd_off[g];
+        for (int layer = 1; layer <= sz; ++layer) {
+            prof_begin(c, "pdb_layer");
+            pdb_layer_kernel<<<(unsigned)(((1ull << sz) + kB - 1) / kB), kB, 0, c->stream>>>(s.d_bsv.p, sz, layer, pd);
+            prof_end(c);
+        }
+        ULG_HIP(c, hipStreamSynchronize(c->stream));  // bitpos / bsv reused by the next group
+    }
+    ULG_HIP(c, hipGetLastError());
+    // host copies (small) for the exact-order search and the group table for device h
+    s.pd_host.resize(total);
+    ULG_HIP(c, hipMemcpyAsync(s.pd_host.data(), s.d_pd.p, total * 4, hipMemcpyDeviceToHost, c->stream));
+    std::vector<uint64_t> gmeta(2 * kMaxGroups, 0);
+    for (int g = 0; g < pd_count; ++g) {
+        gmeta[g] = s.groups[g];
+        gmeta[kMaxGroups + g] = s.pd_off[g];
+    }
+    if ((rc = ensure(c, s.d_groups, gmeta.size()))) return rc;
+    ULG_HIP(c, hipMemcpyAsync(s.d_groups.p, gmeta.data(), gmeta.size() * 8, hipMemcpyHostToDevice, c->stream));
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    s.pd_count = pd_count;
+    s.pdb_ready = true;
+    return ULG_OK;
+}
+
+int search_quantize_device(ulg_ctx *c, const float *d_scores, float *d_costs, int64_t count) {
+    if (count <= 0) return ULG_OK;
+    prof_begin(c, "quantize_lists");
+    quantize_lists_kernel<<<(unsigned)((count + kB - 1) / kB), kB, 0, c->stream>>>(d_scores, d_costs, count);
+    prof_end(c);
+    ULG_HIP(c, hipGetLastError());
+    return ULG_OK;
+}
+
+int search_cost_table_host(ulg_ctx *c) {
+    SearchState &s = *c->search;
+    if (s.host_costs_ready) return ULG_OK;
+    const uint64_t total = s.table_entries;
+    int rc;
+    if ((rc = ensure(c, s.d_cost_table, total))) return rc;
+    prof_begin(c, "bs_cost_table");
+    cost_table_kernel<<<(unsigned)((total + kB - 1) / kB), kB, 0, c->stream>>>(s.d_table.p, total, s.d_cost_table.p);
+    prof_end(c);
+    if (s.host_cost_cap < total) {
+        if (s.host_costs) (void)hipHostFree(s.host_costs);
+        s.host_costs = nullptr;
+        ULG_HIP(c, hipHostMalloc((void **)&s.host_costs, total * 4, hipHostMallocDefault));
+        s.host_cost_cap = total;
+    }
+    ULG_HIP(c, hipMemcpyAsync(s.host_costs, s.d_cost_table.p, total * 4, hipMemcpyDeviceToHost, c->stream));
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    s.host_costs_ready = true;
+    return ULG_OK;
+}
+
+int search_query(ulg_ctx *c, int64_t count, const int *vars, const uint64_t *S, float *costs, uint64_t *parents) {
+    SearchState &s = *c->search;
+    int rc;
+    if ((rc = ensure(c, s.q_vars, (size_t)count)) || (rc = ensure(c, s.q_sets, (size_t)count)) ||
+        (rc = ensure(c, s.q_costs, (size_t)count)) || (rc = ensure(c, s.q_par, (size_t)count)))
+        return rc;
+    ULG_HIP(c, hipMemcpyAsync(s.q_vars.p, vars, (size_t)count * 4, hipMemcpyHostToDevice, c->stream));
+    ULG_HIP(c, hipMemcpyAsync(s.q_sets.p, S, (size_t)count * 8, hipMemcpyHostToDevice, c->stream));
+    query_kernel<<<(unsigned)((count + kB - 1) / kB), kB, 0, c->stream>>>(s.dev(), count, s.q_vars.p, s.q_sets.p,
+                                                                       s.q_costs.p, s.q_par.p);
+    ULG_HIP(c, hipGetLastError());
+    if (costs) ULG_HIP(c, hipMemcpyAsync(costs, s.q_costs.p, (size_t)count * 4, hipMemcpyDeviceToHost, c->stream));
+    if (parents) ULG_HIP(c, hipMemcpyAsync(parents, s.q_par.p, (size_t)count * 8, hipMemcpyDeviceToHost, c->stream));
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    return ULG_OK;
+}
+
+int search_pdb_query(ulg_ctx *c, int64_t count, const uint64_t *S, float *h, int *complete) {
+    SearchState &s = *c->search;
+    int rc;
+    if ((rc = ensure(c, s.q_sets, (size_t)count)) || (rc = ensure(c, s.q_costs, (size_t)count)) ||
+        (rc = ensure(c, s.q_vars, (size_t)count)))
+        return rc;
+    ULG_HIP(c, hipMemcpyAsync(s.q_sets.p, S, (size_t)count * 8, hipMemcpyHostToDevice, c->stream));
+    pdb_query_kernel<<<(unsigned)((count + kB - 1) / kB), kB, 0, c->stream>>>(s.dev(), count, s.q_sets.p, s.q_costs.p,
+                                                                           s.q_vars.p);
+    ULG_HIP(c, hipGetLastError());
+    ULG_HIP(c, hipMemcpyAsync(h, s.q_costs.p, (size_t)count * 4, hipMemcpyDeviceToHost, c->stream));
+    if (complete) ULG_HIP(c, hipMemcpyAsync(complete, s.q_vars.p, (size_t)count * 4, hipMemcpyDeviceToHost, c->stream));
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    return ULG_OK;
+}
+
+}  // namespace ulg

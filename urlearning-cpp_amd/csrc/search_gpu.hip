@@ -1,0 +1,271 @@
+// search_gpu.hip -- order-graph search on the GPU (ULG_ASTAR_GPU).
+//
+// The order graph of run_astar_on_one_scc (astar/astar_main.cpp:216-546) is
+// layered by |S|: every edge S -> S u {leaf} goes from layer d to d+1 with
+// cost getScore(leaf, S) (the reference adds it as g(u) + leaf_score, :327).
+// Instead of a priority queue the GPU sweeps the layers: layer d+1 is one
+// launch in which every node T "pulls" its cost from the d+1 predecessors
+// T \ {leaf} of layer d (colex-indexed dense layers, no hashing, no atomics):
+//     g(T) = min_leaf fl(g(T \ leaf) + bs(leaf, T \ leaf)),   leaf(T) = argmin
+// subject to the reference's skeleton filter (a leaf may only follow a
+// non-empty set that contains one of its neighbours, astar_main.cpp:305-313).
+// That is the same shortest-path problem A* solves, so the goal cost is the
+// optimal order cost; every node of the component is expanded once, which
+// makes this the expansions/s path.  The DAG it returns is an optimal one
+// (Markov equivalent to the exact-order result when the optimum is unique up
+// to equivalence); the bit-exact reference DAG is ULG_ASTAR_EXACT's job.
+#include <algorithm>
+#include <cfloat>
+#include <cstring>
+
+#include "search_internal.h"
+
+using namespace ulg;
+
+namespace {
+
+constexpr int kB = 256;
+constexpr int kMaxM = 32;  // nodes of a searched component (2^32 nodes is already 4 GB of leaf bytes)
+
+struct LayerArgs {
+    SearchDev d;
+    const uint64_t *binom;   // [33][33] C(a, b)
+    const int *comp_vars;    // compact bit -> variable
+    const uint64_t *edges;   // skeleton rows (may be null)
+    int skeleton;            // apply the neighbour filter
+    int m;                   // component size
+    int layer;               // layer of the nodes computed by this launch (>= 1)
+    uint64_t count;          // C(m, layer)
+    const float *gprev;      // layer - 1
+    float *gcur;             // layer
+    uint8_t *leaf;           // leaf bytes of this layer
+};
+
+__device__ __forceinline__ uint64_t Bn(const uint64_t *b, int a, int k) { return b[a * 33 + k]; }
+
+__global__ void __launch_bounds__(kB) layer_pull_kernel(LayerArgs a) {
+    __shared__ uint64_t binom[33 * 33];
+    __shared__ int cv[kMaxM];
+    for (int i = threadIdx.x; i < 33 * 33; i += kB) binom[i] = a.binom[i];
+    for (int i = threadIdx.x; i < a.m; i += kB) cv[i] = a.comp_vars[i];
+    __syncthreads();
+    const uint64_t r = (uint64_t)blockIdx.x * kB + threadIdx.x;
+    if (r >= a.count) return;
+    const int L = a.layer;
+    // unrank T (colex over the component's compact bits)
+    uint64_t Tc = 0;
+    {
+        uint64_t rr = r;
+        int c = a.m - 1;
+        for (int i = L; i >= 1; --i) {
+            while (Bn(binom, c, i) > rr) --c;
+            Tc |= 1ull << c;
+            rr -= Bn(binom, c, i);
+            --c;
+        }
+    }
+    uint64_t Tg = 0;
+    for (uint64_t x = Tc; x; x &= x - 1) Tg |= 1ull << cv[__builtin_ctzll(x)];
+    // rank(T \ a_j) = sum_{i<j} C(a_i, i+1) + sum_{i>j} C(a_i, i)   (a_0 < a_1 < ...)
+    uint64_t suffix = 0;
+    {
+        int i = 0;
+        for (uint64_t x = Tc; x; x &= x - 1, ++i)
+            if (i >= 1) suffix += Bn(binom, __builtin_ctzll(x), i);
+    }
+    uint64_t prefix = 0;
+    float best = FLT_MAX;
+    int bestj = 255;
+    bool reached = false;
+    uint64_t x = Tc;
+    for (int j = 0; j < L; ++j) {
+        const int aj = __builtin_ctzll(x);
+        x &= x - 1;  // x now holds a_{j+1}, ...
+        const int leaf = cv[aj];
+        const uint64_t P = Tg & ~(1ull << leaf);
+        bool ok = !(a.skeleton && P != 0 && (P & a.edges[leaf]) == 0);
+        if (ok) {
+            const float gp = a.gprev[prefix + suffix];
+            if (gp < FLT_MAX) {
+                reached = true;
+                const float cand = gp + key_cost(bs_key(a.d, leaf, P));
+                if (cand < best || bestj == 255) {
+                    best = cand;
+                    bestj = j;
+                }
+            }
+        }
+        // advance to j+1: a_{j+1} leaves the suffix, a_j joins the prefix
+        if (x) suffix -= Bn(binom, __builtin_ctzll(x), j + 1);
+        prefix += Bn(binom, aj, j + 1);
+    }
+    a.gcur[r] = reached ? best : FLT_MAX;
+    a.leaf[r] = (uint8_t)(reached ? bestj : 255);
+}
+
+__global__ void count_reached_kernel(const float *g, uint64_t count, unsigned long long *acc) {
+    const uint64_t r = (uint64_t)blockIdx.x * kB + threadIdx.x;
+    bool ok = r < count && g[r] < FLT_MAX;
+    const unsigned long long b = __ballot(ok);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(acc, (unsigned long long)__popcll(b));
+}
+
+// walk the leaf pointers from the goal back to the root (one thread)
+__global__ void reconstruct_kernel(const uint8_t *leaf, const uint64_t *layer_off, const uint64_t *binom, int m,
+                                   int *chain) {
+    uint64_t T = (m >= 64) ? ~0ull : ((1ull << m) - 1ull);  // compact goal
+    for (int d = m; d >= 1; --d) {
+        uint64_t rank = 0;
+        int i = 0;
+        uint64_t x = T;
+        while (x) {
+            const int b = __builtin_ctzll(x);
+            x &= x - 1;
+            ++i;
+            rank += binom[b * 33 + i];
+        }
+        const int j = leaf[layer_off[d] + rank];
+        if (j == 255) { chain[d - 1] = -1; return; }
+        // j-th element of T
+        x = T;
+        for (int t = 0; t < j; ++t) x &= x - 1;
+        const int bit = __builtin_ctzll(x);
+        chain[d - 1] = bit;
+        T &= ~(1ull << bit);
+    }
+}
+
+}  // namespace
+
+namespace ulg {
+
+namespace {
+int components_gpu(const uint64_t *edges, int n, std::vector<uint64_t> &out) {
+    out.clear();
+    uint64_t visited = 0;
+    for (int v = 0; v < n; ++v) {
+        if ((visited >> v) & 1ull) continue;
+        uint64_t comp = 1ull << v;
+        visited |= comp;
+        std::vector<int> st{v};
+        while (!st.empty()) {
+            const int cur = st.back();
+            st.pop_back();
+            for (int i = 0; i < n; ++i)
+                if (!((visited >> i) & 1ull) && ((edges[cur] >> i) & 1ull)) {
+                    visited |= 1ull << i;
+                    comp |= 1ull << i;
+                    st.push_back(i);
+                }
+        }
+        out.push_back(comp);
+    }
+    return (int)out.size();
+}
+}  // namespace
+
+int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, float *goal_cost, int64_t *expanded) {
+    SearchState &s = *c->search;
+    const int n = s.n;
+    const uint64_t all = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+    std::vector<uint64_t> comps;
+    if (edges) components_gpu(edges, n, comps);
+    else comps.push_back(all);
+    // binomials C(a, b), a, b <= 32
+    std::vector<uint64_t> bn(33 * 33, 0);
+    for (int a = 0; a <= 32; ++a)
+        for (int b = 0; b <= 32; ++b) bn[a * 33 + b] = binom64(a, b);
+    DevBuf<uint64_t> d_bn, d_edges, d_layer_off;
+    DevBuf<int> d_cv, d_chain;
+    DevBuf<float> d_g0, d_g1;
+    DevBuf<uint8_t> d_leaf;
+    DevBuf<unsigned long long> d_acc;
+    auto cleanup = [&]() {
+        release(d_bn); release(d_edges); release(d_layer_off); release(d_cv); release(d_chain);
+        release(d_g0); release(d_g1); release(d_leaf); release(d_acc);
+    };
+    int rc;
+    if ((rc = ensure(c, d_bn, bn.size())) || (rc = ensure(c, d_edges, 64)) || (rc = ensure(c, d_cv, kMaxM)) ||
+        (rc = ensure(c, d_chain, kMaxM)) || (rc = ensure(c, d_acc, 1))) {
+        cleanup();
+        return rc;
+    }
+    hipError_t e = hipMemcpyAsync(d_bn.p, bn.data(), bn.size() * 8, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess && edges) e = hipMemcpyAsync(d_edges.p, edges, (size_t)n * 8, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d_acc.p, 0, 8, c->stream);
+    if (e != hipSuccess) { cleanup(); return set_err(c, ULG_ERR_HIP, hipGetErrorString(e)); }
+    const SearchDev dv = s.dev();
+    bool fail = false;
+    for (uint64_t comp : comps) {
+        const int m = __builtin_popcountll(comp);
+        if (m > kMaxM) { cleanup(); return set_err(c, ULG_ERR_UNSUPPORTED, "ulg_astar(GPU): component larger than 32 variables"); }
+        std::vector<int> cv;
+        for (int b = 0; b < n; ++b)
+            if ((comp >> b) & 1ull) cv.push_back(b);
+        std::vector<uint64_t> loff(m + 2, 0);
+        uint64_t maxl = 1;
+        for (int d = 0; d <= m; ++d) {
+            loff[d + 1] = loff[d] + binom64(m, d);
+            maxl = std::max<uint64_t>(maxl, binom64(m, d));
+        }
+        if ((rc = ensure(c, d_g0, maxl)) || (rc = ensure(c, d_g1, maxl)) || (rc = ensure(c, d_leaf, loff[m + 1])) ||
+            (rc = ensure(c, d_layer_off, (size_t)m + 2))) {
+            cleanup();
+            return rc;
+        }
+        e = hipMemcpyAsync(d_cv.p, cv.data(), (size_t)m * 4, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(d_layer_off.p, loff.data(), (size_t)(m + 2) * 8, hipMemcpyHostToDevice, c->stream);
+        // root: g = 0 (Node(0.0f, 0.0f, ancestors, leaf), astar_main.cpp:236)
+        const float zero = 0.0f;
+        if (e == hipSuccess) e = hipMemcpyAsync(d_g0.p, &zero, 4, hipMemcpyHostToDevice, c->stream);
+        if (e != hipSuccess) { cleanup(); return set_err(c, ULG_ERR_HIP, hipGetErrorString(e)); }
+        float *gprev = d_g0.p, *gcur = d_g1.p;
+        for (int d = 1; d <= m; ++d) {
+            const uint64_t cnt = binom64(m, d);
+            // nodes of layer d-1 that are reached and expanded (the goal layer is not expanded)
+            count_reached_kernel<<<(unsigned)((binom64(m, d - 1) + kB - 1) / kB), kB, 0, c->stream>>>(gprev, binom64(m, d - 1), d_acc.p);
+            LayerArgs a{dv, d_bn.p, d_cv.p, d_edges.p, edges ? 1 : 0, m, d, cnt, gprev, gcur, d_leaf.p + loff[d]};
+            prof_begin(c, "search_layer_pull");
+            layer_pull_kernel<<<(unsigned)((cnt + kB - 1) / kB), kB, 0, c->stream>>>(a);
+            prof_end(c);
+            std::swap(gprev, gcur);
+        }
+        reconstruct_kernel<<<1, 1, 0, c->stream>>>(d_leaf.p, d_layer_off.p, d_bn.p, m, d_chain.p);
+        e = hipGetLastError();
+        float g = 0.0f;
+        std::vector<int> chain(m);
+        if (e == hipSuccess) e = hipMemcpyAsync(&g, gprev, 4, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(chain.data(), d_chain.p, (size_t)m * 4, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) { cleanup(); return set_err(c, ULG_ERR_HIP, hipGetErrorString(e)); }
+        if (!(g < FLT_MAX) || std::find(chain.begin(), chain.end(), -1) != chain.end()) { fail = true; continue; }
+        // reconstruction as reconstructSolution: leaf order and getParents(remaining)
+        std::vector<int> total(n, 0), qv(m);
+        std::vector<uint64_t> qs(m), opt(n, 0), qp(m);
+        std::vector<float> qc(m);
+        uint64_t remaining = comp;
+        for (int i = m - 1; i >= 0; --i) {
+            const int leaf = cv[chain[i]];
+            total[i] = leaf;
+            qv[i] = leaf;
+            qs[i] = remaining;
+            remaining &= ~(1ull << leaf);
+        }
+        if ((rc = search_query(c, m, qv.data(), qs.data(), qc.data(), qp.data()))) { cleanup(); return rc; }
+        for (int i = 0; i < m; ++i) opt[i] = qp[i];
+        for (int v = 0; v < n; ++v) vpar[v] = 0;
+        for (int v = 0; v < n; ++v) vpar[total[v]] = opt[v];
+        for (int v = 0; v < n; ++v) order[v] = total[v];
+        *goal_cost = g;
+    }
+    unsigned long long acc = 0;
+    e = hipMemcpy(&acc, d_acc.p, 8, hipMemcpyDeviceToHost);
+    prof_collect(c);
+    cleanup();
+    if (e != hipSuccess) return set_err(c, ULG_ERR_HIP, hipGetErrorString(e));
+    *expanded = (int64_t)acc;
+    if (fail) return set_err(c, ULG_ERR_STATE, "ulg_astar(GPU): a component has no goal");
+    return ULG_OK;
+}
+
+}  // namespace ulg

@@ -1,0 +1,501 @@
+// search_host.cpp -- C ABI of the search side and the exact-order A*.
+//
+// Exact-order mode (ULG_ASTAR_EXACT) replays the reference's sequential
+// search -- run_astar_on_one_scc (astar/astar_main.cpp:216-546) with its
+// libstdc++-derived heap (priority_queue/priority_queue-inl.h:19-234) and the
+// epsilon/depth comparator (base/node.h:124-135) -- on the host, because the
+// DAG the reference returns is decided by that heap's pop order among
+// float-tied Markov-equivalent orders.  Every per-successor
+// lookup it needs is O(1) on tables the GPU built: getScore() is one read of
+// the best-score lattice (instead of the reference's linear scan of the
+// sorted list, sparse_parent_list.cpp:44-55) and h() two reads of the
+// pattern databases.  Parent sets for the reconstruction come from the device
+// query kernel.
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "search_internal.h"
+
+using namespace ulg;
+
+namespace {
+
+struct Node {
+    float g, h;
+    uint64_t sub;
+    uint8_t leaf;
+    int32_t pq;
+};
+
+bool g_have_bmi2 = __builtin_cpu_supports("bmi2");
+
+__attribute__((target("bmi2"))) inline uint64_t pext_bmi2(uint64_t x, uint64_t m) { return __builtin_ia32_pext_di(x, m); }
+
+// Host view of the best-score lattice: cost per subset of D_v.
+struct HostTables {
+    const float *cost;
+    const uint64_t *tb_off;
+    const uint64_t *support;
+    std::vector<int> hole;  // D_v == all \ {hole}: pext is a shift
+    uint64_t all;
+    int n;
+    const float *pd;
+    std::vector<uint64_t> groups;
+    std::vector<uint64_t> pd_off;
+
+    inline uint64_t index(int v, uint64_t S) const {
+        const uint64_t D = support[v];
+        S &= D;
+        const int h = hole[v];
+        if (h >= 0) return ((S >> (h + 1)) << h) | (S & ((1ull << h) - 1ull));
+        return g_have_bmi2 ? pext_bmi2(S, D) : pext64(S, D);
+    }
+    inline float bs(int v, uint64_t S) const { return cost[tb_off[v] + index(v, S)]; }
+    inline uint64_t gidx(uint64_t vs, uint64_t grp) const { return g_have_bmi2 ? pext_bmi2(vs, grp) : pext64(vs, grp); }
+    // StaticPatternDatabase::h (static_pattern_database.cpp:145-174)
+    inline float h(uint64_t S, bool *complete) const {
+        const uint64_t remaining = ~S & all;
+        float hv = 0.0f;
+        for (size_t g = 0; g < groups.size(); ++g) {
+            const uint64_t vs = groups[g] & remaining;
+            const float val = pd[pd_off[g] + gidx(vs, groups[g])];
+            if (vs == remaining) {
+                *complete = true;
+                return val;
+            }
+            hv += val;
+        }
+        return hv;
+    }
+};
+
+// generatedNodes (NodeMap): open addressing u64 -> node index
+struct NodeIndex {
+    std::vector<uint64_t> keys;
+    std::vector<uint32_t> vals;
+    uint64_t mask = 0, size = 0;
+    static constexpr uint64_t kEmpty = ~0ull;
+    void init(uint64_t cap) {
+        uint64_t c = 1024;
+        while (c < cap * 2) c <<= 1;
+        keys.assign(c, kEmpty);
+        vals.assign(c, 0);
+        mask = c - 1;
+        size = 0;
+    }
+    static inline uint64_t mix(uint64_t x) {
+        x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+        return x;
+    }
+    inline int64_t find(uint64_t k) const {
+        uint64_t i = mix(k) & mask;
+        while (true) {
+            const uint64_t kk = keys[i];
+            if (kk == k) return vals[i];
+            if (kk == kEmpty) return -1;
+            i = (i + 1) & mask;
+        }
+    }
+    void grow() {
+        std::vector<uint64_t> ok;
+        std::vector<uint32_t> ov;
+        ok.swap(keys);
+        ov.swap(vals);
+        init((ok.size()));
+        for (size_t i = 0; i < ok.size(); ++i)
+            if (ok[i] != kEmpty) insert(ok[i], ov[i]);
+    }
+    inline void insert(uint64_t k, uint32_t v) {
+        if ((size + 1) * 2 > keys.size()) grow();
+        uint64_t i = mix(k) & mask;
+        while (keys[i] != kEmpty && keys[i] != k) i = (i + 1) & mask;
+        if (keys[i] == kEmpty) ++size;
+        keys[i] = k;
+        vals[i] = v;
+    }
+};
+
+// PriorityQueue with the reference's heap algorithms and pqPos bookkeeping.
+struct Heap {
+    std::vector<uint32_t> a;
+    std::vector<Node> *nodes;
+    bool hang = false;
+
+    // CompareNodeStar: true if x has LOWER priority than y
+    inline bool cns(uint32_t x, uint32_t y) const {
+        const Node &A = (*nodes)[x], &B = (*nodes)[y];
+        const float fa = A.g + A.h;
+        const float fb = B.g + B.h;
+        const float diff = fa - fb;
+        if (std::fabs(diff) < FLT_EPSILON) {
+            const int la = __builtin_popcountll(A.sub) & 0xff, lb = __builtin_popcountll(B.sub) & 0xff;
+            return (lb - la) > 0;
+        }
+        return diff > 0;
+    }
+    inline void setpos(uint32_t x, int64_t p) { (*nodes)[x].pq = (int32_t)p; }
+    void push_hole(int64_t hole, int64_t top, uint32_t value) {
+        int64_t parent = (hole - 1) / 2;
+        while (hole > top && cns(a[parent], value)) {
+            a[hole] = a[parent];
+            setpos(a[hole], hole);
+            hole = parent;
+            parent = (hole - 1) / 2;
+        }
+        a[hole] = value;
+        setpos(value, hole);
+    }
+    void push(uint32_t x) {
+        a.push_back(x);
+        push_hole((int64_t)a.size() - 1, 0, x);
+    }
+    void adjust(int64_t hole, int64_t len, uint32_t value) {
+        const int64_t top = hole;
+        int64_t second = hole;
+        while (second < (len - 1) / 2) {
+            second = 2 * (second + 1);
+            if (cns(a[second], a[second - 1])) second--;
+            a[hole] = a[second];
+            setpos(a[hole], hole);
+            hole = second;
+        }
+        if ((len & 1) == 0 && second == (len - 2) / 2) {
+            second = 2 * (second + 1);
+            a[hole] = a[second - 1];
+            setpos(a[hole], hole);
+            hole = second - 1;
+        }
+        push_hole(hole, top, value);
+    }
+    uint32_t pop() {
+        const uint32_t ret = a[0];
+        const int64_t last = (int64_t)a.size() - 1;
+        const uint32_t value = a[last];
+        a[last] = a[0];
+        adjust(0, last, value);
+        a.pop_back();
+        return ret;
+    }
+    void update(uint32_t x) {
+        const int64_t pos = (*nodes)[x].pq;
+        const int64_t parent = (pos - 1) / 2;
+        const uint32_t value = a[pos];
+        if (pos > 0 && cns(a[parent], value)) {
+            int64_t par = (pos - 1) / 2, index = pos;
+            while (index > 0 && cns(a[par], value)) {
+                a[index] = a[par];
+                setpos(a[index], index);
+                index = par;
+                par = (par - 1) / 2;
+            }
+            if (pos != index) {
+                a[index] = value;
+                setpos(value, index);
+            }
+        } else {
+            // __down_heap as written: follows the left child only and does not
+            // record the moved value's position (priority_queue-inl.h:176-208)
+            const int64_t len = (int64_t)a.size();
+            int64_t index = pos, left = 2 * index + 1, right = 2 * index + 2, largest = len, guard = 0;
+            while (index < len) {
+                if ((right >= len) || ((left < len) && cns(a[right], a[left]))) largest = left;
+                if (largest < len && cns(value, a[largest])) {
+                    if (largest == index || ++guard > 128) { hang = true; break; }  // the reference would spin
+                    a[index] = a[largest];
+                    setpos(a[largest], index);
+                    index = largest;
+                    left = index * 2 + 1;
+                    right = index * 2 + 2;
+                } else
+                    break;
+            }
+            if (pos != index) a[index] = value;
+        }
+    }
+};
+
+// connected components of the skeleton (skeleton.cpp:187-230), discovery order
+int components(const uint64_t *edges, int n, std::vector<uint64_t> &out) {
+    out.clear();
+    uint64_t visited = 0;
+    for (int v = 0; v < n; ++v) {
+        if ((visited >> v) & 1ull) continue;
+        uint64_t comp = 0;
+        std::vector<int> stack{v};
+        visited |= 1ull << v;
+        comp |= 1ull << v;
+        while (!stack.empty()) {
+            const int cur = stack.back();
+            stack.pop_back();
+            for (int i = 0; i < n; ++i)
+                if (!((visited >> i) & 1ull) && ((edges[cur] >> i) & 1ull)) {
+                    visited |= 1ull << i;
+                    comp |= 1ull << i;
+                    stack.push_back(i);
+                }
+        }
+        out.push_back(comp);
+    }
+    return (int)out.size();
+}
+
+struct ExactResult {
+    bool found = false;
+    float goal_g = 0.0f;
+    std::vector<int> total;
+    std::vector<uint64_t> opt;
+};
+
+// run_astar_on_one_scc (astar_main.cpp:216-546)
+int astar_one(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool skeleton_good, uint64_t ancestors,
+              uint64_t the_scc, int64_t *expanded, bool *hang, ExactResult &res) {
+    const int n = T.n;
+    std::vector<Node> nodes;
+    nodes.reserve(1 << 16);
+    NodeIndex generated;
+    generated.init(1 << 16);
+    Heap open;
+    open.nodes = &nodes;
+    const uint64_t r1 = the_scc >> 1;
+    nodes.push_back(Node{0.0f, 0.0f, ancestors, (uint8_t)(r1 ? __builtin_ctzll(r1) + 1 : 0), 0});
+    open.push(0);
+    int64_t goal = -1;
+    const uint64_t allVariables = ancestors | the_scc;
+    const float upperBound = FLT_MAX;
+    int64_t nexp = 0;
+    while (!open.a.empty()) {
+        const uint32_t ui = open.pop();
+        ++nexp;
+        const uint64_t variables = nodes[ui].sub;
+        if (variables == allVariables) { goal = ui; break; }
+        if (nodes[ui].g + nodes[ui].h > upperBound) break;
+        nodes[ui].pq = -2;
+        const float ug = nodes[ui].g;
+        for (int leaf = 0; leaf < n; ++leaf) {
+            if ((variables >> leaf) & 1ull) continue;
+            if (!((the_scc >> leaf) & 1ull)) continue;
+            if (skeleton_good && variables != 0 && (variables & edges[leaf]) == 0) continue;
+            const uint64_t nv = variables | (1ull << leaf);
+            const int64_t si = generated.find(nv);
+            if (si < 0) {
+                const float leaf_score = T.bs(leaf, nv);
+                const float g = ug + leaf_score;
+                bool complete = false;
+                const float h = T.h(nv, &complete);
+                const uint32_t idx = (uint32_t)nodes.size();
+                nodes.push_back(Node{g, h, nv, (uint8_t)leaf, 0});
+                open.push(idx);
+                generated.insert(nv, idx);
+                continue;
+            }
+            if (nodes[si].pq == -2) continue;
+            const float g = ug + T.bs(leaf, variables);
+            if (g < nodes[si].g) {
+                nodes[si].leaf = (uint8_t)leaf;
+                nodes[si].g = g;
+                open.update((uint32_t)si);
+            }
+        }
+    }
+    *expanded += nexp;
+    if (open.hang) *hang = true;
+    if (goal < 0) return ULG_OK;
+    // reconstructSolution (astar_main.cpp:140-166)
+    const int count = __builtin_popcountll(the_scc);
+    res.total.assign(n, 0);
+    res.opt.assign(n, 0);
+    std::vector<int> qv;
+    std::vector<uint64_t> qs;
+    std::vector<int> pos;
+    uint64_t remaining = nodes[goal].sub;
+    int64_t cur = goal;
+    for (int i = 0; i < count && cur >= 0; ++i) {
+        const int leaf = nodes[cur].leaf;
+        res.total[count - 1 - i] = leaf;
+        qv.push_back(leaf);
+        qs.push_back(remaining);
+        pos.push_back(count - 1 - i);
+        remaining ^= 1ull << leaf;
+        cur = generated.find(remaining);
+    }
+    if (!qv.empty()) {
+        std::vector<float> qc(qv.size());
+        std::vector<uint64_t> qp(qv.size());
+        int rc = search_query(c, (int64_t)qv.size(), qv.data(), qs.data(), qc.data(), qp.data());
+        if (rc) return rc;
+        for (size_t i = 0; i < qv.size(); ++i) res.opt[pos[i]] = qp[i];
+    }
+    res.found = true;
+    res.goal_g = nodes[goal].g;
+    return ULG_OK;
+}
+
+SearchState &state(ulg_ctx *c) {
+    if (!c->search) c->search = new SearchState();
+    return *c->search;
+}
+
+}  // namespace
+
+namespace ulg {
+
+int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, float *goal_cost, int64_t *expanded);
+
+}  // namespace ulg
+
+extern "C" {
+
+int ulg_search_load(ulg_ctx *c, int n, const int64_t *offsets, const uint64_t *sets, const float *costs) {
+    if (!c || n < 1 || n > kMaxVars || !offsets || !sets || !costs) return set_err(c, ULG_ERR_ARG, "ulg_search_load: bad arguments");
+    ULG_HIP(c, hipSetDevice(c->device));
+    SearchState &s = state(c);
+    s.n = n;
+    s.offsets.assign(offsets, offsets + n + 1);
+    const int64_t total = offsets[n];
+    for (int v = 0; v < n; ++v)
+        if (offsets[v + 1] < offsets[v] || offsets[v + 1] - offsets[v] > 0xffffffffll)
+            return set_err(c, ULG_ERR_ARG, "ulg_search_load: bad offsets");
+    int rc;
+    if ((rc = ensure(c, s.d_sets, (size_t)std::max<int64_t>(total, 1))) || (rc = ensure(c, s.d_costs, (size_t)std::max<int64_t>(total, 1))) ||
+        (rc = ensure(c, s.d_offsets, (size_t)n + 1)))
+        return rc;
+    if (total) {
+        ULG_HIP(c, hipMemcpyAsync(s.d_sets.p, sets, (size_t)total * 8, hipMemcpyHostToDevice, c->stream));
+        ULG_HIP(c, hipMemcpyAsync(s.d_costs.p, costs, (size_t)total * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    ULG_HIP(c, hipMemcpyAsync(s.d_offsets.p, offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    s.host_costs_ready = false;
+    return search_build_tables(c);
+}
+
+int ulg_search_from_scores(ulg_ctx *c) {
+    if (!c) return ULG_ERR_ARG;
+    if (!c->scored) return set_err(c, ULG_ERR_STATE, "ulg_search_from_scores: call ulg_cbic_score first");
+    if (c->nv != c->n) return set_err(c, ULG_ERR_STATE, "ulg_search_from_scores: every variable must be scored in this context");
+    ULG_HIP(c, hipSetDevice(c->device));
+    SearchState &s = state(c);
+    const int n = c->n;
+    std::vector<int64_t> src(n + 1);
+    ULG_HIP(c, hipMemcpyAsync(src.data(), c->out_offsets.p, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    const int64_t total = src[n];
+    int rc;
+    if ((rc = ensure(c, s.d_sets, (size_t)std::max<int64_t>(total, 1))) || (rc = ensure(c, s.d_costs, (size_t)std::max<int64_t>(total, 1))) ||
+        (rc = ensure(c, s.d_offsets, (size_t)n + 1)) || (rc = ensure(c, s.d_scores_tmp, (size_t)std::max<int64_t>(total, 1))))
+        return rc;
+    // order the lists by variable index (the .pss variable order)
+    std::vector<int> where(n, -1);
+    for (int i = 0; i < n; ++i) where[c->vars[i]] = i;
+    s.n = n;
+    s.offsets.assign(n + 1, 0);
+    for (int v = 0; v < n; ++v) {
+        const int i = where[v];
+        const int64_t cnt = src[i + 1] - src[i];
+        s.offsets[v + 1] = s.offsets[v] + cnt;
+        if (cnt) {
+            ULG_HIP(c, hipMemcpyAsync(s.d_sets.p + s.offsets[v], c->out_sets.p + src[i], (size_t)cnt * 8, hipMemcpyDeviceToDevice, c->stream));
+            ULG_HIP(c, hipMemcpyAsync(s.d_scores_tmp.p + s.offsets[v], c->out_scores.p + src[i], (size_t)cnt * 4, hipMemcpyDeviceToDevice, c->stream));
+        }
+    }
+    ULG_HIP(c, hipMemcpyAsync(s.d_offsets.p, s.offsets.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    if ((rc = search_quantize_device(c, s.d_scores_tmp.p, s.d_costs.p, total))) return rc;
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    s.host_costs_ready = false;
+    return search_build_tables(c);
+}
+
+int ulg_bestscore_query(ulg_ctx *c, int64_t count, const int *vars, const uint64_t *S, float *costs, uint64_t *parents) {
+    if (!c || count < 0 || (count && (!vars || !S))) return ULG_ERR_ARG;
+    if (!c->search || !c->search->tables_ready) return set_err(c, ULG_ERR_STATE, "ulg_bestscore_query: no best-score tables");
+    for (int64_t i = 0; i < count; ++i)
+        if (vars[i] < 0 || vars[i] >= c->search->n) return set_err(c, ULG_ERR_ARG, "ulg_bestscore_query: bad variable");
+    if (count == 0) return ULG_OK;
+    ULG_HIP(c, hipSetDevice(c->device));
+    return search_query(c, count, vars, S, costs, parents);
+}
+
+int ulg_pdb_build(ulg_ctx *c, int pd_count, uint64_t ancestors, uint64_t scc) {
+    if (!c) return ULG_ERR_ARG;
+    if (!c->search || !c->search->tables_ready) return set_err(c, ULG_ERR_STATE, "ulg_pdb_build: no best-score tables");
+    ULG_HIP(c, hipSetDevice(c->device));
+    return search_build_pdb(c, pd_count, ancestors, scc);
+}
+
+int ulg_pdb_query(ulg_ctx *c, int64_t count, const uint64_t *S, float *h, int *complete) {
+    if (!c || count < 0 || (count && (!S || !h))) return ULG_ERR_ARG;
+    if (!c->search || !c->search->pdb_ready) return set_err(c, ULG_ERR_STATE, "ulg_pdb_query: no pattern database");
+    if (count == 0) return ULG_OK;
+    ULG_HIP(c, hipSetDevice(c->device));
+    return search_pdb_query(c, count, S, h, complete);
+}
+
+int ulg_astar(ulg_ctx *c, const uint64_t *edges, int pd_count, int mode, uint64_t *vpar, int *order,
+              float *goal_cost, int64_t *expanded, char *net_text, int64_t net_cap) {
+    if (!c || !vpar || !order || !goal_cost || !expanded) return ULG_ERR_ARG;
+    if (!c->search || !c->search->tables_ready) return set_err(c, ULG_ERR_STATE, "ulg_astar: no best-score tables");
+    ULG_HIP(c, hipSetDevice(c->device));
+    SearchState &s = *c->search;
+    const int n = s.n;
+    const uint64_t all = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+    int rc;
+    // astar(): the heuristic covers all variables, no ancestors (astar_main.cpp:590-611)
+    if (!s.pdb_ready || s.pd_count != pd_count || s.scc != all || s.ancestors != 0)
+        if ((rc = search_build_pdb(c, pd_count, 0, all))) return rc;
+    *expanded = 0;
+    *goal_cost = 0.0f;
+    for (int i = 0; i < n; ++i) { vpar[i] = 0; order[i] = 0; }
+    if (net_text && net_cap > 0) net_text[0] = 0;
+    if (mode == ULG_ASTAR_GPU) return astar_gpu(c, edges, vpar, order, goal_cost, expanded);
+    if (mode != ULG_ASTAR_EXACT) return set_err(c, ULG_ERR_ARG, "ulg_astar: unknown mode");
+    if ((rc = search_cost_table_host(c))) return rc;
+    HostTables T;
+    T.cost = s.host_costs;
+    T.tb_off = s.tb_off.data();
+    T.support = s.support.data();
+    T.all = all;
+    T.n = n;
+    T.hole.assign(n, -1);
+    for (int v = 0; v < n; ++v) {
+        const uint64_t D = s.support[v];
+        const uint64_t miss = ~D & all;
+        if (__builtin_popcountll(miss) == 1 && ((D & ~all) == 0)) T.hole[v] = __builtin_ctzll(miss);
+    }
+    T.pd = s.pd_host.data();
+    T.groups = s.groups;
+    T.pd_off = s.pd_off;
+    std::vector<uint64_t> comps;
+    const bool good = edges != nullptr;
+    if (good) components(edges, n, comps);
+    else comps.push_back(all);
+    bool hang = false;
+    bool fail = false;
+    for (uint64_t comp : comps) {
+        ExactResult r;
+        if ((rc = astar_one(c, T, edges, good, 0, comp, expanded, &hang, r))) return rc;
+        if (!r.found) { fail = true; continue; }
+        // each component rewrites netFile and netFile.csv (astar_main.cpp:470,519)
+        for (int v = 0; v < n; ++v) vpar[v] = 0;
+        for (int v = 0; v < n; ++v) vpar[r.total[v]] = r.opt[v];
+        for (int v = 0; v < n; ++v) order[v] = r.total[v];
+        *goal_cost = r.goal_g;
+        if (net_text && net_cap > 0) {
+            int64_t len = 0;
+            len += snprintf(net_text + len, (size_t)(net_cap - len), "NumVars %d\n", n);
+            for (int v = 0; v < n && len < net_cap; ++v) {
+                len += snprintf(net_text + len, (size_t)(net_cap - len), "Var %d, parents", r.total[v] + 1);
+                for (int i = 0; i < n && len < net_cap; ++i)
+                    if ((r.opt[v] >> i) & 1ull) len += snprintf(net_text + len, (size_t)(net_cap - len), ", %d", i + 1);
+                if (len < net_cap) len += snprintf(net_text + len, (size_t)(net_cap - len), "\n");
+            }
+        }
+    }
+    if (hang) return set_err(c, ULG_ERR_STATE, "ulg_astar: the reference heap's __down_heap would not terminate here");
+    if (fail) return set_err(c, ULG_ERR_STATE, "ulg_astar: a component has no goal");
+    return ULG_OK;
+}
+
+}  // extern "C"

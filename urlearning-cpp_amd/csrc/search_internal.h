@@ -1,0 +1,193 @@
+// search_internal.h -- state and device helpers of the search side
+// (best-score tables, pattern database, A*).
+#pragma once
+
+#include <cfloat>
+#include <cstdint>
+#include <vector>
+
+#include "ulg_internal.h"
+
+namespace ulg {
+
+constexpr int kMaxGroups = 8;
+
+// ---- device helpers ----------------------------------------------------------
+__host__ __device__ inline uint64_t pext64(uint64_t x, uint64_t m) {
+    uint64_t r = 0;
+    int k = 0;
+    while (m) {
+        const uint64_t b = m & (0 - m);
+        if (x & b) r |= 1ull << k;
+        ++k;
+        m ^= b;
+    }
+    return r;
+}
+
+// float -> uint32 whose unsigned order is the float order; -0 folds onto +0 so
+// that ties between signed zeros fall to the file index, as in the reference's
+// float compare (sparse_parent_list.cpp:7-9).
+__host__ __device__ inline uint32_t ordkey(float f) {
+    if (f == 0.0f) f = 0.0f;
+    uint32_t u;
+#ifdef __HIP_DEVICE_COMPILE__
+    u = __float_as_uint(f);
+#else
+    __builtin_memcpy(&u, &f, 4);
+#endif
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__host__ __device__ inline float key_cost(uint64_t key) {
+    if (key == ~0ull) return FLT_MAX;  // no stored subset: getScore returns FLT_MAX
+    const uint32_t k = (uint32_t)(key >> 32);
+    const uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+    float f;
+#ifdef __HIP_DEVICE_COMPILE__
+    f = __uint_as_float(u);
+#else
+    __builtin_memcpy(&f, &u, 4);
+#endif
+    return f;
+}
+
+// The .pss "%f" + atof round trip (score_main.cpp:191, score_cache.cpp:151):
+// D = round-half-even(|x| * 10^6) in exact integers (glibc printf is exact,
+// ties to even); strtod(D / 10^6) is the correctly rounded double quotient;
+// cost = float(-1 * value).
+__host__ __device__ inline float quantize_score(float x) {
+    uint32_t u;
+#ifdef __HIP_DEVICE_COMPILE__
+    u = __float_as_uint(x);
+#else
+    __builtin_memcpy(&u, &x, 4);
+#endif
+    const uint32_t ex = (u >> 23) & 0xffu;
+    const bool neg = (u >> 31) != 0;
+    if (ex == 0xffu) return -x;  // inf -> -inf; nan stays nan
+    uint64_t M;
+    int E;
+    if (ex == 0) { M = u & 0x7fffffu; E = -149; }
+    else { M = (u & 0x7fffffu) | 0x800000u; E = (int)ex - 150; }
+    double mag;
+    if (E >= 0) {
+        mag = neg ? -(double)x : (double)x;  // x * 10^6 is an integer: printed exactly
+    } else {
+        const int sh = -E;
+        const uint64_t num = M * 1000000ull;  // < 2^44
+        uint64_t D;
+        if (sh >= 64) D = 0;
+        else {
+            D = num >> sh;
+            const uint64_t rem = num & ((1ull << sh) - 1ull);
+            const uint64_t half = 1ull << (sh - 1);
+            if (rem > half || (rem == half && (D & 1ull))) ++D;
+        }
+        mag = (double)D / 1000000.0;
+    }
+    const double val = neg ? -mag : mag;
+    return (float)(-1.0 * val);
+}
+
+// device view of the search tables (passed by value to kernels)
+struct SearchDev {
+    const uint64_t *table;   // packed (ordered cost << 32 | file index) per subset of D_v
+    const uint64_t *tb_off;  // [n+1]
+    const uint64_t *support; // D_v
+    const uint64_t *sets;    // per-variable lists, file order
+    const int64_t *offsets;  // [n+1]
+    const float *pd;         // pattern databases
+    const uint64_t *gmeta;   // groups[kMaxGroups], pd_off[kMaxGroups]
+    int pd_count;
+    int n;
+};
+
+__device__ inline uint64_t bs_key(const SearchDev &d, int v, uint64_t S) {
+    const uint64_t D = d.support[v];
+    return d.table[d.tb_off[v] + pext64(S & D, D)];
+}
+
+// StaticPatternDatabase::h (static_pattern_database.cpp:145-174)
+__device__ inline float pdb_h(const SearchDev &d, uint64_t S, int *complete) {
+    const uint64_t mask = (d.n >= 64) ? ~0ull : ((1ull << d.n) - 1ull);
+    const uint64_t remaining = ~S & mask;
+    float h = 0.0f;
+    for (int g = 0; g < d.pd_count; ++g) {
+        const uint64_t grp = d.gmeta[g];
+        const uint64_t vs = grp & remaining;
+        const float val = d.pd[d.gmeta[kMaxGroups + g] + pext64(vs, grp)];
+        if (vs == remaining) {
+            *complete = 1;
+            return val;
+        }
+        h += val;
+    }
+    return h;
+}
+
+// ---- host state -----------------------------------------------------------------
+struct SearchState {
+    int n = 0;
+    std::vector<int64_t> offsets;  // [n+1] host copy
+    DevBuf<uint64_t> d_sets;
+    DevBuf<float> d_costs, d_scores_tmp;
+    DevBuf<int64_t> d_offsets;
+    // best-score tables
+    std::vector<uint64_t> support, tb_off;
+    std::vector<int> mbits;
+    uint64_t table_entries = 0;
+    DevBuf<uint64_t> d_table, d_tb_off, d_support;
+    DevBuf<int> d_mbits, d_prefix;
+    bool tables_ready = false;
+    // host copy of the per-subset best costs (exact-order search)
+    DevBuf<float> d_cost_table;
+    float *host_costs = nullptr;
+    uint64_t host_cost_cap = 0;
+    bool host_costs_ready = false;
+    // pattern database
+    int pd_count = 0;
+    uint64_t ancestors = 0, scc = 0;
+    std::vector<uint64_t> groups, pd_off;
+    std::vector<float> pd_host;
+    DevBuf<float> d_pd, d_bsv;
+    DevBuf<int> d_bitpos;
+    DevBuf<uint64_t> d_groups;
+    bool pdb_ready = false;
+    // query scratch
+    DevBuf<int> q_vars;
+    DevBuf<uint64_t> q_sets, q_par;
+    DevBuf<float> q_costs;
+
+    SearchDev dev() const {
+        SearchDev d;
+        d.table = d_table.p;
+        d.tb_off = d_tb_off.p;
+        d.support = d_support.p;
+        d.sets = d_sets.p;
+        d.offsets = d_offsets.p;
+        d.pd = d_pd.p;
+        d.gmeta = d_groups.p;
+        d.pd_count = pd_count;
+        d.n = n;
+        return d;
+    }
+    void release_all() {
+        release(d_sets); release(d_costs); release(d_scores_tmp); release(d_offsets);
+        release(d_table); release(d_tb_off); release(d_support); release(d_mbits); release(d_prefix);
+        release(d_cost_table); release(d_pd); release(d_bsv); release(d_bitpos); release(d_groups);
+        release(q_vars); release(q_sets); release(q_par); release(q_costs);
+        if (host_costs) (void)hipHostFree(host_costs);
+        host_costs = nullptr;
+        host_cost_cap = 0;
+    }
+};
+
+int search_build_tables(ulg_ctx *c);
+int search_build_pdb(ulg_ctx *c, int pd_count, uint64_t ancestors, uint64_t scc);
+int search_quantize_device(ulg_ctx *c, const float *d_scores, float *d_costs, int64_t count);
+int search_cost_table_host(ulg_ctx *c);
+int search_query(ulg_ctx *c, int64_t count, const int *vars, const uint64_t *S, float *costs, uint64_t *parents);
+int search_pdb_query(ulg_ctx *c, int64_t count, const uint64_t *S, float *h, int *complete);
+
+}  // namespace ulg

@@ -2,7 +2,7 @@
 #include <cstdio>
 #include <cstring>
 
-#include "ulg_internal.h"
+#include "search_internal.h"
 
 namespace ulg {
 
@@ -103,6 +103,11 @@ void ulg_destroy(ulg_ctx *c) {
     release(c->d_cand); release(c->d_meta); release(c->d_binom);
     release(c->out_sets); release(c->out_scores); release(c->out_offsets);
     release(c->qbuf_in); release(c->qbuf_out);
+    if (c->search) {
+        c->search->release_all();
+        delete c->search;
+        c->search = nullptr;
+    }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }

@@ -24,6 +24,8 @@ struct DevBuf {
     size_t cap = 0;  // elements
 };
 
+struct SearchState;
+
 struct ProfRec {
     std::string name;
     hipEvent_t start, stop;
@@ -64,6 +66,9 @@ struct ulg_ctx {
     ulg::DevBuf<int64_t> out_offsets;
 
     ulg::DevBuf<float> qbuf_in, qbuf_out;
+
+    // ---- search side (best-score tables, pattern database, A*) ----
+    ulg::SearchState *search = nullptr;
 
     // ---- profiling ----
     bool prof = false;

@@ -42,6 +42,12 @@ def lib():
         L.ulg_cbic_fetch.argtypes = [P, P, P, P, I]
         L.ulg_cbic_score_vars.argtypes = [P, P, I, P, I, P, P, P, I64]
         L.ulg_quantize_costs.argtypes = [P, P, P, I64]
+        L.ulg_search_load.argtypes = [P, I, P, P, P]
+        L.ulg_search_from_scores.argtypes = [P]
+        L.ulg_bestscore_query.argtypes = [P, I64, P, P, P, P]
+        L.ulg_pdb_build.argtypes = [P, I, C.c_uint64, C.c_uint64]
+        L.ulg_pdb_query.argtypes = [P, I64, P, P, P]
+        L.ulg_astar.argtypes = [P, P, I, I, P, P, C.POINTER(F), C.POINTER(I64), C.c_char_p, I64]
         L.ulg_profile_enable.argtypes = [P, I]
         L.ulg_profile_get.argtypes = [P, C.c_char_p, C.POINTER(D), C.POINTER(I64), C.POINTER(D)]
         L.ulg_profile_dump.argtypes = [P, C.c_char_p, I64]
@@ -135,6 +141,61 @@ class Context:
         out = np.empty_like(s)
         self._check(lib().ulg_quantize_costs(self._h, _ptr(s), _ptr(out), s.size), "ulg_quantize_costs")
         return out
+
+    # ---- search side -------------------------------------------------------
+    ASTAR_EXACT = 0
+    ASTAR_GPU = 1
+
+    def search_load(self, offsets, sets, costs):
+        o = np.ascontiguousarray(offsets, dtype=np.int64)
+        s = np.ascontiguousarray(sets, dtype=np.uint64)
+        c = np.ascontiguousarray(costs, dtype=np.float32)
+        if s.size == 0:
+            s = np.zeros(1, dtype=np.uint64)
+            c = np.zeros(1, dtype=np.float32)
+        self._check(lib().ulg_search_load(self._h, len(o) - 1, _ptr(o), _ptr(s), _ptr(c)), "ulg_search_load")
+        self.search_n = len(o) - 1
+
+    def search_from_scores(self):
+        self._check(lib().ulg_search_from_scores(self._h), "ulg_search_from_scores")
+        self.search_n = self.n
+
+    def bestscore(self, variables, S):
+        v = np.ascontiguousarray(variables, dtype=np.int32)
+        s = np.ascontiguousarray([int(x) for x in S], dtype=np.uint64)
+        costs = np.empty(len(v), dtype=np.float32)
+        par = np.empty(len(v), dtype=np.uint64)
+        self._check(lib().ulg_bestscore_query(self._h, len(v), _ptr(v), _ptr(s), _ptr(costs), _ptr(par)),
+                    "ulg_bestscore_query")
+        return costs, par
+
+    def pdb_build(self, pd_count=2, ancestors=0, scc=None):
+        if scc is None:
+            scc = (1 << self.search_n) - 1
+        self._check(lib().ulg_pdb_build(self._h, int(pd_count), int(ancestors), int(scc)), "ulg_pdb_build")
+
+    def pdb_h(self, S):
+        s = np.ascontiguousarray([int(x) for x in S], dtype=np.uint64)
+        h = np.empty(len(s), dtype=np.float32)
+        comp = np.empty(len(s), dtype=np.int32)
+        self._check(lib().ulg_pdb_query(self._h, len(s), _ptr(s), _ptr(h), _ptr(comp)), "ulg_pdb_query")
+        return h, comp
+
+    def astar(self, edges=None, pd_count=2, mode=0, net_text=True):
+        n = self.search_n
+        vpar = np.zeros(n, dtype=np.uint64)
+        order = np.zeros(n, dtype=np.int32)
+        cost = C.c_float()
+        exp = C.c_int64()
+        buf = C.create_string_buffer(1 << 16) if net_text else None
+        e = None
+        if edges is not None:
+            e = np.ascontiguousarray([int(x) for x in edges], dtype=np.uint64)
+        self._check(lib().ulg_astar(self._h, _ptr(e) if e is not None else None, int(pd_count), int(mode),
+                                    _ptr(vpar), _ptr(order), C.byref(cost), C.byref(exp), buf,
+                                    len(buf) if buf is not None else 0), "ulg_astar")
+        return {"vpar": vpar, "order": order, "cost": cost.value, "expanded": exp.value,
+                "net_text": buf.value.decode() if buf is not None else None}
 
     # ---- profiling ----------------------------------------------------------
     def profile(self, on: bool = True):
