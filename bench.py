@@ -93,6 +93,61 @@ def roofline(ctx, cfg, per_launch_sets):
              "fp64_tflops": sets * flops_per_set / (p["avg_ms"] * 1e-3) / 1e12}, p)
 
 
+def search_metrics(ctx, cfg, variables, cands, rank, ws, reps=3):
+    """Order-graph search side on this rank's scored lists: GPU best-score
+    tables + pattern database + GPU layer-synchronous search at the bench
+    config (A* expansions/s), then the exact-order A* (reference pop order,
+    bit-exact DAG) and the CPU oracle's A* on config C2 (rank 0, N=1 only)."""
+    import time as _t
+    n, k = cfg["n"], cfg["k"]
+    full = [(1 << n) - 1] * n
+    out = {}
+    ctx.score(list(range(n)), full, k)
+    t0 = _t.perf_counter()
+    ctx.search_from_scores()
+    t1 = _t.perf_counter()
+    ctx.pdb_build(2)
+    t2 = _t.perf_counter()
+    best = None
+    for _ in range(reps):
+        ts = _t.perf_counter()
+        g = ctx.astar(edges=full, mode=1, net_text=False)
+        dt = _t.perf_counter() - ts
+        best = dt if best is None else min(best, dt)
+    out["gpu_search"] = {"config": f"C3 lists (n={n}, k={k}), full skeleton, static PDB(2)",
+                         "expansions": g["expanded"], "ms": 1e3 * best,
+                         "expansions_per_s": g["expanded"] / best, "goal_cost": g["cost"],
+                         "tables_ms": 1e3 * (t1 - t0), "pdb_ms": 1e3 * (t2 - t1),
+                         "note": "layer-synchronous pull over the whole order lattice; best of %d" % reps}
+    if rank == 0 and ws == 1:
+        c2 = CONFIGS["c2"]
+        n2, N2, k2 = c2["n"], c2["N"], c2["k"]
+        X2, _ = synth.gaussian_sem(n2, N2, 9200)
+        full2 = [(1 << n2) - 1] * n2
+        ctx.load(X2, c2["lam"])
+        ctx.score(list(range(n2)), full2, k2)
+        ctx.search_from_scores()
+        ts = _t.perf_counter()
+        e = ctx.astar(edges=full2, mode=0, net_text=False)
+        dt = _t.perf_counter() - ts
+        out["exact"] = {"config": f"C2 (n={n2}, N={N2}, k={k2}), full skeleton", "expansions": e["expanded"],
+                        "ms": 1e3 * dt, "expansions_per_s": e["expanded"] / dt, "goal_cost": e["cost"],
+                        "note": "reference pop order replayed on the host over GPU-built O(1) tables (incl. table D2H)"}
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        offs, sets, scores = ctx.fetch(ctx.score(list(range(n2)), full2, k2)[0])
+        costs = ctx.quantize(scores)
+        srch = oracle.Search(n2, offs, sets, costs)
+        ts = _t.perf_counter()
+        r = srch.astar(edges=full2)
+        dt = _t.perf_counter() - ts
+        out["cpu_baseline"] = {"value": r["expanded"] / dt, "unit": "A* expansions/s", "cores": 1, "kind": "port",
+                               "sample": f"CPU oracle A* (sorted-list scans, reference heap) on C2: "
+                                         f"{r['expanded']} expansions in {dt:.2f} s",
+                               "same_dag_as_exact": [int(x) for x in r["vpar"]] == [int(x) for x in e["vpar"]]}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -101,6 +156,7 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--mode", default="weak", choices=["weak", "shard"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-search", action="store_true")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -178,6 +234,10 @@ def main():
     roof, _ = roofline(ctx, cfg, per_launch)
     kernels = ctx.profile_dump()
 
+    search = None
+    if args.mode == "weak" and not args.no_search:
+        search = search_metrics(ctx, cfg, variables, cands, rank, ws)
+
     if rank == 0:
         res = {
             "metric": METRIC,
@@ -200,6 +260,8 @@ def main():
             "roofline": roof,
             "kernel_ms_total": {kk: round(vv["total_ms"], 4) for kk, vv in kernels.items()},
         }
+        if search is not None:
+            res["astar"] = search
         if ws == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(cfg, X)
         print(json.dumps(res))
