@@ -141,6 +141,12 @@ int ulg_astar(ulg_ctx *ctx, const uint64_t *edges, int pd_count, int mode,
               uint64_t *vpar, int *order, float *goal_cost, int64_t *expanded,
               char *net_text, int64_t net_cap);
 
+/* ---- tuning knobs -------------------------------------------------------
+ * "score_variant" (0..3, default 1): bit 0 = fully unrolled presence gather
+ * in the scorer (layers <= 6), bit 1 = stack-machine dominance recursion.
+ * All variants compute identical results; the knob exists for A/B timing. */
+int ulg_set_option(ulg_ctx *ctx, const char *name, int64_t value);
+
 /* ---- profiling (per-kernel HIP-event timing on the context stream) ---- */
 int ulg_profile_enable(ulg_ctx *ctx, int on);
 /* Average duration (ms) and launch count of kernels whose name matches

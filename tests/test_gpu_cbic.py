@@ -137,3 +137,22 @@ def test_rescoring_is_deterministic(ulg_ctx):
     b = ulg_ctx.score_all(list(range(15)), [(1 << 15) - 1] * 15, 5)
     for x, y in zip(a, b):
         assert x.tobytes() == y.tobytes()
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_scorer_variants_identical(ulg_ctx, oracle_built, variant):
+    """Every scorer variant (presence gather x recursion form) stores exactly
+    the oracle's sets (k=6 exercises the unrolled presence, k=7,8 the loop)."""
+    n = 11
+    X, _ = synth.gaussian_sem(n, 2500, 9230 + variant)
+    variables = list(range(n))
+    cands = [(1 << n) - 1] * n
+    ulg_ctx.load(X, 2.0)
+    ulg_ctx.set_option("score_variant", variant)
+    try:
+        for k in (6, 8):
+            g = ulg_ctx.score_all(variables, cands, k)
+            o = _oracle_lists(oracle_built, X, 2.0, variables, cands, k)
+            _compare_lists(*o, *g, variables, ctx=f"variant {variant} k={k}")
+    finally:
+        ulg_ctx.set_option("score_variant", 1)

@@ -218,6 +218,110 @@ __device__ __forceinline__ void best_subset(uint32_t T, uint32_t pv, const Bits<
     }
 }
 
+// Same recursion as an explicit stack machine: one loop iteration advances
+// one step of this lane's own traversal, so a wave costs the max over its
+// lanes' step counts instead of the union of their recursion trees (the
+// nested form above executes a level's loops whenever ANY lane recurses).
+// Saved frames live in LDS, one u64 per frame, lane-interleaved
+// (stk[slot * kBlock + tid]): T | idx << 10 | j << 14 | pv << 18; the loop
+// position i and the partial vector npv are re-derived from (pv, u, j).
+template <int L, int W>
+__device__ __forceinline__ void best_subset_stack(uint32_t Ptop, uint32_t pvtop, const Bits<W> &present,
+                                                  Bits<W> &checked, Bits<W> &visited, uint64_t *stk) {
+    const int tid = threadIdx.x;
+    uint32_t T = Ptop, pv = pvtop, npv = 0, u = 0;
+    int sp = 0, m = L, idx = 0, i = 0, j = 0;
+    bool inner = false;
+    while (true) {
+        if (!inner) {
+            if (idx == m) {  // fb returns
+                if (sp == 0) break;
+                const uint32_t childT = T;
+                --sp;
+                const uint64_t F = stk[sp * 256 + tid];
+                T = (uint32_t)(F & 1023u);
+                idx = (int)((F >> 10) & 15u);
+                j = (int)((F >> 14) & 15u);
+                pv = (uint32_t)(F >> 18);
+                u = (pv >> (4 * idx)) & 15u;
+                npv = 0;
+                i = 0;
+                for (int jj = 0; jj < j;) {
+                    const uint32_t pi = (pv >> (4 * i)) & 15u;
+                    ++i;
+                    if (pi == u) continue;
+                    npv |= pi << (4 * jj);
+                    ++jj;
+                }
+                m = L - sp;
+                inner = true;
+                checked.set(childT);  // checked.insert(thin_parents) after each recursive call
+                continue;
+            }
+            u = (pv >> (4 * idx)) & 15u;
+            const uint32_t T2 = T ^ (1u << u);
+            if (checked.test(T2)) { ++idx; continue; }
+            if (present.test(T2)) { visited.set(T2); ++idx; continue; }
+            inner = true;
+            i = 0;
+            j = 0;
+            npv = 0;
+        } else {
+            if (i == m) { inner = false; ++idx; continue; }
+            const uint32_t pi = (pv >> (4 * i)) & 15u;
+            ++i;
+            if (pi == u) continue;
+            npv |= pi << (4 * j);
+            ++j;
+            // recurse into fb(T ^ u, npv, m - 1)
+            stk[sp * 256 + tid] = (uint64_t)T | ((uint64_t)idx << 10) | ((uint64_t)j << 14) | ((uint64_t)pv << 18);
+            ++sp;
+            T = T ^ (1u << u);
+            pv = npv;
+            m = L - sp;
+            idx = 0;
+            inner = false;
+        }
+    }
+}
+
+// Presence of every key with a fully unrolled subset loop: the rank of each
+// subset t of the Q local bits is a compile-time sum of per-(bit, position)
+// binomials preloaded into registers.  Q = L when variable 0 is in P (local
+// bits = P), Q = L + 1 otherwise (P plus variable 0).
+template <int L, int PHASE, int Q, int W>
+__device__ __forceinline__ void presence_unrolled(Bits<W> &present, const uint32_t *binom, uint64_t cpack, bool z,
+                                                  const float *table, const uint64_t *toffv) {
+    constexpr uint32_t Plocal = (Q == L) ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
+    uint32_t RB[Q][L + 1];
+#pragma unroll
+    for (int lb = 0; lb < Q; ++lb) {
+        const int ci = (int)((cpack >> (6 * lb)) & 63ull);
+#pragma unroll
+        for (int p = 1; p <= L; ++p) RB[lb][p] = (p <= lb + 1) ? B(binom, ci, p) : 0u;
+    }
+    uint64_t off[L + 1];
+#pragma unroll
+    for (int pc = 1; pc <= L; ++pc) off[pc] = toffv[pc];
+#pragma unroll
+    for (uint32_t t = 1; t < (1u << Q); ++t) {
+        const int pc = __builtin_popcount(t);
+        if (pc > L || t == Plocal) continue;
+        if (pc == L && (PHASE == 0 || !(t & 1u))) continue;
+        if ((t & 1u) && !z) continue;
+        uint64_t rk = 0;
+        int jj = 0;
+#pragma unroll
+        for (int b = 0; b < Q; ++b)
+            if ((t >> b) & 1u) {
+                ++jj;
+                rk += RB[b][jj];
+            }
+        const float val = table[off[pc] + rk];
+        if (fbits(val) != kAbsentBits) present.set(t);
+    }
+}
+
 struct ScoreArgs {
     const double *gram;      // n x n row-major
     const uint32_t *binom;   // [64][kBinomK]
@@ -229,31 +333,34 @@ struct ScoreArgs {
     double N;
     double lambda;
     int n, nv, S;
+    int variant;  // bit 0: unrolled presence (L <= 6), bit 1: stack-machine recursion
 };
 
-// LDS carve: gram | binom | work | tbl_off   (all offsets 16-B aligned)
+// LDS carve: gram | binom | work | tbl_off | recursion stack (16-B aligned)
 struct LdsLayout {
-    int gram, binom, work, toff, total;
+    int gram, binom, work, toff, stack, total;
 };
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
-__host__ __device__ inline LdsLayout lds_layout(int n, int nv, int S) {
+__host__ __device__ inline LdsLayout lds_layout(int n, int nv, int S, int L) {
     LdsLayout l;
     l.gram = 0;
     l.binom = align16(l.gram + n * n * 8);
     l.work = align16(l.binom + 64 * kBinomK * 4);
     l.toff = align16(l.work + (nv + 1) * 8);
-    l.total = align16(l.toff + (nv * S + 1) * 8);
+    l.stack = align16(l.toff + (nv * S + 1) * 8);
+    l.total = l.stack + L * kBlock * 8;
     return l;
 }
 
 template <int L, int PHASE>  // PHASE 0: sets containing variable 0; 1: the rest
 __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const LdsLayout lay = lds_layout(a.n, a.nv, a.S);
+    const LdsLayout lay = lds_layout(a.n, a.nv, a.S, L);
     double *g = reinterpret_cast<double *>(smem + lay.gram);
     uint32_t *binom = reinterpret_cast<uint32_t *>(smem + lay.binom);
     uint64_t *work = reinterpret_cast<uint64_t *>(smem + lay.work);
     uint64_t *toff = reinterpret_cast<uint64_t *>(smem + lay.toff);
+    uint64_t *stk = reinterpret_cast<uint64_t *>(smem + lay.stack);
     for (int i = threadIdx.x; i < a.n * a.n; i += kBlock) g[i] = a.gram[i];
     for (int i = threadIdx.x; i < 64 * kBinomK; i += kBlock) binom[i] = a.binom[i];
     for (int i = threadIdx.x; i <= a.nv; i += kBlock) work[i] = a.work[i];
@@ -362,24 +469,33 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         // presence of every candidate key in the cache as it stands now
         Bits<W> present;
         present.clear();
-        const uint32_t full = 1u << q;
-#pragma nounroll
-        for (uint32_t t = 1; t < full; ++t) {
-            const int pc = __builtin_popcount(t);
-            bool cand = pc <= L && t != Plocal && (z || !(t & 1u));
-            if (pc == L) cand = cand && PHASE == 1 && (t & 1u);
-            if (!cand) continue;
-            uint64_t rk = 0;
-            uint32_t rem = t;
-            int j = 0;
-            while (rem) {
-                const int lb = __builtin_ctz(rem);
-                rem &= rem - 1;
-                ++j;
-                rk += B(binom, (int)((cpack >> (6 * lb)) & 63ull), j);
+        bool unrolled = false;
+        if constexpr (L <= 6) {
+            if (a.variant & 1) {
+                presence_unrolled<L, PHASE, (PHASE == 0 ? L : L + 1), W>(present, binom, cpack, z, a.table, toff + vbase);
+                unrolled = true;
             }
-            const float val = a.table[toff[vbase + pc] + rk];
-            if (fbits(val) != kAbsentBits) present.set(t);
+        }
+        if (!unrolled) {
+            const uint32_t full = 1u << q;
+    #pragma nounroll
+            for (uint32_t t = 1; t < full; ++t) {
+                const int pc = __builtin_popcount(t);
+                bool cand = pc <= L && t != Plocal && (z || !(t & 1u));
+                if (pc == L) cand = cand && PHASE == 1 && (t & 1u);
+                if (!cand) continue;
+                uint64_t rk = 0;
+                uint32_t rem = t;
+                int j = 0;
+                while (rem) {
+                    const int lb = __builtin_ctz(rem);
+                    rem &= rem - 1;
+                    ++j;
+                    rk += B(binom, (int)((cpack >> (6 * lb)) & 63ull), j);
+                }
+                const float val = a.table[toff[vbase + pc] + rk];
+                if (fbits(val) != kAbsentBits) present.set(t);
+            }
         }
 
         Bits<W> checked, visited;
@@ -389,7 +505,8 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         uint32_t pvtop = 0;
 #pragma unroll
         for (int i = 0; i < L; ++i) pvtop |= (uint32_t)(i + (v0inP ? 0 : 1)) << (4 * i);
-        best_subset<L, W>(Plocal, pvtop, present, checked, visited);
+        if (a.variant & 2) best_subset_stack<L, W>(Plocal, pvtop, present, checked, visited, stk);
+        else best_subset<L, W>(Plocal, pvtop, present, checked, visited);
 
         float best = 0.0f;
 #pragma unroll
@@ -712,7 +829,7 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     sa.n = n;
     sa.nv = nv;
     sa.S = S;
-    const LdsLayout lay = lds_layout(n, nv, S);
+    sa.variant = c->score_variant;
     for (int L = 1; L <= kmax; ++L)
         for (int ph = 0; ph < 2; ++ph) {
             const uint64_t *w = &work[((size_t)L * 2 + ph) * (nv + 1)];
@@ -721,6 +838,7 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
             sa.work = c->d_work.p + ((size_t)L * 2 + ph) * (nv + 1);
             const uint64_t blocks = (cnt + kBlock - 1) / kBlock;
             if (blocks > 0x7fffffffull) return set_err(c, ULG_ERR_UNSUPPORTED, "ulg_cbic_score: layer too large");
+            const LdsLayout lay = lds_layout(n, nv, S, L);
             prof_begin(c, kLayerNames[ph][L]);
             hipLaunchKernelGGL(layer_kernel(L, ph), dim3((unsigned)blocks), dim3(kBlock), (size_t)lay.total, c->stream, sa);
             prof_end(c);

@@ -48,6 +48,7 @@ def lib():
         L.ulg_pdb_build.argtypes = [P, I, C.c_uint64, C.c_uint64]
         L.ulg_pdb_query.argtypes = [P, I64, P, P, P]
         L.ulg_astar.argtypes = [P, P, I, I, P, P, C.POINTER(F), C.POINTER(I64), C.c_char_p, I64]
+        L.ulg_set_option.argtypes = [P, C.c_char_p, I64]
         L.ulg_profile_enable.argtypes = [P, I]
         L.ulg_profile_get.argtypes = [P, C.c_char_p, C.POINTER(D), C.POINTER(I64), C.POINTER(D)]
         L.ulg_profile_dump.argtypes = [P, C.c_char_p, I64]
@@ -196,6 +197,9 @@ class Context:
                                     len(buf) if buf is not None else 0), "ulg_astar")
         return {"vpar": vpar, "order": order, "cost": cost.value, "expanded": exp.value,
                 "net_text": buf.value.decode() if buf is not None else None}
+
+    def set_option(self, name: str, value: int):
+        self._check(lib().ulg_set_option(self._h, name.encode(), int(value)), "ulg_set_option")
 
     # ---- profiling ----------------------------------------------------------
     def profile(self, on: bool = True):
