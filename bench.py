@@ -31,6 +31,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "urlearning-cpp_amd"))
 
+import shard  # noqa: E402
 import synth  # noqa: E402
 import ulg  # noqa: E402
 
@@ -176,7 +177,7 @@ def main():
     ctx.load(X, lam)
     cands_all = [(1 << n) - 1] * n
     if args.mode == "shard":
-        variables = [v for v in range(n) if v % ws == rank]
+        variables = shard.stripe(n, ws, rank)
     else:
         variables = list(range(n))
     cands = [cands_all[v] for v in variables]
@@ -185,21 +186,12 @@ def main():
     def step():
         stored, scored = ctx.score(variables, cands, k)
         if args.mode == "shard" and ws > 1:
-            # one RCCL all_gather of the per-variable (set, score) lists
-            cnt = torch.tensor([stored], dtype=torch.int64, device="cuda")
-            cnts = [torch.zeros_like(cnt) for _ in range(ws)]
-            dist.all_gather(cnts, cnt)
-            mx = int(max(int(c.item()) for c in cnts))
+            # one RCCL all-gather of the per-variable (set, score) lists (shard.py)
             sets_t = torch.empty(max(stored, 1), dtype=torch.int64, device="cuda")
             sc_t = torch.empty(max(stored, 1), dtype=torch.float32, device="cuda")
             off_t = torch.empty(len(variables) + 1, dtype=torch.int64, device="cuda")
             ctx.fetch_device(sets_t.data_ptr(), sc_t.data_ptr(), off_t.data_ptr())
-            packed = torch.zeros(mx, 3, dtype=torch.int32, device="cuda")
-            if stored:
-                packed[:stored, 0:2] = sets_t[:stored].view(torch.int32).view(stored, 2)
-                packed[:stored, 2] = sc_t[:stored].view(torch.int32)
-            out = torch.empty(ws * mx, 3, dtype=torch.int32, device="cuda")
-            dist.all_gather_into_tensor(out, packed)
+            shard.allgather_lists(shard.pack_device(variables, off_t, sets_t, sc_t), ws)
         return scored
 
     for _ in range(args.warmup):
