@@ -139,6 +139,16 @@ int ora_astar(ora_search *s, const ora_varset *edges, int pd_count,
               ora_varset *vpar, int *order, float *goal_cost,
               int64_t *expanded, char *net_text, int64_t net_cap);
 
+/* triplet_astar's astar() (astar/triplet_astar.cpp:991-1622): A* (with
+ * closed-node re-opening and a PDB per cluster) on every triple's cluster,
+ * v-structure / unfaithful-edge bookkeeping, Meek rules 2-4.  directed_graph
+ * (n*n, row-major) receives netFile.csv: (i,j)=1 means i -> j, both set =
+ * undirected.  edges == NULL means no skeleton (every variable a neighbour
+ * of every variable, itself included).  A* results are memoised per cluster
+ * (deterministic); astar_runs counts the reference's calls. */
+int ora_triplet_astar(ora_search *s, const ora_varset *edges, int pd_count, int *directed_graph,
+                      int64_t *astar_runs, int64_t *distinct_runs, int64_t *expanded);
+
 #ifdef __cplusplus
 }
 #endif

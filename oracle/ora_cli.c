@@ -167,3 +167,54 @@ int main(int argc, char **argv) {
     return rc == 0 ? 0 : 1;
 }
 #endif
+
+#ifdef ORA_TRIPLET
+/* ref_triplet <in.pss> [-k skeleton] [-n netFile] [-a pdCount]
+ * (astar/triplet_astar.cpp:991-1687): netFile.csv = directed_graph. */
+int main(int argc, char **argv) {
+    const char *pss = NULL, *skel = "", *net = "";
+    int pd = 2;
+    for (int i = 1; i < argc; i++) {
+        const char *a = argv[i];
+        if (!strcmp(a, "-k") || !strncmp(a, "--skeleton", 10)) skel = opt_val(argc, argv, &i);
+        else if (!strcmp(a, "-n") || !strncmp(a, "--netFile", 9)) net = opt_val(argc, argv, &i);
+        else if (!strcmp(a, "-a") || !strncmp(a, "--argument", 10)) pd = atoi(opt_val(argc, argv, &i));
+        else if (!strcmp(a, "-i") || !strcmp(a, "-f") || !strcmp(a, "-l") || !strcmp(a, "-b") ||
+                 !strcmp(a, "-e") || !strcmp(a, "-r") || !strcmp(a, "-w") || !strcmp(a, "-p") || !strcmp(a, "-s"))
+            (void)opt_val(argc, argv, &i);
+        else if (a[0] == '-' && a[1]) fprintf(stderr, "ref_triplet: option %s ignored\n", a);
+        else if (!pss) pss = a;
+    }
+    if (!pss) { fprintf(stderr, "usage: ref_triplet in.pss [-k skel] [-n netFile] [-a 2]\n"); return 2; }
+    ora_pss p;
+    if (ora_pss_read(pss, &p) != 0) { fprintf(stderr, "ref_triplet: cannot read %s\n", pss); return 1; }
+    const int n = p.n;
+    ora_search *s = ora_search_create(n, p.offsets, p.sets, p.costs);
+    ora_varset edges[64];
+    int good = 0;
+    if (skel && *skel) good = ora_skeleton_read(skel, n, edges, 64) >= 0;
+    int *dg = (int *)calloc((size_t)(n * n), sizeof(int));
+    int64_t runs = 0, distinct = 0, expanded = 0;
+    double t0 = now_s();
+    int rc = ora_triplet_astar(s, good ? edges : NULL, pd, dg, &runs, &distinct, &expanded);
+    double t1 = now_s();
+    printf("ref_triplet: A* runs %lld (distinct clusters %lld), expanded %lld, time %.3fs\n", (long long)runs,
+           (long long)distinct, (long long)expanded, t1 - t0);
+    if (net && *net) {
+        FILE *f = fopen(net, "w");
+        if (f) fclose(f); /* the reference leaves netFile empty (post-processing commented out) */
+        char csv[4096];
+        snprintf(csv, sizeof csv, "%s.csv", net);
+        f = fopen(csv, "w");
+        if (f) {
+            for (int i = 0; i < n; i++)
+                for (int j = 0; j < n; j++) fprintf(f, "%d%c", dg[i * n + j], j == n - 1 ? '\n' : ',');
+            fclose(f);
+        }
+    }
+    free(dg);
+    ora_search_free(s);
+    ora_pss_free(&p);
+    return rc == 0 ? 0 : 1;
+}
+#endif

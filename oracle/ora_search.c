@@ -547,3 +547,328 @@ int ora_astar(ora_search *s, const ora_varset *edges, int pd_count,
     if (hang) return 2;
     return fail;
 }
+
+/* ---- triplet_astar (astar/triplet_astar.cpp) ------------------------------ */
+
+/* run_astar_on_one_scc of triplet_astar.cpp:285-674: a static PDB built on
+ * (ancestors, the_scc) for every call, no skeleton filter (:411-424 is
+ * commented out), EdgeConstraints with no ancestors (always satisfied), and
+ * closed nodes RE-OPENED when a strictly better g arrives (:556-576).
+ * Writes op[v] / oc[v] (optimal parents / children) for the cluster. */
+static int triplet_astar_one(ora_search *s, int pd_count, vs_t ancestors, vs_t the_scc,
+                             vs_t *op, vs_t *oc, int64_t *expanded, int *hang) {
+    const int n = s->n;
+    if (ora_pdb_build(s, pd_count, ancestors, the_scc) != 0) return -1;
+    for (int v = 0; v < n; v++) { op[v] = 0; oc[v] = 0; }
+    omap generated;
+    omap_init(&generated, 1 << 12);
+    pool_t pool;
+    memset(&pool, 0, sizeof pool);
+    heap_t open;
+    memset(&open, 0, sizeof open);
+    const vs_t r1 = the_scc >> 1;
+    node_t *root = pool_new(&pool);
+    root->g = 0.0f; root->h = 0.0f; root->sub = ancestors;
+    root->leaf = (uint8_t)(r1 ? __builtin_ctzll(r1) + 1 : 0);
+    root->pqPos = 0;
+    hp_push(&open, root);
+    node_t *goal = NULL;
+    const vs_t allVariables = ancestors | the_scc;
+    const float upperBound = FLT_MAX;
+    int64_t nexp = 0;
+    while (open.size > 0) {
+        node_t *u = hp_pop(&open);
+        nexp++;
+        const vs_t variables = u->sub;
+        if (variables == allVariables) { goal = u; break; }
+        if (u->g + u->h > upperBound) break;
+        u->pqPos = -2;
+        for (int leaf = 0; leaf < n; leaf++) {
+            if ((variables >> leaf) & 1ULL) continue;
+            if (!((the_scc >> leaf) & 1ULL)) continue;
+            const vs_t nv = variables | (1ULL << leaf);
+            uint64_t idx;
+            node_t *succ = NULL;
+            if (omap_get(&generated, nv, &idx)) succ = (node_t *)(uintptr_t)idx;
+            int64_t b;
+            if (succ == NULL) {
+                const float g = u->g + spl_get(s, leaf, nv, &b);
+                int complete = 0;
+                const float h = ora_pdb_h(s, nv, &complete);
+                succ = pool_new(&pool);
+                succ->g = g; succ->h = h; succ->sub = nv; succ->leaf = (uint8_t)leaf; succ->pqPos = 0;
+                hp_push(&open, succ);
+                omap_put(&generated, nv, (uint64_t)(uintptr_t)succ);
+                continue;
+            }
+            const float g = u->g + spl_get(s, leaf, variables, &b);
+            if (g < succ->g) {
+                succ->leaf = (uint8_t)leaf;
+                succ->g = g;
+                if (succ->pqPos == -2) { succ->pqPos = 0; hp_push(&open, succ); }
+                else hp_update(&open, succ);
+            }
+        }
+    }
+    *expanded += nexp;
+    if (open.hang) *hang = 1;
+    int ok = 0;
+    if (goal) {
+        ok = 1;
+        /* reconstructSolution with children (triplet_astar.cpp:172-224) */
+        const int count = popc64(the_scc);
+        int total[64];
+        vs_t opt[64], ch[64];
+        int var2ord[64];
+        for (int i = 0; i < 64; i++) { total[i] = 0; opt[i] = 0; ch[i] = 0; var2ord[i] = -1; }
+        vs_t remaining = goal->sub;
+        node_t *current = goal;
+        for (int i = 0; i < count && current; i++) {
+            const int leaf = current->leaf;
+            total[count - 1 - i] = leaf;
+            var2ord[leaf] = count - 1 - i;
+            int64_t b;
+            (void)spl_get(s, leaf, remaining, &b);
+            opt[count - 1 - i] = (b < s->spl[leaf].count) ? s->spl[leaf].parents[b] : 0;
+            remaining ^= 1ULL << leaf;
+            uint64_t idx;
+            current = omap_get(&generated, remaining, &idx) ? (node_t *)(uintptr_t)idx : NULL;
+        }
+        for (int i = 0; i < count; i++)
+            for (int j = 0; j < n; j++)
+                if (((opt[i] >> j) & 1ULL) && var2ord[j] >= 0) ch[var2ord[j]] |= 1ULL << total[i];
+        const int num_vars = popc64(allVariables);
+        for (int v = 0; v < num_vars; v++) { op[total[v]] = opt[v]; oc[total[v]] = ch[v]; }
+    }
+    omap_free(&generated);
+    pool_free(&pool);
+    free(open.a);
+    return ok;
+}
+
+typedef struct {
+    ora_search *s;
+    int n, pd_count;
+    vs_t *nb;             /* skeleton neighbours (mutable) */
+    vs_t *clusters;
+    int *dg;              /* directed_graph, n x n */
+    vs_t *vstr_parents;
+    int num_v_structures;
+    omap triplets_checked;
+    /* memo: the A* result depends only on the cluster */
+    omap memo;
+    vs_t *memo_op, *memo_oc;
+    int memo_count, memo_cap;
+    int64_t runs, distinct_runs, expanded;
+    int hang;
+} trip_t;
+
+#define DG(t, a, b) ((t)->dg[(a) * (t)->n + (b)])
+
+static int trip_astar_cached(trip_t *t, vs_t cluster, vs_t **op, vs_t **oc) {
+    uint64_t slot;
+    t->runs++;
+    if (!omap_get(&t->memo, cluster, &slot)) {
+        if (t->memo_count == t->memo_cap) {
+            t->memo_cap = t->memo_cap ? 2 * t->memo_cap : 64;
+            t->memo_op = (vs_t *)realloc(t->memo_op, sizeof(vs_t) * 64 * (size_t)t->memo_cap);
+            t->memo_oc = (vs_t *)realloc(t->memo_oc, sizeof(vs_t) * 64 * (size_t)t->memo_cap);
+        }
+        slot = (uint64_t)t->memo_count++;
+        triplet_astar_one(t->s, t->pd_count, 0ULL, cluster, t->memo_op + 64 * slot, t->memo_oc + 64 * slot,
+                          &t->expanded, &t->hang);
+        t->distinct_runs++;
+        omap_put(&t->memo, cluster, slot);
+    }
+    *op = t->memo_op + 64 * slot;
+    *oc = t->memo_oc + 64 * slot;
+    return 0;
+}
+
+/* process_triple (triplet_astar.cpp:811-989) */
+static void process_triple(trip_t *t, int i, int vj, int vk) {
+    uint64_t arr[3] = {(uint64_t)i, (uint64_t)vj, (uint64_t)vk};
+    for (int a = 0; a < 3; a++)
+        for (int b = a + 1; b < 3; b++)
+            if ((int)arr[b] < (int)arr[a]) { uint64_t x = arr[a]; arr[a] = arr[b]; arr[b] = x; }
+    const vs_t big = t->clusters[i] | t->clusters[vj] | t->clusters[vk];
+    if (popc64(big) > 26) return;
+    const uint64_t key = (arr[0] << 40) + (arr[1] << 20) + arr[2];
+    if (omap_get(&t->triplets_checked, key, NULL)) return;
+    omap_put(&t->triplets_checked, key, 1);
+    vs_t *op, *oc;
+    trip_astar_cached(t, big, &op, &oc);
+    const int parents_vj_vk = ((op[i] >> vj) & 1ULL) && ((op[i] >> vk) & 1ULL);
+    const int parents_i_vj = ((op[vk] >> i) & 1ULL) && ((op[vk] >> vj) & 1ULL);
+    const int parents_i_vk = ((op[vj] >> i) & 1ULL) && ((op[vj] >> vk) & 1ULL);
+    if (parents_vj_vk) {
+        t->num_v_structures++;
+        DG(t, vj, i) = 1; DG(t, vk, i) = 1; DG(t, i, vj) = 0; DG(t, i, vk) = 0;
+        if ((((op[vj] >> vk) & 1ULL) || ((op[vk] >> vj) & 1ULL)) && 0 == DG(t, vk, vj) && 0 == DG(t, vj, vk)) {
+            DG(t, vk, vj) = 1; DG(t, vj, vk) = 1;
+        }
+        t->vstr_parents[i] |= 1ULL << vk;
+        t->vstr_parents[i] |= 1ULL << vj;
+    } else if (parents_i_vj) {
+        t->num_v_structures++;
+        DG(t, vj, vk) = 1; DG(t, i, vk) = 1; DG(t, vk, i) = 0; DG(t, vk, vj) = 0;
+        if ((((op[vj] >> i) & 1ULL) || ((op[i] >> vj) & 1ULL)) && 0 == DG(t, i, vj) && 0 == DG(t, vj, i)) {
+            DG(t, i, vj) = 1; DG(t, vj, i) = 1;
+        }
+        t->vstr_parents[vk] |= 1ULL << i;
+        t->vstr_parents[vk] |= 1ULL << vj;
+    } else if (parents_i_vk) {
+        t->num_v_structures++;
+        DG(t, vk, vj) = 1; DG(t, i, vj) = 1; DG(t, vj, i) = 0; DG(t, vj, vk) = 0;
+        if ((((op[vk] >> i) & 1ULL) || ((op[i] >> vk) & 1ULL)) && 0 == DG(t, i, vk) && 0 == DG(t, vk, i)) {
+            DG(t, i, vk) = 1; DG(t, vk, i) = 1;
+        }
+        t->vstr_parents[vj] |= 1ULL << i;
+        t->vstr_parents[vj] |= 1ULL << vk;
+    } else {
+        if ((((op[vj] >> vk) & 1ULL) || ((op[vk] >> vj) & 1ULL)) && 0 == DG(t, vk, vj) && 0 == DG(t, vj, vk)) {
+            DG(t, vk, vj) = 1; DG(t, vj, vk) = 1;
+        }
+        if ((((op[vj] >> i) & 1ULL) || ((op[i] >> vj) & 1ULL)) && 0 == DG(t, i, vj) && 0 == DG(t, vj, i)) {
+            DG(t, i, vj) = 1; DG(t, vj, i) = 1;
+        }
+        if ((((op[vk] >> i) & 1ULL) || ((op[i] >> vk) & 1ULL)) && 0 == DG(t, i, vk) && 0 == DG(t, vk, i)) {
+            DG(t, i, vk) = 1; DG(t, vk, i) = 1;
+        }
+    }
+}
+
+static void trip_add_edge(trip_t *t, int a, int b) {
+    t->nb[a] |= 1ULL << b;
+    t->nb[b] |= 1ULL << a;
+    t->clusters[a] = t->nb[a];
+    t->clusters[b] = t->nb[b];
+}
+
+/* astar() of triplet_astar.cpp:991-1622 */
+int ora_triplet_astar(ora_search *s, const ora_varset *edges, int pd_count, int *directed_graph,
+                      int64_t *astar_runs, int64_t *distinct_runs, int64_t *expanded) {
+    const int n = s->n;
+    trip_t T;
+    memset(&T, 0, sizeof T);
+    T.s = s; T.n = n; T.pd_count = pd_count;
+    T.nb = (vs_t *)calloc(64, sizeof(vs_t));
+    T.clusters = (vs_t *)calloc(64, sizeof(vs_t));
+    T.vstr_parents = (vs_t *)calloc(64, sizeof(vs_t));
+    T.dg = directed_graph;
+    for (int a = 0; a < n * n; a++) T.dg[a] = 0;
+    omap_init(&T.triplets_checked, 1024);
+    omap_init(&T.memo, 64);
+    const vs_t all = (n >= 64) ? ~0ULL : ((1ULL << n) - 1ULL);
+    /* no skeleton: Skeleton::get_neighbors returns all_bit_set (self included) */
+    for (int v = 0; v < n; v++) T.nb[v] = edges ? edges[v] : all;
+    for (int v = 0; v < n; v++) T.clusters[v] = T.nb[v] | (1ULL << v);
+    for (int i = 0; i < n; i++) {
+        const vs_t pin = T.nb[i];
+        int parents[64], np = 0;
+        for (int j = 0; j < n; j++)
+            if ((pin >> j) & 1ULL) parents[np++] = j;
+        int unc[65], nu = 0;
+        for (int j = 0; j < np; j++) unc[nu++] = parents[j];
+        if (nu == 1 && np > 1) {
+            for (int m = 0; m < np; m++)
+                if (parents[m] != unc[0]) { unc[nu++] = parents[m]; break; }
+        } else if (nu == 1 && np == 1 && i < parents[0] && popc64(T.nb[parents[0]]) == 1) {
+            const int vj = unc[0];
+            int64_t b;
+            (void)spl_get(s, i, 1ULL << vj, &b);
+            const vs_t thep = (b < s->spl[i].count) ? s->spl[i].parents[b] : 0;
+            if (thep == (1ULL << vj)) { DG(&T, i, vj) = 1; DG(&T, vj, i) = 1; }
+        }
+        for (int j = 0; j < nu; j++) {
+            const int vj = unc[j];
+            for (int k = 0; k < j; k++) {
+                const int vk = unc[k];
+                process_triple(&T, i, vj, vk);
+                if (!((T.nb[vj] >> vk) & 1ULL) && (DG(&T, vj, vk) || DG(&T, vk, vj))) trip_add_edge(&T, vj, vk);
+            }
+        }
+    }
+    /* unfaithful-edge fixpoint (triplet_astar.cpp:1256-1290) */
+    int delta;
+    do {
+        delta = 0;
+        for (int i = 0; i < n; i++) {
+            for (int j = 0; j < i; j++) {
+                const int unfaithful = (DG(&T, i, j) || DG(&T, j, i)) && 0 == ((T.nb[i] >> j) & 1ULL);
+                delta += unfaithful;
+                if (!unfaithful) continue;
+                trip_add_edge(&T, i, j);
+                for (int k = 0; k < n; k++)
+                    if (k != i && k != j && (((T.clusters[i] >> k) & 1ULL) || ((T.clusters[j] >> k) & 1ULL)))
+                        process_triple(&T, i, j, k);
+            }
+        }
+    } while (delta > 0);
+    /* Meek rules 2, 3, 4 until nothing changes (triplet_astar.cpp:1297-1478) */
+    for (int iter = 0; iter < n; iter++) {
+        int num_oriented = 0;
+        for (int v = 0; v < n; v++) { /* rule 2 */
+            int ins[64], outs[64], ni = 0, no = 0;
+            for (int j = 0; j < n; j++) {
+                if (1 == DG(&T, v, j) && 0 == DG(&T, j, v)) outs[no++] = j;
+                else if (1 == DG(&T, j, v) && 0 == DG(&T, v, j)) ins[ni++] = j;
+            }
+            if (ni == 0 || no == 0) continue;
+            for (int a = 0; a < ni; a++)
+                for (int b = 0; b < no; b++) {
+                    const int parent = ins[a], child = outs[b];
+                    if (DG(&T, parent, child) && DG(&T, child, parent)) {
+                        DG(&T, parent, child) = 1; DG(&T, child, parent) = 0; num_oriented++;
+                    }
+                }
+        }
+        for (int v = 0; v < n; v++) { /* rule 3 */
+            const int num_vps = popc64(T.vstr_parents[v]);
+            int vp[64], und[64], nvp = 0, nun = 0;
+            for (int j = 0; j < n; j++) {
+                if ((T.vstr_parents[v] >> j) & 1ULL) vp[nvp++] = j;
+                if (1 == DG(&T, v, j) && 1 == DG(&T, j, v)) und[nun++] = j;
+            }
+            if (num_vps < 2 || nun == 0) continue;
+            for (int a = 0; a < nun; a++) {
+                const int neighbor = und[a];
+                int cnt = 0;
+                for (int b = 0; b < nvp; b++)
+                    if (1 == DG(&T, vp[b], neighbor) && 1 == DG(&T, neighbor, vp[b])) cnt++;
+                if (cnt >= 2) { DG(&T, v, neighbor) = 0; num_oriented++; }
+            }
+        }
+        for (int v = 0; v < n; v++) { /* rule 4 */
+            int ins[64], outs[64], und[64], ni = 0, no = 0, nun = 0;
+            for (int j = 0; j < n; j++) {
+                if (1 == DG(&T, v, j) && 0 == DG(&T, j, v)) outs[no++] = j;
+                else if (1 == DG(&T, j, v) && 0 == DG(&T, v, j)) ins[ni++] = j;
+                else if (1 == DG(&T, v, j) && 1 == DG(&T, j, v)) und[nun++] = j;
+            }
+            if (no == 0 || ni == 0 || nun == 0) continue;
+            for (int a = 0; a < nun; a++) {
+                const int neighbor = und[a];
+                int nd = 0;
+                for (int b = 0; b < ni; b++)
+                    if (1 == DG(&T, neighbor, ins[b]) && 1 == DG(&T, ins[b], neighbor)) nd++;
+                if (nd == 0) continue;
+                for (int b = 0; b < no; b++) {
+                    const int child = outs[b];
+                    if (0 == DG(&T, neighbor, child) || 0 == DG(&T, child, neighbor)) continue;
+                    num_oriented++;
+                    DG(&T, child, neighbor) = 0;
+                }
+            }
+        }
+        if (num_oriented == 0) break;
+    }
+    if (astar_runs) *astar_runs = T.runs;
+    if (distinct_runs) *distinct_runs = T.distinct_runs;
+    if (expanded) *expanded = T.expanded;
+    omap_free(&T.triplets_checked);
+    omap_free(&T.memo);
+    free(T.memo_op); free(T.memo_oc);
+    free(T.nb); free(T.clusters); free(T.vstr_parents);
+    return T.hang ? 2 : 0;
+}

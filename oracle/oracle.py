@@ -17,6 +17,7 @@ BUILD = os.path.join(HERE, "build")
 LIB = os.path.join(BUILD, "liboracle.so")
 REF_SCORE = os.path.join(BUILD, "ref_score")
 REF_ASTAR = os.path.join(BUILD, "ref_astar")
+REF_TRIPLET = os.path.join(BUILD, "ref_triplet")
 
 _lib = None
 
@@ -66,6 +67,7 @@ def lib():
         L.ora_pdb_value.argtypes = [P, I, U64]
         L.ora_pdb_value.restype = F
         L.ora_astar.argtypes = [P, P, I, P, P, C.POINTER(F), C.POINTER(I64), C.c_char_p, I64]
+        L.ora_triplet_astar.argtypes = [P, P, I, P, C.POINTER(I64), C.POINTER(I64), C.POINTER(I64)]
         _lib = L
     return _lib
 
@@ -202,6 +204,19 @@ class Search:
                              C.byref(cost), C.byref(exp), buf, len(buf))
         return {"rc": rc, "vpar": vpar, "order": order, "cost": cost.value, "expanded": exp.value,
                 "net_text": buf.value.decode()}
+
+
+def triplet(search, edges=None, pd_count=2):
+    n = search.n
+    dg = np.zeros(n * n, dtype=np.int32)
+    runs, distinct, exp = C.c_int64(), C.c_int64(), C.c_int64()
+    e = None
+    if edges is not None:
+        e = np.ascontiguousarray([int(x) for x in edges], dtype=np.uint64)
+    rc = lib().ora_triplet_astar(search.h, _p(e) if e is not None else None, pd_count, _p(dg), C.byref(runs),
+                                 C.byref(distinct), C.byref(exp))
+    return {"rc": rc, "mec": dg.reshape(n, n), "runs": runs.value, "distinct": distinct.value,
+            "expanded": exp.value}
 
 
 def dag_matrix(vpar, n):

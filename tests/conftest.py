@@ -53,3 +53,16 @@ def load_fig(fig):
 def fig_dag(fig):
     name = {1: "fig1_astar_dag_8000.csv", 2: "fig2_astar_dag_5000.csv"}[fig]
     return read_matrix(os.path.join(GOLDEN, name))
+
+
+def fig_mec(fig):
+    name = {1: "fig1_triplet_mec_8000.csv", 2: "fig2_triplet_mec_5000.csv"}[fig]
+    return read_matrix(os.path.join(GOLDEN, name))
+
+
+# The skeleton each triplet_mec fixture is reproduced with.  The fixtures do not
+# record it; Figure 1's fully oriented MEC needs the all-ones matrix (diagonal
+# included: the degenerate triples (i, i, k) orient every A* edge), Figure 2's
+# CPDAG-shaped MEC needs the off-diagonal skeleton.  Both give the A* DAG fixture.
+TRIPLET_SKELETON = {1: "1,1,1,1\n1,1,1,1\n1,1,1,1\n1,1,1,1\n",
+                    2: "0,1,1,1\n1,0,1,1\n1,1,0,1\n1,1,1,0\n"}

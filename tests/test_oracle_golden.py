@@ -7,7 +7,7 @@ import sys
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, fig_dag, load_fig, read_matrix
+from conftest import GOLDEN, TRIPLET_SKELETON, fig_dag, fig_mec, load_fig, read_matrix
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "urlearning-cpp_amd"))
 import synth  # noqa: E402
@@ -116,3 +116,36 @@ def test_pdb_groups_split(oracle_built):
     assert comp == 0 and h <= 0
     h, comp = srch.pdb_h((1 << n) - 1)
     assert comp == 1 and h == 0
+
+
+@pytest.mark.parametrize("fig", [1, 2])
+@pytest.mark.parametrize("lam", ["0.5", "1", "2"])
+def test_oracle_cli_reproduces_triplet_mec(oracle_built, tmp_path, fig, lam):
+    """ref_score -> .pss -> ref_triplet reproduces triplet_data/Figure_*/triplet_mec_*.csv
+    (astar/triplet_astar.cpp:991-1687; netFile.csv = directed_graph, netFile left empty)."""
+    o = oracle_built
+    skel = tmp_path / "skel.csv"
+    skel.write_text(TRIPLET_SKELETON[fig])
+    pss = tmp_path / "s.pss"
+    net = tmp_path / "net"
+    subprocess.run([o.REF_SCORE, os.path.join(GOLDEN, FIG_CSV[fig]), str(pss), "-f", "cBIC", "--lambda", lam,
+                    "-k", str(skel)], check=True, stdout=subprocess.DEVNULL)
+    subprocess.run([o.REF_TRIPLET, str(pss), "-k", str(skel), "-n", str(net)], check=True, capture_output=True)
+    assert read_matrix(str(net) + ".csv") == fig_mec(fig)
+    assert net.read_text() == ""
+    # the same skeleton also reproduces the plain A* fixture
+    subprocess.run([o.REF_ASTAR, str(pss), "-k", str(skel), "-n", str(tmp_path / "a")], check=True,
+                   stdout=subprocess.DEVNULL)
+    assert read_matrix(str(tmp_path / "a.csv")) == fig_dag(fig)
+
+
+def test_oracle_triplet_api_memoizes_clusters(oracle_built):
+    """Every triple on a 4-variable full skeleton sorts into the one cluster
+    {0,1,2,3}: one distinct A* search, many memoized runs."""
+    o = oracle_built
+    ds = o.Dataset(load_fig(1))
+    offs, sets, scores = ds.score_all(2.0, [0xF] * 4, 3)
+    costs = np.array([o.quantize(float(s)) for s in scores], dtype=np.float32)
+    res = o.triplet(o.Search(4, offs, sets, costs), edges=[0xF] * 4)
+    assert res["rc"] == 0 and res["distinct"] == 1 and res["runs"] > 1
+    assert res["mec"].tolist() == fig_mec(1)
