@@ -26,6 +26,9 @@
  *                        (heuristic/static_pattern_database.cpp:82-247).
  *   ulg_astar            replaces run_astar_on_one_scc
  *                        (astar/astar_main.cpp:216-546).
+ *   ulg_triplet_astar    replaces triplet_astar's astar() driver and its
+ *                        re-opening run_astar_on_one_scc
+ *                        (astar/triplet_astar.cpp:285-674,811-1622).
  *
  * Conventions (mirroring the reference's): the caller owns host buffers;
  * device memory is owned by the context; hot calls report errors by an int
@@ -140,6 +143,21 @@ int ulg_pdb_query(ulg_ctx *ctx, int64_t count, const uint64_t *S, float *h,
 int ulg_astar(ulg_ctx *ctx, const uint64_t *edges, int pd_count, int mode,
               uint64_t *vpar, int *order, float *goal_cost, int64_t *expanded,
               char *net_text, int64_t net_cap);
+
+/* triplet_astar's astar() (astar/triplet_astar.cpp:991-1622): for every
+ * variable i and pair of its skeleton neighbours, an exact-order A* with
+ * re-opening (run_astar_on_one_scc, :285-674) over the union of the three
+ * clusters (skipped above 26 variables, :837-844; one search per distinct
+ * cluster -- the result depends on the cluster only), v-structure and
+ * undirected-edge bookkeeping (process_triple, :811-989), the
+ * unfaithful-edge fixpoint (:1256-1290) and Meek rules 2-4 (:1297-1478).
+ * directed_graph (n*n ints, row-major) receives what netFile.csv holds:
+ * [i*n+j] = 1 iff the MEC has i -> j (both set = undirected).  edges as in
+ * ulg_astar (NULL = no skeleton: every row is the full set, self included).
+ * stats (optional, 3 entries): A* runs requested, distinct clusters
+ * searched, nodes expanded. */
+int ulg_triplet_astar(ulg_ctx *ctx, const uint64_t *edges, int pd_count,
+                      int *directed_graph, int64_t *stats);
 
 /* ---- tuning knobs -------------------------------------------------------
  * "score_variant" (0..3, default 1): bit 0 = fully unrolled presence gather

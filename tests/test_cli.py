@@ -1,4 +1,5 @@
-"""The drop-in command lines (urlearning-cpp_amd/bin/score, bin/astar): option
+"""The drop-in command lines (urlearning-cpp_amd/bin/score, bin/astar,
+bin/triplet_astar): option
 handling on the CPU, and the end-to-end CSV -> .pss -> netFile path on the
 GPU against the oracle's command lines and the golden DAGs."""
 import os
@@ -6,10 +7,11 @@ import subprocess
 
 import pytest
 
-from conftest import GOLDEN, PKG, fig_dag, read_matrix
+from conftest import GOLDEN, PKG, TRIPLET_SKELETON, fig_dag, fig_mec, read_matrix
 
 SCORE = os.path.join(PKG, "bin", "score")
 ASTAR = os.path.join(PKG, "bin", "astar")
+TRIPLET = os.path.join(PKG, "bin", "triplet_astar")
 FIG_CSV = {1: "fig1_raw_data_8000.csv", 2: "fig2_raw_data_5000.csv"}
 
 
@@ -18,7 +20,16 @@ def _run(cmd, **kw):
 
 
 def test_cli_binaries_built():
-    assert os.access(SCORE, os.X_OK) and os.access(ASTAR, os.X_OK)
+    assert os.access(SCORE, os.X_OK) and os.access(ASTAR, os.X_OK) and os.access(TRIPLET, os.X_OK)
+
+
+def test_triplet_help_and_option_errors(tmp_path):
+    r = _run([TRIPLET, "--help"])
+    assert r.returncode == 0 and "--skeleton" in r.stdout
+    r = _run([TRIPLET, str(tmp_path / "x.pss"), "-e", "dynamic"])
+    assert r.returncode == 2 and "static" in r.stderr
+    r = _run([TRIPLET, str(tmp_path / "missing.pss")])
+    assert r.returncode == 1 and "Could not open the score cache file" in r.stderr
 
 
 def test_score_rejects_other_scoring_functions():
@@ -67,3 +78,25 @@ def test_cli_end_to_end_matches_oracle_and_golden(tmp_path, oracle_built, fig, l
             subprocess.run([o.REF_ASTAR, str(pss), "-k", str(skel), "-n", str(ref_net)], check=True,
                            stdout=subprocess.DEVNULL)
             assert net.read_text() == ref_net.read_text()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fig", [1, 2])
+@pytest.mark.parametrize("lam", ["0.5", "1", "2"])
+def test_triplet_cli_reproduces_mec(tmp_path, oracle_built, fig, lam):
+    """score -> .pss -> triplet_astar: netFile.csv is the triplet_mec fixture,
+    netFile is left empty, and the oracle's ref_triplet agrees on the same .pss."""
+    o = oracle_built
+    csv = os.path.join(GOLDEN, FIG_CSV[fig])
+    skel = tmp_path / "skel.csv"
+    skel.write_text(TRIPLET_SKELETON[fig])
+    pss = tmp_path / "gpu.pss"
+    r = _run([SCORE, csv, str(pss), "-f", "cBIC", "--lambda", lam, "-k", str(skel)])
+    assert r.returncode == 0, r.stderr
+    net, ref_net = tmp_path / "net", tmp_path / "ref_net"
+    r = _run([TRIPLET, str(pss), "-k", str(skel), "-n", str(net)])
+    assert r.returncode == 0, r.stderr
+    assert read_matrix(str(net) + ".csv") == fig_mec(fig)
+    assert net.read_text() == ""
+    subprocess.run([o.REF_TRIPLET, str(pss), "-k", str(skel), "-n", str(ref_net)], check=True, stdout=subprocess.DEVNULL)
+    assert (tmp_path / "net.csv").read_text() == (tmp_path / "ref_net.csv").read_text()

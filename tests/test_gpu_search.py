@@ -44,6 +44,32 @@ def test_bestscore_tables_match_list_scan(ulg_ctx, oracle_built):
         assert int(p) == ep, (v, S, p, ep)
 
 
+def test_bestscore_tables_heterogeneous_supports(ulg_ctx, oracle_built):
+    """Supports of very different sizes (6..19 candidate parents, as a sparse
+    skeleton's 2-hop sets give): per-variable tables start at offsets that are
+    not aligned to their own size, and m > 14 exercises the strided zeta pass."""
+    o = oracle_built
+    n = 20
+    X, _ = synth.gaussian_sem(n, 2000, 9302)
+    rng = np.random.default_rng(11)
+    cands = []
+    for v in range(n):
+        others = [u for u in range(n) if u != v]
+        m = [6, 19, 9, 15, 17, 7, 16, 12, 18, 8, 14, 19, 6, 11, 15, 10, 17, 13, 9, 16][v]
+        pick = rng.choice(others, size=m, replace=False)
+        cands.append(int(sum(1 << int(u) for u in pick)))
+    offs, sets, scores, costs = _oracle_pipeline(o, X, 0.5, 2, cands)
+    ulg_ctx.search_load(offs, sets, costs)
+    srch = o.Search(n, offs, sets, costs)
+    vs = [int(v) for v in rng.integers(0, n, 20000)]
+    Ss = _random_subsets(rng, n, 20000)
+    gc, gp = ulg_ctx.bestscore(vs, Ss)
+    for v, S, c, p in zip(vs, Ss, gc, gp):
+        ec, ep = srch.bestscore(v, S)
+        assert np.float32(c) == np.float32(ec), (v, S, c, ec)
+        assert int(p) == ep, (v, S, p, ep)
+
+
 def test_bestscore_ties_fall_to_file_order(ulg_ctx, oracle_built):
     """Equal costs: the first set in file order wins (pinned N7)."""
     o = oracle_built

@@ -107,12 +107,15 @@ __global__ void __launch_bounds__(1024) zeta_strided_kernel(ZetaBArgs a) {
     const int G = std::min(kColBits, m - bit_lo);
     const int nlow = bit_lo - kRowBits;
     const uint64_t bid = blockIdx.x - a.blocks_prefix[v];
-    const uint64_t base = a.tb_off[v] + (((bid & ((1ull << nlow) - 1)) << kRowBits) | ((bid >> nlow) << (bit_lo + G)));
+    // tile origin inside v's table; v's table itself starts at tb_off[v], which
+    // is not aligned to 2^m when the supports differ in size: add, never OR
+    uint64_t *tv = a.table + a.tb_off[v];
+    const uint64_t base = ((bid & ((1ull << nlow) - 1)) << kRowBits) | ((bid >> nlow) << (bit_lo + G));
     const int rows = 1 << G;
     const int size = rows << kRowBits;
     for (int e = threadIdx.x; e < size; e += 1024) {
         const uint64_t hc = (uint64_t)(e >> kRowBits), lw = (uint64_t)(e & 15);
-        t[e] = a.table[base | (hc << bit_lo) | lw];
+        t[e] = tv[base | (hc << bit_lo) | lw];
     }
     __syncthreads();
     for (int j = 0; j < G; ++j) {
@@ -127,7 +130,7 @@ __global__ void __launch_bounds__(1024) zeta_strided_kernel(ZetaBArgs a) {
     }
     for (int e = threadIdx.x; e < size; e += 1024) {
         const uint64_t hc = (uint64_t)(e >> kRowBits), lw = (uint64_t)(e & 15);
-        a.table[base | (hc << bit_lo) | lw] = t[e];
+        tv[base | (hc << bit_lo) | lw] = t[e];
     }
 }
 

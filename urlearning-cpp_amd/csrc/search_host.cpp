@@ -17,205 +17,13 @@
 #include <cstdio>
 #include <cstring>
 
-#include "search_internal.h"
+#include "search_exact.h"
 
 using namespace ulg;
+using namespace ulg::exact;
 
 namespace {
 
-struct Node {
-    float g, h;
-    uint64_t sub;
-    uint8_t leaf;
-    int32_t pq;
-};
-
-bool g_have_bmi2 = __builtin_cpu_supports("bmi2");
-
-__attribute__((target("bmi2"))) inline uint64_t pext_bmi2(uint64_t x, uint64_t m) { return __builtin_ia32_pext_di(x, m); }
-
-// Host view of the best-score lattice: cost per subset of D_v.
-struct HostTables {
-    const float *cost;
-    const uint64_t *tb_off;
-    const uint64_t *support;
-    std::vector<int> hole;  // D_v == all \ {hole}: pext is a shift
-    uint64_t all;
-    int n;
-    const float *pd;
-    std::vector<uint64_t> groups;
-    std::vector<uint64_t> pd_off;
-
-    inline uint64_t index(int v, uint64_t S) const {
-        const uint64_t D = support[v];
-        S &= D;
-        const int h = hole[v];
-        if (h >= 0) return ((S >> (h + 1)) << h) | (S & ((1ull << h) - 1ull));
-        return g_have_bmi2 ? pext_bmi2(S, D) : pext64(S, D);
-    }
-    inline float bs(int v, uint64_t S) const { return cost[tb_off[v] + index(v, S)]; }
-    inline uint64_t gidx(uint64_t vs, uint64_t grp) const { return g_have_bmi2 ? pext_bmi2(vs, grp) : pext64(vs, grp); }
-    // StaticPatternDatabase::h (static_pattern_database.cpp:145-174)
-    inline float h(uint64_t S, bool *complete) const {
-        const uint64_t remaining = ~S & all;
-        float hv = 0.0f;
-        for (size_t g = 0; g < groups.size(); ++g) {
-            const uint64_t vs = groups[g] & remaining;
-            const float val = pd[pd_off[g] + gidx(vs, groups[g])];
-            if (vs == remaining) {
-                *complete = true;
-                return val;
-            }
-            hv += val;
-        }
-        return hv;
-    }
-};
-
-// generatedNodes (NodeMap): open addressing u64 -> node index
-struct NodeIndex {
-    std::vector<uint64_t> keys;
-    std::vector<uint32_t> vals;
-    uint64_t mask = 0, size = 0;
-    static constexpr uint64_t kEmpty = ~0ull;
-    void init(uint64_t cap) {
-        uint64_t c = 1024;
-        while (c < cap * 2) c <<= 1;
-        keys.assign(c, kEmpty);
-        vals.assign(c, 0);
-        mask = c - 1;
-        size = 0;
-    }
-    static inline uint64_t mix(uint64_t x) {
-        x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
-        return x;
-    }
-    inline int64_t find(uint64_t k) const {
-        uint64_t i = mix(k) & mask;
-        while (true) {
-            const uint64_t kk = keys[i];
-            if (kk == k) return vals[i];
-            if (kk == kEmpty) return -1;
-            i = (i + 1) & mask;
-        }
-    }
-    void grow() {
-        std::vector<uint64_t> ok;
-        std::vector<uint32_t> ov;
-        ok.swap(keys);
-        ov.swap(vals);
-        init((ok.size()));
-        for (size_t i = 0; i < ok.size(); ++i)
-            if (ok[i] != kEmpty) insert(ok[i], ov[i]);
-    }
-    inline void insert(uint64_t k, uint32_t v) {
-        if ((size + 1) * 2 > keys.size()) grow();
-        uint64_t i = mix(k) & mask;
-        while (keys[i] != kEmpty && keys[i] != k) i = (i + 1) & mask;
-        if (keys[i] == kEmpty) ++size;
-        keys[i] = k;
-        vals[i] = v;
-    }
-};
-
-// PriorityQueue with the reference's heap algorithms and pqPos bookkeeping.
-struct Heap {
-    std::vector<uint32_t> a;
-    std::vector<Node> *nodes;
-    bool hang = false;
-
-    // CompareNodeStar: true if x has LOWER priority than y
-    inline bool cns(uint32_t x, uint32_t y) const {
-        const Node &A = (*nodes)[x], &B = (*nodes)[y];
-        const float fa = A.g + A.h;
-        const float fb = B.g + B.h;
-        const float diff = fa - fb;
-        if (std::fabs(diff) < FLT_EPSILON) {
-            const int la = __builtin_popcountll(A.sub) & 0xff, lb = __builtin_popcountll(B.sub) & 0xff;
-            return (lb - la) > 0;
-        }
-        return diff > 0;
-    }
-    inline void setpos(uint32_t x, int64_t p) { (*nodes)[x].pq = (int32_t)p; }
-    void push_hole(int64_t hole, int64_t top, uint32_t value) {
-        int64_t parent = (hole - 1) / 2;
-        while (hole > top && cns(a[parent], value)) {
-            a[hole] = a[parent];
-            setpos(a[hole], hole);
-            hole = parent;
-            parent = (hole - 1) / 2;
-        }
-        a[hole] = value;
-        setpos(value, hole);
-    }
-    void push(uint32_t x) {
-        a.push_back(x);
-        push_hole((int64_t)a.size() - 1, 0, x);
-    }
-    void adjust(int64_t hole, int64_t len, uint32_t value) {
-        const int64_t top = hole;
-        int64_t second = hole;
-        while (second < (len - 1) / 2) {
-            second = 2 * (second + 1);
-            if (cns(a[second], a[second - 1])) second--;
-            a[hole] = a[second];
-            setpos(a[hole], hole);
-            hole = second;
-        }
-        if ((len & 1) == 0 && second == (len - 2) / 2) {
-            second = 2 * (second + 1);
-            a[hole] = a[second - 1];
-            setpos(a[hole], hole);
-            hole = second - 1;
-        }
-        push_hole(hole, top, value);
-    }
-    uint32_t pop() {
-        const uint32_t ret = a[0];
-        const int64_t last = (int64_t)a.size() - 1;
-        const uint32_t value = a[last];
-        a[last] = a[0];
-        adjust(0, last, value);
-        a.pop_back();
-        return ret;
-    }
-    void update(uint32_t x) {
-        const int64_t pos = (*nodes)[x].pq;
-        const int64_t parent = (pos - 1) / 2;
-        const uint32_t value = a[pos];
-        if (pos > 0 && cns(a[parent], value)) {
-            int64_t par = (pos - 1) / 2, index = pos;
-            while (index > 0 && cns(a[par], value)) {
-                a[index] = a[par];
-                setpos(a[index], index);
-                index = par;
-                par = (par - 1) / 2;
-            }
-            if (pos != index) {
-                a[index] = value;
-                setpos(value, index);
-            }
-        } else {
-            // __down_heap as written: follows the left child only and does not
-            // record the moved value's position (priority_queue-inl.h:176-208)
-            const int64_t len = (int64_t)a.size();
-            int64_t index = pos, left = 2 * index + 1, right = 2 * index + 2, largest = len, guard = 0;
-            while (index < len) {
-                if ((right >= len) || ((left < len) && cns(a[right], a[left]))) largest = left;
-                if (largest < len && cns(value, a[largest])) {
-                    if (largest == index || ++guard > 128) { hang = true; break; }  // the reference would spin
-                    a[index] = a[largest];
-                    setpos(a[largest], index);
-                    index = largest;
-                    left = index * 2 + 1;
-                    right = index * 2 + 2;
-                } else
-                    break;
-            }
-            if (pos != index) a[index] = value;
-        }
-    }
-};
 
 // connected components of the skeleton (skeleton.cpp:187-230), discovery order
 int components(const uint64_t *edges, int n, std::vector<uint64_t> &out) {
@@ -341,6 +149,28 @@ SearchState &state(ulg_ctx *c) {
 }  // namespace
 
 namespace ulg {
+namespace exact {
+
+void host_tables(const SearchState &s, HostTables &T) {
+    const int n = s.n;
+    const uint64_t all = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+    T.cost = s.host_costs;
+    T.tb_off = s.tb_off.data();
+    T.support = s.support.data();
+    T.all = all;
+    T.n = n;
+    T.hole.assign(n, -1);
+    for (int v = 0; v < n; ++v) {
+        const uint64_t D = s.support[v];
+        const uint64_t miss = ~D & all;
+        if (__builtin_popcountll(miss) == 1 && ((D & ~all) == 0)) T.hole[v] = __builtin_ctzll(miss);
+    }
+    T.pd = s.pd_host.data();
+    T.groups = s.groups;
+    T.pd_off = s.pd_off;
+}
+
+}  // namespace exact
 
 int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, float *goal_cost, int64_t *expanded);
 
@@ -453,20 +283,7 @@ int ulg_astar(ulg_ctx *c, const uint64_t *edges, int pd_count, int mode, uint64_
     if (mode != ULG_ASTAR_EXACT) return set_err(c, ULG_ERR_ARG, "ulg_astar: unknown mode");
     if ((rc = search_cost_table_host(c))) return rc;
     HostTables T;
-    T.cost = s.host_costs;
-    T.tb_off = s.tb_off.data();
-    T.support = s.support.data();
-    T.all = all;
-    T.n = n;
-    T.hole.assign(n, -1);
-    for (int v = 0; v < n; ++v) {
-        const uint64_t D = s.support[v];
-        const uint64_t miss = ~D & all;
-        if (__builtin_popcountll(miss) == 1 && ((D & ~all) == 0)) T.hole[v] = __builtin_ctzll(miss);
-    }
-    T.pd = s.pd_host.data();
-    T.groups = s.groups;
-    T.pd_off = s.pd_off;
+    host_tables(s, T);
     std::vector<uint64_t> comps;
     const bool good = edges != nullptr;
     if (good) components(edges, n, comps);

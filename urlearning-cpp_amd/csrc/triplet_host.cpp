@@ -1,0 +1,331 @@
+// triplet_host.cpp -- ulg_triplet_astar: the reference's triplet_astar driver
+// (astar/triplet_astar.cpp:991-1622) over the GPU-built best-score lattice.
+//
+// Every A* the driver asks for is over one "big cluster" (the union of the
+// clusters of a triple) and its answer depends on that cluster alone, so the
+// searches are memoised per cluster: on a full skeleton every triple maps to
+// the same cluster and the reference's thousands of identical searches become
+// one.  Each distinct cluster gets its own static pattern database built on
+// the GPU (ulg_pdb_build(pd_count, 0, cluster), triplet_astar.cpp:303) and an
+// exact-order search on the host over O(1) table reads -- the re-opening
+// variant of run_astar_on_one_scc (:285-674), whose pop order decides which
+// of several tied optimal DAGs the orientation rules see.
+//
+// The orientation state is held as bit rows: out[i] bit j == directed_graph
+// [i][j].  Both directions set = undirected edge.
+#include <algorithm>
+#include <cstring>
+#include <unordered_map>
+#include <unordered_set>
+
+#include "search_exact.h"
+
+using namespace ulg;
+using namespace ulg::exact;
+
+namespace {
+
+constexpr int kMaxCluster = 26;  // triplet_astar.cpp:840
+
+inline bool bit(uint64_t s, int i) { return (s >> i) & 1ull; }
+
+struct Triplet {
+    ulg_ctx *c = nullptr;
+    SearchState *s = nullptr;
+    int n = 0, pd_count = 2;
+    uint64_t nb[64] = {}, clusters[64] = {}, vstr[64] = {}, out[64] = {};
+    std::unordered_set<uint64_t> checked;
+    std::unordered_map<uint64_t, std::vector<uint64_t>> memo;  // cluster -> optimal parents
+    int64_t runs = 0, distinct = 0, expanded = 0;
+    int num_v_structures = 0;
+    bool hang = false;
+    int rc = ULG_OK;
+
+    bool dg(int a, int b) const { return bit(out[a], b); }
+    void set(int a, int b, bool v) {
+        if (v) out[a] |= 1ull << b;
+        else out[a] &= ~(1ull << b);
+    }
+    // an undirected a-b unless either direction is already decided
+    void undirected_if_free(int a, int b, bool adjacent) {
+        if (adjacent && !dg(a, b) && !dg(b, a)) {
+            set(a, b, true);
+            set(b, a, true);
+        }
+    }
+    void add_edge(int a, int b) {  // Skeleton::add_edge + cluster refresh (:1186-1191)
+        nb[a] |= 1ull << b;
+        nb[b] |= 1ull << a;
+        clusters[a] = nb[a];
+        clusters[b] = nb[b];
+    }
+};
+
+// run_astar_on_one_scc of triplet_astar.cpp:285-674 with ancestors = {} and
+// the_scc = cluster: no skeleton filter, and a closed node whose g strictly
+// improves is pushed back onto the open list (:556-576).
+int cluster_astar(Triplet &t, uint64_t cluster, std::vector<uint64_t> &op) {
+    ulg_ctx *c = t.c;
+    int rc;
+    if ((rc = search_build_pdb(c, t.pd_count, 0, cluster))) return rc;
+    HostTables T;
+    host_tables(*t.s, T);
+    const int n = t.n;
+    op.assign(n, 0);
+    std::vector<Node> nodes;
+    nodes.reserve(1024);
+    NodeIndex generated;
+    generated.init(1024);
+    Heap open;
+    open.nodes = &nodes;
+    const uint64_t r1 = cluster >> 1;
+    nodes.push_back(Node{0.0f, 0.0f, 0, (uint8_t)(r1 ? __builtin_ctzll(r1) + 1 : 0), 0});
+    open.push(0);
+    int64_t goal = -1, nexp = 0;
+    const float upperBound = FLT_MAX;
+    while (!open.a.empty()) {
+        const uint32_t ui = open.pop();
+        ++nexp;
+        const uint64_t variables = nodes[ui].sub;
+        if (variables == cluster) { goal = ui; break; }
+        if (nodes[ui].g + nodes[ui].h > upperBound) break;
+        nodes[ui].pq = -2;
+        const float ug = nodes[ui].g;
+        uint64_t cand = cluster & ~variables;
+        while (cand) {
+            const int leaf = __builtin_ctzll(cand);
+            cand &= cand - 1;
+            const uint64_t nv = variables | (1ull << leaf);
+            const int64_t si = generated.find(nv);
+            if (si < 0) {
+                bool complete = false;
+                const float g = ug + T.bs(leaf, nv);
+                const float h = T.h(nv, &complete);
+                const uint32_t idx = (uint32_t)nodes.size();
+                nodes.push_back(Node{g, h, nv, (uint8_t)leaf, 0});
+                open.push(idx);
+                generated.insert(nv, idx);
+                continue;
+            }
+            const float g = ug + T.bs(leaf, variables);
+            if (g < nodes[si].g) {
+                nodes[si].leaf = (uint8_t)leaf;
+                nodes[si].g = g;
+                if (nodes[si].pq == -2) open.push((uint32_t)si);  // re-open
+                else open.update((uint32_t)si);
+            }
+        }
+    }
+    t.expanded += nexp;
+    if (open.hang) t.hang = true;
+    if (goal < 0) return ULG_OK;  // no goal: every parent set stays empty
+    // reconstructSolution (:172-224): walk the leaves back from the goal and
+    // ask the device for each leaf's best parent set among its predecessors
+    const int count = __builtin_popcountll(cluster);
+    std::vector<int> qv;
+    std::vector<uint64_t> qs;
+    uint64_t remaining = nodes[goal].sub;
+    int64_t cur = goal;
+    for (int i = 0; i < count && cur >= 0; ++i) {
+        const int leaf = nodes[cur].leaf;
+        qv.push_back(leaf);
+        qs.push_back(remaining);
+        remaining ^= 1ull << leaf;
+        cur = generated.find(remaining);
+    }
+    if (!qv.empty()) {
+        std::vector<float> qc(qv.size());
+        std::vector<uint64_t> qp(qv.size());
+        if ((rc = search_query(c, (int64_t)qv.size(), qv.data(), qs.data(), qc.data(), qp.data()))) return rc;
+        for (size_t i = 0; i < qv.size(); ++i) op[qv[i]] = qp[i];
+    }
+    return ULG_OK;
+}
+
+const std::vector<uint64_t> *cluster_parents(Triplet &t, uint64_t cluster) {
+    ++t.runs;
+    auto it = t.memo.find(cluster);
+    if (it != t.memo.end()) return &it->second;
+    std::vector<uint64_t> op;
+    if ((t.rc = cluster_astar(t, cluster, op))) return nullptr;
+    ++t.distinct;
+    return &t.memo.emplace(cluster, std::move(op)).first->second;
+}
+
+// process_triple (triplet_astar.cpp:811-989)
+void process_triple(Triplet &t, int i, int vj, int vk) {
+    if (t.rc) return;
+    int a[3] = {i, vj, vk};
+    std::sort(a, a + 3);
+    const uint64_t big = t.clusters[i] | t.clusters[vj] | t.clusters[vk];
+    if (__builtin_popcountll(big) > kMaxCluster) return;
+    const uint64_t key = ((uint64_t)a[0] << 40) + ((uint64_t)a[1] << 20) + (uint64_t)a[2];
+    if (!t.checked.insert(key).second) return;
+    const std::vector<uint64_t> *opp = cluster_parents(t, big);
+    if (!opp) return;
+    const std::vector<uint64_t> &op = *opp;
+    auto adjacent = [&](int x, int y) { return bit(op[x], y) || bit(op[y], x); };
+    // collider c with parents p, q: p -> c <- q, then p - q if the DAG joins them
+    auto collider = [&](int cc, int p, int q) {
+        ++t.num_v_structures;
+        t.set(p, cc, true);
+        t.set(q, cc, true);
+        t.set(cc, p, false);
+        t.set(cc, q, false);
+        t.undirected_if_free(p, q, adjacent(p, q));
+        t.vstr[cc] |= (1ull << p) | (1ull << q);
+    };
+    if (bit(op[i], vj) && bit(op[i], vk)) collider(i, vj, vk);
+    else if (bit(op[vk], i) && bit(op[vk], vj)) collider(vk, vj, i);
+    else if (bit(op[vj], i) && bit(op[vj], vk)) collider(vj, vk, i);
+    else {
+        t.undirected_if_free(vk, vj, adjacent(vj, vk));
+        t.undirected_if_free(i, vj, adjacent(vj, i));
+        t.undirected_if_free(i, vk, adjacent(vk, i));
+    }
+}
+
+// Meek rules 2, 3 and 4 as the reference applies them (:1297-1478), until a
+// sweep orients nothing or n sweeps have run.
+void meek(Triplet &t) {
+    const int n = t.n;
+    for (int iter = 0; iter < n; ++iter) {
+        int oriented = 0;
+        for (int v = 0; v < n; ++v) {  // rule 2: a -> v -> b and a - b  =>  a -> b
+            uint64_t ins = 0, outs = 0;
+            for (int j = 0; j < n; ++j) {
+                if (t.dg(v, j) && !t.dg(j, v)) outs |= 1ull << j;
+                else if (t.dg(j, v) && !t.dg(v, j)) ins |= 1ull << j;
+            }
+            if (!ins || !outs) continue;
+            for (uint64_t pi = ins; pi; pi &= pi - 1) {
+                const int p = __builtin_ctzll(pi);
+                for (uint64_t co = outs; co; co &= co - 1) {
+                    const int ch = __builtin_ctzll(co);
+                    if (t.dg(p, ch) && t.dg(ch, p)) {
+                        t.set(ch, p, false);
+                        ++oriented;
+                    }
+                }
+            }
+        }
+        for (int v = 0; v < n; ++v) {  // rule 3: two v-structure parents of v both undirected to w  =>  w -> v
+            uint64_t und = 0;
+            for (int j = 0; j < n; ++j)
+                if (t.dg(v, j) && t.dg(j, v)) und |= 1ull << j;
+            if (__builtin_popcountll(t.vstr[v]) < 2 || !und) continue;
+            for (uint64_t wi = und; wi; wi &= wi - 1) {
+                const int w = __builtin_ctzll(wi);
+                int cnt = 0;
+                for (uint64_t pi = t.vstr[v]; pi; pi &= pi - 1) {
+                    const int p = __builtin_ctzll(pi);
+                    cnt += t.dg(p, w) && t.dg(w, p);
+                }
+                if (cnt >= 2) {
+                    t.set(v, w, false);
+                    ++oriented;
+                }
+            }
+        }
+        for (int v = 0; v < n; ++v) {  // rule 4
+            uint64_t ins = 0, outs = 0, und = 0;
+            for (int j = 0; j < n; ++j) {
+                const bool f = t.dg(v, j), b = t.dg(j, v);
+                if (f && !b) outs |= 1ull << j;
+                else if (b && !f) ins |= 1ull << j;
+                else if (f && b) und |= 1ull << j;
+            }
+            if (!outs || !ins || !und) continue;
+            for (uint64_t wi = und; wi; wi &= wi - 1) {
+                const int w = __builtin_ctzll(wi);
+                bool joined = false;
+                for (uint64_t pi = ins; pi && !joined; pi &= pi - 1) {
+                    const int p = __builtin_ctzll(pi);
+                    joined = t.dg(w, p) && t.dg(p, w);
+                }
+                if (!joined) continue;
+                for (uint64_t co = outs; co; co &= co - 1) {
+                    const int ch = __builtin_ctzll(co);
+                    if (!t.dg(w, ch) || !t.dg(ch, w)) continue;
+                    ++oriented;
+                    t.set(ch, w, false);
+                }
+            }
+        }
+        if (oriented == 0) break;
+    }
+}
+
+}  // namespace
+
+extern "C" int ulg_triplet_astar(ulg_ctx *c, const uint64_t *edges, int pd_count, int *directed_graph, int64_t *stats) {
+    if (!c || !directed_graph || pd_count < 1) return ULG_ERR_ARG;
+    if (!c->search || !c->search->tables_ready) return set_err(c, ULG_ERR_STATE, "ulg_triplet_astar: no best-score tables");
+    ULG_HIP(c, hipSetDevice(c->device));
+    SearchState &s = *c->search;
+    const int n = s.n;
+    int rc;
+    if ((rc = search_cost_table_host(c))) return rc;
+    Triplet t;
+    t.c = c;
+    t.s = &s;
+    t.n = n;
+    t.pd_count = pd_count;
+    const uint64_t all = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+    // Skeleton::get_neighbors: the file's rows, or every variable (self
+    // included) without a skeleton; clusters add the variable itself (:1061-1072)
+    for (int v = 0; v < n; ++v) {
+        t.nb[v] = edges ? edges[v] : all;
+        t.clusters[v] = t.nb[v] | (1ull << v);
+    }
+    for (int i = 0; i < n && !t.rc; ++i) {
+        const uint64_t pin = t.nb[i];
+        std::vector<int> unc;
+        for (int j = 0; j < n; ++j)
+            if (bit(pin, j)) unc.push_back(j);
+        // an isolated orphan edge i - vj (:1166-1178)
+        if (unc.size() == 1 && i < unc[0] && __builtin_popcountll(t.nb[unc[0]]) == 1) {
+            const int vj = unc[0];
+            const uint64_t parset = 1ull << vj;
+            float cost;
+            uint64_t par;
+            if ((rc = search_query(c, 1, &i, &parset, &cost, &par))) return rc;
+            if (par == parset) {
+                t.set(i, vj, true);
+                t.set(vj, i, true);
+            }
+        }
+        for (size_t j = 0; j < unc.size() && !t.rc; ++j) {
+            const int vj = unc[j];
+            for (size_t k = 0; k < j && !t.rc; ++k) {
+                const int vk = unc[k];
+                process_triple(t, i, vj, vk);
+                if (!bit(t.nb[vj], vk) && (t.dg(vj, vk) || t.dg(vk, vj))) t.add_edge(vj, vk);
+            }
+        }
+    }
+    // unfaithful edges: oriented pairs the skeleton lacks (:1256-1290)
+    int delta = 1;
+    while (delta > 0 && !t.rc) {
+        delta = 0;
+        for (int i = 0; i < n; ++i)
+            for (int j = 0; j < i; ++j) {
+                if (!((t.dg(i, j) || t.dg(j, i)) && !bit(t.nb[i], j))) continue;
+                ++delta;
+                t.add_edge(i, j);
+                for (int k = 0; k < n; ++k)
+                    if (k != i && k != j && (bit(t.clusters[i], k) || bit(t.clusters[j], k))) process_triple(t, i, j, k);
+            }
+    }
+    if (t.rc) return t.rc;
+    meek(t);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) directed_graph[i * n + j] = t.dg(i, j) ? 1 : 0;
+    if (stats) {
+        stats[0] = t.runs;
+        stats[1] = t.distinct;
+        stats[2] = t.expanded;
+    }
+    if (t.hang) return set_err(c, ULG_ERR_STATE, "ulg_triplet_astar: the reference heap's __down_heap would not terminate here");
+    return ULG_OK;
+}

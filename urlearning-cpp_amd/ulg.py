@@ -48,6 +48,7 @@ def lib():
         L.ulg_pdb_build.argtypes = [P, I, C.c_uint64, C.c_uint64]
         L.ulg_pdb_query.argtypes = [P, I64, P, P, P]
         L.ulg_astar.argtypes = [P, P, I, I, P, P, C.POINTER(F), C.POINTER(I64), C.c_char_p, I64]
+        L.ulg_triplet_astar.argtypes = [P, P, I, P, P]
         L.ulg_set_option.argtypes = [P, C.c_char_p, I64]
         L.ulg_profile_enable.argtypes = [P, I]
         L.ulg_profile_get.argtypes = [P, C.c_char_p, C.POINTER(D), C.POINTER(I64), C.POINTER(D)]
@@ -197,6 +198,18 @@ class Context:
                                     len(buf) if buf is not None else 0), "ulg_astar")
         return {"vpar": vpar, "order": order, "cost": cost.value, "expanded": exp.value,
                 "net_text": buf.value.decode() if buf is not None else None}
+
+    def triplet(self, edges=None, pd_count=2):
+        """ulg_triplet_astar -> {"mec": n x n int32 (i -> j at [i, j]), "runs", "distinct", "expanded"}."""
+        n = self.search_n
+        dg = np.zeros(n * n, dtype=np.int32)
+        stats = np.zeros(3, dtype=np.int64)
+        e = None
+        if edges is not None:
+            e = np.ascontiguousarray([int(x) for x in edges], dtype=np.uint64)
+        self._check(lib().ulg_triplet_astar(self._h, _ptr(e) if e is not None else None, int(pd_count), _ptr(dg),
+                                            _ptr(stats)), "ulg_triplet_astar")
+        return {"mec": dg.reshape(n, n), "runs": int(stats[0]), "distinct": int(stats[1]), "expanded": int(stats[2])}
 
     def set_option(self, name: str, value: int):
         self._check(lib().ulg_set_option(self._h, name.encode(), int(value)), "ulg_set_option")
