@@ -160,8 +160,9 @@ int ulg_triplet_astar(ulg_ctx *ctx, const uint64_t *edges, int pd_count,
                       int *directed_graph, int64_t *stats);
 
 /* ---- tuning knobs -------------------------------------------------------
- * "score_variant" (0..3, default 1): bit 0 = fully unrolled presence gather
- * in the scorer (layers <= 6), bit 1 = stack-machine dominance recursion.
+ * "score_variant" (0..7, default 1): bit 0 = fully unrolled presence gather
+ * in the scorer (layers <= 6), bit 1 = stack-machine dominance recursion,
+ * bit 2 = decision-only walk (stops at the first visited key >= -ts).
  * All variants compute identical results; the knob exists for A/B timing. */
 int ulg_set_option(ulg_ctx *ctx, const char *name, int64_t value);
 

@@ -139,10 +139,11 @@ def test_rescoring_is_deterministic(ulg_ctx):
         assert x.tobytes() == y.tobytes()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 def test_scorer_variants_identical(ulg_ctx, oracle_built, variant):
-    """Every scorer variant (presence gather x recursion form) stores exactly
-    the oracle's sets (k=6 exercises the unrolled presence, k=7,8 the loop)."""
+    """Every scorer variant (presence gather x recursion form x decision-only
+    walk) stores exactly the oracle's sets (k=6 exercises the unrolled
+    presence, k=7,8 the loop)."""
     n = 11
     X, _ = synth.gaussian_sem(n, 2500, 9230 + variant)
     variables = list(range(n))

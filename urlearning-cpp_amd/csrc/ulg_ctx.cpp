@@ -117,7 +117,7 @@ const char *ulg_last_error(const ulg_ctx *c) { return c ? c->err.c_str() : "null
 int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
     if (!c || !name) return ULG_ERR_ARG;
     if (std::strcmp(name, "score_variant") == 0) {
-        if (value < 0 || value > 3) return set_err(c, ULG_ERR_ARG, "score_variant must be 0..3");
+        if (value < 0 || value > 7) return set_err(c, ULG_ERR_ARG, "score_variant must be 0..7");
         c->score_variant = (int)value;
         return ULG_OK;
     }
