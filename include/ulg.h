@@ -105,6 +105,24 @@ int ulg_cbic_score_vars(ulg_ctx *ctx, const int *vars, int nv,
 int ulg_quantize_costs(ulg_ctx *ctx, const float *scores, float *costs,
                        int64_t count);
 
+/* ---- the .pss score-cache text (score_main.cpp:173-203,383-400) -------- */
+/* Formats the lists of the last ulg_cbic_score (every variable scored) as
+ * the .pss file the reference's score command writes: `header` verbatim
+ * (the META block and its blank line), then for each variable in index
+ * order "VAR <name>", "META arity=<a>", one line per stored set -- the
+ * score as glibc "%f" prints it, a space, each parent's name followed by a
+ * space -- and a blank line.  The text is formatted on the GPU; *text points
+ * to a context-owned host buffer of *len bytes (NUL-terminated), valid until
+ * the next format call or ulg_destroy. */
+int ulg_pss_format(ulg_ctx *ctx, const char *header, const char *const *names,
+                   const int *arity, const char **text, int64_t *len);
+/* Same for host lists (offsets[n+1], sets, scores; variable v owns
+ * [offsets[v], offsets[v+1]) ), e.g. after the multi-GPU exchange. */
+int ulg_pss_format_lists(ulg_ctx *ctx, int n, const int64_t *offsets,
+                         const uint64_t *sets, const float *scores,
+                         const char *header, const char *const *names,
+                         const int *arity, const char **text, int64_t *len);
+
 /* ---- search side (best-score tables, pattern database, A*) ------------ */
 /* Load per-variable parent-set lists (file order within each variable;
  * costs = A* costs, i.e. -1 * atof(score), score_cache.cpp:151) and build

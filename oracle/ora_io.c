@@ -153,20 +153,32 @@ int ora_pss_read(const char *path, ora_pss *out) {
     }
     free(line);
     fclose(f);
+    /* putScore: (*cache[v])[parents] = score (score_cache.h:47-49) -- a repeated
+     * set keeps one entry, its first position in file order and its last value */
+    omap *seen = (omap *)malloc(sizeof(omap) * (size_t)(n > 0 ? n : 1));
+    for (int v = 0; v < n; v++) { omap_init(&seen[v], 64); cnt[v] = 0; }
+    int64_t *slot = (int64_t *)malloc(sizeof(int64_t) * (size_t)(total ? total : 1));
+    for (int64_t i = 0; i < total; i++) {
+        const int v = var_of[i];
+        uint64_t first;
+        if (omap_get(&seen[v], sets[i], &first)) { slot[i] = -1 - (int64_t)first; continue; }
+        omap_put(&seen[v], sets[i], (uint64_t)cnt[v]);
+        slot[i] = cnt[v]++;
+    }
     /* group by variable, keeping file order within each variable */
     out->offsets = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n + 1));
     out->offsets[0] = 0;
     for (int v = 0; v < n; v++) out->offsets[v + 1] = out->offsets[v] + cnt[v];
     out->sets = (ora_varset *)malloc(sizeof(ora_varset) * (size_t)(total ? total : 1));
     out->costs = (float *)malloc(sizeof(float) * (size_t)(total ? total : 1));
-    int64_t *fill = (int64_t *)calloc((size_t)n + 1, sizeof(int64_t));
     for (int64_t i = 0; i < total; i++) {
-        int v = var_of[i];
-        int64_t p = out->offsets[v] + fill[v]++;
-        out->sets[p] = sets[i];
-        out->costs[p] = costs[i];
+        const int v = var_of[i];
+        const int64_t k = slot[i] >= 0 ? slot[i] : -1 - slot[i];
+        out->sets[out->offsets[v] + k] = sets[i];
+        out->costs[out->offsets[v] + k] = costs[i];
     }
-    free(fill); free(cnt); free(var_of); free(sets); free(costs);
+    for (int v = 0; v < n; v++) omap_free(&seen[v]);
+    free(seen); free(slot); free(cnt); free(var_of); free(sets); free(costs);
     return 0;
 }
 

@@ -219,6 +219,48 @@ def triplet(search, edges=None, pd_count=2):
             "expanded": exp.value}
 
 
+class _OraPss(C.Structure):
+    _fields_ = [("n", C.c_int), ("names", C.POINTER(C.c_char_p)), ("offsets", C.POINTER(C.c_int64)),
+                ("sets", C.POINTER(C.c_uint64)), ("costs", C.POINTER(C.c_float))]
+
+
+def write_pss(path, names, arity, offsets, sets, scores, input_file="x.csv", num_records=0, parent_limit=3,
+              score_type="cbic"):
+    """ora_pss_write: glibc printf("%f ") lines (score_main.cpp:173-203,383-389)."""
+    L = lib()
+    L.ora_pss_write.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                C.c_void_p, C.c_char_p, C.c_int64, C.c_int, C.c_char_p]
+    n = len(names)
+    stride = max(len(x) for x in names) + 1
+    blob = b"".join(x.encode().ljust(stride, b"\0") for x in names)
+    ar = np.ascontiguousarray(arity, dtype=np.int32)
+    offs = np.ascontiguousarray(offsets, dtype=np.int64)
+    st = np.ascontiguousarray(sets, dtype=np.uint64)
+    sc = np.ascontiguousarray(scores, dtype=np.float32)
+    rc = L.ora_pss_write(path.encode(), n, blob, stride, _p(ar), _p(offs), _p(st), _p(sc), input_file.encode(),
+                         int(num_records), int(parent_limit), score_type.encode())
+    if rc != 0:
+        raise OSError(path)
+
+
+def read_pss(path):
+    """ora_pss_read (ScoreCache::read restatement) -> (names, offsets, sets, costs) or None."""
+    L = lib()
+    L.ora_pss_read.argtypes = [C.c_char_p, C.POINTER(_OraPss)]
+    L.ora_pss_free.argtypes = [C.POINTER(_OraPss)]
+    p = _OraPss()
+    if L.ora_pss_read(path.encode(), C.byref(p)) != 0:
+        return None
+    n = p.n
+    names = [p.names[i].decode() for i in range(n)]
+    offs = np.array([p.offsets[i] for i in range(n + 1)], dtype=np.int64)
+    tot = int(offs[-1])
+    sets = np.array([p.sets[i] for i in range(tot)], dtype=np.uint64)
+    costs = np.array([p.costs[i] for i in range(tot)], dtype=np.float32)
+    L.ora_pss_free(C.byref(p))
+    return names, offs, sets, costs
+
+
 def dag_matrix(vpar, n):
     """netFile.csv matrix: row v, column i = 1 iff i -> v."""
     M = np.zeros((n, n), dtype=np.int64)

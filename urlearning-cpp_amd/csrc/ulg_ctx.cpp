@@ -103,6 +103,7 @@ void ulg_destroy(ulg_ctx *c) {
     release(c->d_cand); release(c->d_meta); release(c->d_binom);
     release(c->out_sets); release(c->out_scores); release(c->out_offsets);
     release(c->qbuf_in); release(c->qbuf_out);
+    pss_release(c);
     if (c->search) {
         c->search->release_all();
         delete c->search;

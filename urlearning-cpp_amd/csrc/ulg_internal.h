@@ -25,6 +25,7 @@ struct DevBuf {
 };
 
 struct SearchState;
+struct PssState;
 
 struct ProfRec {
     std::string name;
@@ -71,6 +72,9 @@ struct ulg_ctx {
     // ---- search side (best-score tables, pattern database, A*) ----
     ulg::SearchState *search = nullptr;
 
+    // ---- .pss text formatting (pss.hip) ----
+    ulg::PssState *pss = nullptr;
+
     // ---- profiling ----
     bool prof = false;
     std::vector<ulg::ProfRec> pending;
@@ -115,6 +119,7 @@ void release(DevBuf<T> &b) {
 void prof_begin(ulg_ctx *c, const char *name);
 void prof_end(ulg_ctx *c);
 void prof_collect(ulg_ctx *c);  // after a stream sync
+void pss_release(ulg_ctx *c);    // pss.hip
 
 // binomial table C(a, b), a < 64, b < kBinomK, clamped to uint32
 const std::vector<uint32_t> &host_binom();

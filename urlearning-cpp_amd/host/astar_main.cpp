@@ -87,6 +87,7 @@ int main(int argc, char **argv) {
         good = ulgio::read_skeleton(skel, n, rows, nv);
         if (good) rows.resize(std::max<size_t>(rows.size(), (size_t)n));
     }
+    const double tr = ulgcli::now_s();
     const int dev = std::atoi(args.get("device").c_str());
     ulg_ctx *ctx = nullptr;
     if (ulg_create(&dev, 1, &ctx) != ULG_OK) {
@@ -113,8 +114,8 @@ int main(int argc, char **argv) {
     ulg_destroy(ctx);
     std::printf("Found solution: %f\n", (double)cost);
     std::printf("Nodes expanded: %lld\n", (long long)expanded);
-    std::printf("Timing: read .pss %.3f s, GPU best-score tables %.3f s, search (%s) %.3f s (%.3g expansions/s)\n", t1 - t0,
-                t2 - t1, mode.c_str(), t3 - t2, (double)expanded / (t3 - t2));
+    std::printf("Timing: read .pss %.3f s, HIP init %.3f s, GPU best-score tables %.3f s, search (%s) %.3f s (%.3g expansions/s)\n",
+                tr - t0, t1 - tr, t2 - t1, mode.c_str(), t3 - t2, (double)expanded / (t3 - t2));
     const std::string net = args.get("netFile");
     if (!net.empty()) {
         std::string txt(text.data());

@@ -38,9 +38,10 @@ struct PssHeader {
     std::string score_type;
     std::string ess = "1";
 };
-bool write_pss(const std::string &path, const PssHeader &h, const std::vector<std::string> &names,
-               const std::vector<int> &arity, const std::vector<int64_t> &offsets, const std::vector<uint64_t> &sets,
-               const std::vector<float> &scores);
+// The META block the .pss starts with (score_main.cpp:383-389), blank line
+// included; the per-variable blocks come from ulg_pss_format.
+std::string pss_header_text(const PssHeader &h);
+bool write_bytes(const std::string &path, const char *data, int64_t len);
 
 // ScoreCache::read (score_cache/score_cache.cpp:55-160): two passes with the
 // reference's case-insensitive "var " / "meta" substring tests; costs are

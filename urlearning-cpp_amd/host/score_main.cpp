@@ -108,17 +108,12 @@ int main(int argc, char **argv) {
     for (int v = 0; v < n; ++v) vars[v] = v;
     int64_t stored = 0, scored = 0;
     if (rc == ULG_OK) rc = ulg_cbic_score(ctx, vars.data(), n, cands.data(), maxp, &stored, &scored);
-    std::vector<uint64_t> sets((size_t)std::max<int64_t>(stored, 1));
-    std::vector<float> scores((size_t)std::max<int64_t>(stored, 1));
-    std::vector<int64_t> offsets(n + 1);
-    if (rc == ULG_OK) rc = ulg_cbic_fetch(ctx, sets.data(), scores.data(), offsets.data(), 0);
     const double t1 = ulgcli::now_s();
     if (rc != ULG_OK) {
         std::fprintf(stderr, "score: %s\n", ulg_last_error(ctx));
         ulg_destroy(ctx);
         return 1;
     }
-    ulg_destroy(ctx);
     ulgio::PssHeader h;
     h.input_file = input;
     h.num_records = rs.num_records;
@@ -130,13 +125,29 @@ int main(int argc, char **argv) {
         std::snprintf(buf, sizeof buf, "%.9g", (double)std::strtof(args.get("ess").c_str(), nullptr));
         h.ess = buf;
     }
-    if (!ulgio::write_pss(output, h, rs.names, rs.arity, offsets, sets, scores)) {
-        std::fprintf(stderr, "score: cannot write '%s'\n", output.c_str());
+    const std::string header = ulgio::pss_header_text(h);
+    std::vector<const char *> cnames(n);
+    for (int v = 0; v < n; ++v) cnames[v] = rs.names[v].c_str();
+    const char *text = nullptr;
+    int64_t len = 0;
+    rc = ulg_pss_format(ctx, header.c_str(), cnames.data(), rs.arity.data(), &text, &len);
+    const double t2 = ulgcli::now_s();
+    if (rc != ULG_OK) {
+        std::fprintf(stderr, "score: %s\n", ulg_last_error(ctx));
+        ulg_destroy(ctx);
         return 1;
     }
-    const double t2 = ulgcli::now_s();
+    if (!ulgio::write_bytes(output, text, len)) {
+        std::fprintf(stderr, "score: cannot write '%s'\n", output.c_str());
+        ulg_destroy(ctx);
+        return 1;
+    }
+    ulg_destroy(ctx);
+    const double t3 = ulgcli::now_s();
     std::printf("URLearning (MI355X), Score Calculator: n=%d N=%lld k=%d lambda=%g\n", n, (long long)N, maxp, lambda);
-    std::printf("Parent sets scored: %lld, stored: %lld, GPU scoring %.3f s (%.3g sets/s), .pss write %.3f s\n",
-                (long long)scored, (long long)stored, t1 - t0, (double)scored / (t1 - t0), t2 - t1);
+    std::printf("Parent sets scored: %lld, stored: %lld, GPU scoring %.3f s (%.3g sets/s), GPU .pss format %.3f s, "
+                "file write %.3f s (%lld bytes)\n",
+                (long long)scored, (long long)stored, t1 - t0, (double)scored / (t1 - t0), t2 - t1, t3 - t2,
+                (long long)len);
     return 0;
 }

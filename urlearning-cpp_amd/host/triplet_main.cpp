@@ -81,6 +81,7 @@ int main(int argc, char **argv) {
         good = ulgio::read_skeleton(skel, n, rows, nv);
         if (good) rows.resize(std::max<size_t>(rows.size(), (size_t)n));
     }
+    const double tr = ulgcli::now_s();
     const int dev = std::atoi(args.get("device").c_str());
     ulg_ctx *ctx = nullptr;
     if (ulg_create(&dev, 1, &ctx) != ULG_OK) {
@@ -102,8 +103,8 @@ int main(int argc, char **argv) {
     ulg_destroy(ctx);
     std::printf("A* runs %lld (distinct clusters %lld), nodes expanded %lld\n", (long long)stats[0],
                 (long long)stats[1], (long long)stats[2]);
-    std::printf("Timing: read .pss %.3f s, GPU best-score tables %.3f s, triplet search %.3f s\n", t1 - t0, t2 - t1,
-                t3 - t2);
+    std::printf("Timing: read .pss %.3f s, HIP init %.3f s, GPU best-score tables %.3f s, triplet search %.3f s\n",
+                tr - t0, t1 - tr, t2 - t1, t3 - t2);
     const std::string net = args.get("netFile");
     if (!net.empty()) {
         std::string csv;

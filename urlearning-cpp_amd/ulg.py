@@ -49,6 +49,8 @@ def lib():
         L.ulg_pdb_query.argtypes = [P, I64, P, P, P]
         L.ulg_astar.argtypes = [P, P, I, I, P, P, C.POINTER(F), C.POINTER(I64), C.c_char_p, I64]
         L.ulg_triplet_astar.argtypes = [P, P, I, P, P]
+        L.ulg_pss_format.argtypes = [P, C.c_char_p, P, P, C.POINTER(C.c_void_p), C.POINTER(I64)]
+        L.ulg_pss_format_lists.argtypes = [P, I, P, P, P, C.c_char_p, P, P, C.POINTER(C.c_void_p), C.POINTER(I64)]
         L.ulg_set_option.argtypes = [P, C.c_char_p, I64]
         L.ulg_profile_enable.argtypes = [P, I]
         L.ulg_profile_get.argtypes = [P, C.c_char_p, C.POINTER(D), C.POINTER(I64), C.POINTER(D)]
@@ -198,6 +200,31 @@ class Context:
                                     len(buf) if buf is not None else 0), "ulg_astar")
         return {"vpar": vpar, "order": order, "cost": cost.value, "expanded": exp.value,
                 "net_text": buf.value.decode() if buf is not None else None}
+
+    def _names_arg(self, names):
+        arr = (C.c_char_p * len(names))(*[x.encode() for x in names])
+        return arr
+
+    def pss_format(self, header: str, names, arity) -> bytes:
+        """ulg_pss_format: the .pss text of the last score() call (every variable)."""
+        nm = self._names_arg(names)
+        ar = np.ascontiguousarray(arity, dtype=np.int32)
+        text, ln = C.c_void_p(), C.c_int64()
+        self._check(lib().ulg_pss_format(self._h, header.encode(), C.cast(nm, C.c_void_p), _ptr(ar), C.byref(text),
+                                         C.byref(ln)), "ulg_pss_format")
+        return C.string_at(text.value, ln.value)
+
+    def pss_format_lists(self, header: str, names, arity, offsets, sets, scores) -> bytes:
+        nm = self._names_arg(names)
+        ar = np.ascontiguousarray(arity, dtype=np.int32)
+        offs = np.ascontiguousarray(offsets, dtype=np.int64)
+        st = np.ascontiguousarray(sets, dtype=np.uint64)
+        sc = np.ascontiguousarray(scores, dtype=np.float32)
+        text, ln = C.c_void_p(), C.c_int64()
+        self._check(lib().ulg_pss_format_lists(self._h, len(names), _ptr(offs), _ptr(st), _ptr(sc), header.encode(),
+                                               C.cast(nm, C.c_void_p), _ptr(ar), C.byref(text), C.byref(ln)),
+                    "ulg_pss_format_lists")
+        return C.string_at(text.value, ln.value)
 
     def triplet(self, edges=None, pd_count=2):
         """ulg_triplet_astar -> {"mec": n x n int32 (i -> j at [i, j]), "runs", "distinct", "expanded"}."""
