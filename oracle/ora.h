@@ -135,6 +135,15 @@ float ora_pdb_value(ora_search *s, int g, ora_varset R);
  * ordering and goal cost, and expansions summed over components.  The
  * netFile text (astar_main.cpp:192-212) is written to net_text if non-NULL
  * (capacity net_cap).  Returns 0, or 1 if some component found no goal. */
+/* get_dag_score (astar/calc_dag_score.cpp:10-119) over a parsed DAG file:
+ * rows[v] (v < nrows <= variableCount) has bit i set iff |atof(token i)| >
+ * 1e-5.  s == NULL means no readable score file (spgs all NULL): scores stay
+ * 0 and only the edge count is computed.  Outputs the row-wise total, the
+ * transposed ("alt") total, the undirected edge count and the two
+ * "edges to remove" counts (bits differing from getParents()). */
+void ora_dag_score(ora_search *s, int variableCount, int nrows, const ora_varset *rows, float *total,
+                   float *alt, int *num_edges, int *remove, int *remove_alt);
+
 int ora_astar(ora_search *s, const ora_varset *edges, int pd_count,
               ora_varset *vpar, int *order, float *goal_cost,
               int64_t *expanded, char *net_text, int64_t net_cap);

@@ -5,13 +5,18 @@
  *              (score/score_main.cpp:209-403)
  *   ref_astar  <in.pss> [-k skel] [-n netFile] [-a pdCount]
  *              (astar/astar_main.cpp:548-709; post-processing skipped, N8)
- * Built twice from this file (-DORA_SCORE / -DORA_ASTAR).
+ *   ref_triplet <in.pss> [-k skel] [-n netFile] [-a pdCount]
+ *              (astar/triplet_astar.cpp:991-1687)
+ *   ref_calc_dag_score <in.pss> <dag.csv>...
+ *              (astar/calc_dag_score.cpp:10-176)
+ * Built once per command from this file (-DORA_SCORE / -DORA_ASTAR / ...).
  */
 #define _GNU_SOURCE
 #include "ora.h"
 #include "ora_io.h"
 
 #include <ctype.h>
+#include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -216,5 +221,80 @@ int main(int argc, char **argv) {
     ora_search_free(s);
     ora_pss_free(&p);
     return rc == 0 ? 0 : 1;
+}
+#endif
+
+#ifdef ORA_DAGSCORE
+/* ref_calc_dag_score <in.pss> <dag.csv>... (astar/calc_dag_score.cpp:121-176):
+ * one output line "NAME  score  edges E  [remove R ]..." for all DAGs. */
+static int dag_tokens(const char *line, double *vals, int cap) {
+    int n = 0;
+    const char *p = line;
+    while (*p) {
+        while (*p && strchr(", \n\r", *p)) p++;
+        if (!*p) break;
+        const char *b = p;
+        while (*p && !strchr(", \n\r", *p)) p++;
+        char tok[256];
+        size_t l = (size_t)(p - b) < sizeof tok - 1 ? (size_t)(p - b) : sizeof tok - 1;
+        memcpy(tok, b, l);
+        tok[l] = 0;
+        if (n < cap) vals[n] = atof(tok);
+        n++;
+    }
+    return n;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 2) { fprintf(stderr, "usage: ref_calc_dag_score in.pss dag.csv...\n"); return 2; }
+    ora_pss p;
+    ora_search *s = NULL;
+    FILE *probe = fopen(argv[1], "r");
+    if (probe) {
+        fclose(probe);
+        if (ora_pss_read(argv[1], &p) == 0) s = ora_search_create(p.n, p.offsets, p.sets, p.costs);
+    }
+    for (int m = 2; m < argc; m++) {
+        /* model name: basename, cut at the first ".csv", upper case */
+        const char *base = strrchr(argv[m], '/');
+        base = base ? base + 1 : argv[m];
+        char name[1024];
+        snprintf(name, sizeof name, "%s", base);
+        char *dot = strstr(name, ".csv");
+        if (dot) *dot = 0;
+        for (char *c = name; *c; c++) *c = (char)toupper((unsigned char)*c);
+        float total = 0, alt = 0;
+        int ne = 0, rm = 0, rma = 0;
+        FILE *f = fopen(argv[m], "r");
+        if (!f) {
+            fprintf(stderr, "Invalid model file %s\n", argv[m]);
+        } else {
+            char *line = NULL;
+            size_t cap = 0;
+            ora_varset rows[64];
+            double vals[64];
+            int variableCount = 0, nrows = 0;
+            if (getline(&line, &cap, f) >= 0) {
+                variableCount = dag_tokens(line, vals, 64);
+                do {
+                    const int nt = dag_tokens(line, vals, 64);
+                    ora_varset par = 0;
+                    for (int i = 0; i < nt && i < 64; i++)
+                        if (fabsf((float)vals[i]) > 1e-5f) par |= 1ULL << i;
+                    rows[nrows++] = par;
+                } while (getline(&line, &cap, f) >= 0 && nrows < variableCount && nrows < 64);
+            }
+            free(line);
+            fclose(f);
+            ora_dag_score(s, variableCount, nrows, rows, &total, &alt, &ne, &rm, &rma);
+        }
+        const float score = total > alt ? alt : total;
+        const int to_remove = total > alt ? rm : rma;
+        if (m == 2) printf("%s  %f  edges %d  ", name, (double)score, ne);
+        else printf("%s  %f  edges %d remove %d ", name, (double)score, ne, to_remove);
+    }
+    printf("\n");
+    if (s) { ora_search_free(s); ora_pss_free(&p); }
+    return 0;
 }
 #endif

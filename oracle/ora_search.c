@@ -872,3 +872,46 @@ int ora_triplet_astar(ora_search *s, const ora_varset *edges, int pd_count, int 
     free(T.nb); free(T.clusters); free(T.vstr_parents);
     return T.hang ? 2 : 0;
 }
+
+/* ---- calc_dag_score (astar/calc_dag_score.cpp) ------------------------------ */
+void ora_dag_score(ora_search *s, int variableCount, int nrows, const ora_varset *rows, float *total,
+                   float *alt, int *num_edges, int *remove, int *remove_alt) {
+    vs_t alt_parents[64];
+    int edges[64][64];
+    for (int i = 0; i < 64; i++) {
+        alt_parents[i] = 0;
+        for (int j = 0; j < 64; j++) edges[i][j] = 0;
+    }
+    float t = 0.0f, a = 0.0f;
+    int rm = 0, rma = 0;
+    for (int v = 0; v < nrows; v++) {
+        const vs_t parents = rows[v];
+        for (int j = 0; j < 64; j++)
+            if ((parents >> j) & 1ULL) {
+                alt_parents[j] |= 1ULL << v;
+                edges[v][j] = 1;
+                edges[j][v] = 1;
+            }
+        if (s) {
+            int64_t b;
+            t += spl_get(s, v, parents, &b);
+            const vs_t opt = (b < s->spl[v].count) ? s->spl[v].parents[b] : 0;
+            rm += popc64(parents ^ opt);
+        }
+    }
+    if (s)
+        for (int i = 0; i < variableCount; i++) {
+            int64_t b;
+            a += spl_get(s, i, alt_parents[i], &b);
+            const vs_t opt = (b < s->spl[i].count) ? s->spl[i].parents[b] : 0;
+            rma += popc64(alt_parents[i] ^ opt);
+        }
+    int ne = 0;
+    for (int i = 0; i < variableCount; i++)
+        for (int j = i + 1; j < variableCount; j++) ne += edges[i][j];
+    *total = t;
+    *alt = a;
+    *num_edges = ne;
+    *remove = rm;
+    *remove_alt = rma;
+}

@@ -18,6 +18,7 @@ LIB = os.path.join(BUILD, "liboracle.so")
 REF_SCORE = os.path.join(BUILD, "ref_score")
 REF_ASTAR = os.path.join(BUILD, "ref_astar")
 REF_TRIPLET = os.path.join(BUILD, "ref_triplet")
+REF_DAGSCORE = os.path.join(BUILD, "ref_calc_dag_score")
 
 _lib = None
 
