@@ -74,6 +74,22 @@ def cpu_baseline(cfg, X, target_s=15.0):
                       f"on {threads} threads"}
 
 
+PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1", "pmc_traffic.json")
+
+
+def pmc_traffic(cfg, sets):
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3
+    PMC passes of the same config (scripts/pmc_round.sh + pmc_summarize.py);
+    None if there is no summary for this config and launch size."""
+    try:
+        t = json.load(open(PMC_TRAFFIC))
+    except (OSError, ValueError):
+        return None, None
+    if t.get("config_id") != cfg["id"] or int(t.get("sets_per_launch", -1)) != int(sets):
+        return None, None
+    return t["traffic_bytes_per_launch"], "profiles/r1/pmc_traffic.json"
+
+
 def roofline(ctx, cfg, per_launch_sets):
     """Dominant kernel = the layer-k 'rest' launch (sets without variable 0)."""
     k = cfg["k"]
@@ -86,8 +102,10 @@ def roofline(ctx, cfg, per_launch_sets):
     bytes_per_set = 4 * (k + 1)
     achieved = sets * bytes_per_set / (p["avg_ms"] * 1e-3) / 1e9
     flops_per_set = 2 * k ** 3 / 3 + 2 * k * k + 2 * k
+    traffic, traffic_src = pmc_traffic(cfg, sets)
     return ({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-             "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": name,
+             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per launch",
+             "traffic_source": traffic_src, "kernel": name,
              "avg_launch_ms": p["avg_ms"], "launches": p["count"], "sets_per_launch": sets,
              "bytes_per_set": bytes_per_set,
              "fp64_flops_per_set": flops_per_set,
@@ -161,7 +179,7 @@ def main():
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config], id=args.config)
     n, N, k, lam = cfg["n"], cfg["N"], cfg["k"], cfg["lam"]
 
     import torch
