@@ -181,6 +181,12 @@ int ulg_triplet_astar(ulg_ctx *ctx, const uint64_t *edges, int pd_count,
  * "score_variant" (0..7, default 1): bit 0 = fully unrolled presence gather
  * in the scorer (layers <= 6), bit 1 = stack-machine dominance recursion,
  * bit 2 = decision-only walk (stops at the first visited key >= -ts).
+ * "table_budget_kb" (KiB; default 0 = half the free HBM): memory for the dense
+ * best-score tables (16 B per entry incl. the host cost copy).  Lists whose
+ * tables over all variables exceed it (e.g. n = 32 with a full skeleton) are
+ * searched with tables built per skeleton component / triplet cluster, and
+ * lookups outside the current tables scan the lists on the device -- same
+ * answers, less memory.
  * All variants compute identical results; the knob exists for A/B timing. */
 int ulg_set_option(ulg_ctx *ctx, const char *name, int64_t value);
 

@@ -31,12 +31,16 @@ constexpr int kTileBits = 14;  // pass A: 2^14 u64 = 128 KiB LDS
 constexpr int kRowBits = 4;    // pass B rows: 16 contiguous u64 = 128 B
 constexpr int kColBits = 10;   // pass B: 2^10 rows x 16 = 2^14 u64
 
+// D_v = union of v's stored sets inside scope (variables outside scope get
+// D_v = {} and a one-entry table)
 __global__ void __launch_bounds__(kB) support_kernel(const uint64_t *sets, const int64_t *offsets, int n,
-                                                     unsigned long long *support) {
+                                                     uint64_t scope, unsigned long long *support) {
     const int v = blockIdx.y;
     const int64_t b = offsets[v], e = offsets[v + 1];
     uint64_t acc = 0;
-    for (int64_t i = b + (int64_t)blockIdx.x * kB + threadIdx.x; i < e; i += (int64_t)gridDim.x * kB) acc |= sets[i];
+    if ((scope >> v) & 1ull)
+        for (int64_t i = b + (int64_t)blockIdx.x * kB + threadIdx.x; i < e; i += (int64_t)gridDim.x * kB)
+            if ((sets[i] & ~scope) == 0) acc |= sets[i];
     // wave OR-reduction then one atomic per wave
     for (int off = 32; off > 0; off >>= 1) acc |= __shfl_xor(acc, off);
     if ((threadIdx.x & 63) == 0 && acc) atomicOr(&support[v], (unsigned long long)acc);
@@ -49,6 +53,7 @@ __global__ void __launch_bounds__(kB) scatter_kernel(const uint64_t *sets, const
     const int64_t b = offsets[v], e = offsets[v + 1];
     const uint64_t D = support[v];
     for (int64_t i = b + (int64_t)blockIdx.x * kB + threadIdx.x; i < e; i += (int64_t)gridDim.x * kB) {
+        if (sets[i] & ~D) continue;  // outside the scope
         const uint64_t idx = pext64(sets[i], D);
         table[tb_off[v] + idx] = ((uint64_t)ordkey(costs[i]) << 32) | (uint64_t)(i - b);
     }
@@ -208,7 +213,7 @@ __global__ void __launch_bounds__(kB) pdb_query_kernel(SearchDev d, int64_t coun
 
 namespace ulg {
 
-int search_build_tables(ulg_ctx *c) {
+int search_build_tables(ulg_ctx *c, uint64_t scope) {
     SearchState &s = *c->search;
     const int n = s.n;
     int rc;
@@ -219,19 +224,40 @@ int search_build_tables(ulg_ctx *c) {
     for (int v = 0; v < n; ++v) maxcnt = std::max<int64_t>(maxcnt, s.offsets[v + 1] - s.offsets[v]);
     const unsigned gx = (unsigned)std::min<int64_t>((maxcnt + kB - 1) / kB, 4096);
     prof_begin(c, "bs_support");
-    support_kernel<<<dim3(gx, n), kB, 0, c->stream>>>(s.d_sets.p, s.d_offsets.p, n,
+    support_kernel<<<dim3(gx, n), kB, 0, c->stream>>>(s.d_sets.p, s.d_offsets.p, n, scope,
                                                      reinterpret_cast<unsigned long long *>(s.d_support.p));
     prof_end(c);
-    s.support.assign(n, 0);
-    ULG_HIP(c, hipMemcpyAsync(s.support.data(), s.d_support.p, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+    std::vector<uint64_t> support(n, 0);
+    ULG_HIP(c, hipMemcpyAsync(support.data(), s.d_support.p, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
     ULG_HIP(c, hipStreamSynchronize(c->stream));
+    // memory check before touching the current tables: 8 B packed key + 4 B
+    // device cost + 4 B pinned host cost per entry
+    uint64_t total = 0;
+    for (int v = 0; v < n; ++v) {
+        const int m = __builtin_popcountll(support[v]);
+        if (m > 40) return set_err(c, ULG_ERR_UNSUPPORTED, "best-score table over more than 40 candidate parents");
+        total += 1ull << m;
+    }
+    uint64_t budget = c->table_budget_kb << 10;
+    if (budget == 0) {
+        size_t free_b = 0, tot_b = 0;
+        ULG_HIP(c, hipMemGetInfo(&free_b, &tot_b));
+        budget = (uint64_t)(free_b / 2) + (uint64_t)s.d_table.cap * 8 + (uint64_t)s.d_cost_table.cap * 4;
+    }
+    if (total * 16 > budget)
+        return set_err(c, ULG_ERR_UNSUPPORTED, "best-score tables for this scope need " +
+                                                   std::to_string((total * 16) >> 10) + " KiB (budget " +
+                                                   std::to_string(budget >> 10) + " KiB)");
+    s.tables_ready = false;
+    s.pdb_ready = false;
+    s.host_costs_ready = false;
+    s.support = support;
     s.mbits.assign(n, 0);
     s.tb_off.assign(n + 1, 0);
     for (int v = 0; v < n; ++v) {
         s.mbits[v] = __builtin_popcountll(s.support[v]);
         s.tb_off[v + 1] = s.tb_off[v] + (1ull << s.mbits[v]);
     }
-    const uint64_t total = s.tb_off[n];
     s.table_entries = total;
     if ((rc = ensure(c, s.d_table, total)) || (rc = ensure(c, s.d_tb_off, (size_t)n + 1)) ||
         (rc = ensure(c, s.d_mbits, (size_t)n)))
@@ -283,14 +309,20 @@ int search_build_tables(ulg_ctx *c) {
     }
     ULG_HIP(c, hipStreamSynchronize(c->stream));
     prof_collect(c);
+    s.scope = scope;
     s.tables_ready = true;
-    s.pdb_ready = false;
     return ULG_OK;
+}
+
+int search_ensure_scope(ulg_ctx *c, uint64_t need) {
+    SearchState &s = *c->search;
+    if (s.tables_ready && (need & ~s.scope) == 0) return ULG_OK;
+    return search_build_tables(c, need);
 }
 
 int search_build_pdb(ulg_ctx *c, int pd_count, uint64_t ancestors, uint64_t scc) {
     SearchState &s = *c->search;
-    if (!s.tables_ready) return set_err(c, ULG_ERR_STATE, "pattern database needs the best-score tables");
+    if (!s.lists_ready) return set_err(c, ULG_ERR_STATE, "pattern database needs the parent-set lists");
     if (pd_count < 1 || pd_count > kMaxGroups) return set_err(c, ULG_ERR_ARG, "pd_count must be 1..8");
     // groups: consecutive scc variables, ceil(|scc| / pd_count) each (static_pattern_database.cpp:95-120)
     s.groups.clear();

@@ -141,6 +141,25 @@ int astar_one(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool skele
     return ULG_OK;
 }
 
+uint64_t all_vars(int n) { return (n >= 64) ? ~0ull : ((1ull << n) - 1ull); }
+
+// New lists: tables over every variable when they fit the budget; otherwise
+// none yet -- searches build tables per component / cluster, and lookups
+// outside the tables' scope scan the lists on the device.
+int lists_loaded(ulg_ctx *c) {
+    SearchState &s = *c->search;
+    s.lists_ready = true;
+    s.tables_ready = false;
+    s.pdb_ready = false;
+    s.host_costs_ready = false;
+    const int rc = search_build_tables(c, all_vars(s.n));
+    if (rc == ULG_ERR_UNSUPPORTED) {
+        c->err.clear();
+        return ULG_OK;
+    }
+    return rc;
+}
+
 SearchState &state(ulg_ctx *c) {
     if (!c->search) c->search = new SearchState();
     return *c->search;
@@ -198,8 +217,7 @@ int ulg_search_load(ulg_ctx *c, int n, const int64_t *offsets, const uint64_t *s
     }
     ULG_HIP(c, hipMemcpyAsync(s.d_offsets.p, offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, c->stream));
     ULG_HIP(c, hipStreamSynchronize(c->stream));
-    s.host_costs_ready = false;
-    return search_build_tables(c);
+    return lists_loaded(c);
 }
 
 int ulg_search_from_scores(ulg_ctx *c) {
@@ -234,13 +252,12 @@ int ulg_search_from_scores(ulg_ctx *c) {
     ULG_HIP(c, hipMemcpyAsync(s.d_offsets.p, s.offsets.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, c->stream));
     if ((rc = search_quantize_device(c, s.d_scores_tmp.p, s.d_costs.p, total))) return rc;
     ULG_HIP(c, hipStreamSynchronize(c->stream));
-    s.host_costs_ready = false;
-    return search_build_tables(c);
+    return lists_loaded(c);
 }
 
 int ulg_bestscore_query(ulg_ctx *c, int64_t count, const int *vars, const uint64_t *S, float *costs, uint64_t *parents) {
     if (!c || count < 0 || (count && (!vars || !S))) return ULG_ERR_ARG;
-    if (!c->search || !c->search->tables_ready) return set_err(c, ULG_ERR_STATE, "ulg_bestscore_query: no best-score tables");
+    if (!c->search || !c->search->lists_ready) return set_err(c, ULG_ERR_STATE, "ulg_bestscore_query: no parent-set lists");
     for (int64_t i = 0; i < count; ++i)
         if (vars[i] < 0 || vars[i] >= c->search->n) return set_err(c, ULG_ERR_ARG, "ulg_bestscore_query: bad variable");
     if (count == 0) return ULG_OK;
@@ -250,8 +267,11 @@ int ulg_bestscore_query(ulg_ctx *c, int64_t count, const int *vars, const uint64
 
 int ulg_pdb_build(ulg_ctx *c, int pd_count, uint64_t ancestors, uint64_t scc) {
     if (!c) return ULG_ERR_ARG;
-    if (!c->search || !c->search->tables_ready) return set_err(c, ULG_ERR_STATE, "ulg_pdb_build: no best-score tables");
+    if (!c->search || !c->search->lists_ready) return set_err(c, ULG_ERR_STATE, "ulg_pdb_build: no parent-set lists");
     ULG_HIP(c, hipSetDevice(c->device));
+    int rc = search_ensure_scope(c, ancestors | scc);  // lookups outside the tables scan the lists
+    if (rc == ULG_ERR_UNSUPPORTED) c->err.clear();
+    else if (rc) return rc;
     return search_build_pdb(c, pd_count, ancestors, scc);
 }
 
@@ -266,24 +286,26 @@ int ulg_pdb_query(ulg_ctx *c, int64_t count, const uint64_t *S, float *h, int *c
 int ulg_astar(ulg_ctx *c, const uint64_t *edges, int pd_count, int mode, uint64_t *vpar, int *order,
               float *goal_cost, int64_t *expanded, char *net_text, int64_t net_cap) {
     if (!c || !vpar || !order || !goal_cost || !expanded) return ULG_ERR_ARG;
-    if (!c->search || !c->search->tables_ready) return set_err(c, ULG_ERR_STATE, "ulg_astar: no best-score tables");
+    if (!c->search || !c->search->lists_ready) return set_err(c, ULG_ERR_STATE, "ulg_astar: no parent-set lists");
     ULG_HIP(c, hipSetDevice(c->device));
     SearchState &s = *c->search;
     const int n = s.n;
-    const uint64_t all = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+    const uint64_t all = all_vars(n);
     int rc;
+    if (mode == ULG_ASTAR_GPU && (rc = search_ensure_scope(c, all))) return rc;  // the whole lattice
     // astar(): the heuristic covers all variables, no ancestors (astar_main.cpp:590-611)
-    if (!s.pdb_ready || s.pd_count != pd_count || s.scc != all || s.ancestors != 0)
+    if (!s.pdb_ready || s.pd_count != pd_count || s.scc != all || s.ancestors != 0) {
+        rc = search_ensure_scope(c, all);
+        if (rc == ULG_ERR_UNSUPPORTED) c->err.clear();  // the PDB build scans the lists
+        else if (rc) return rc;
         if ((rc = search_build_pdb(c, pd_count, 0, all))) return rc;
+    }
     *expanded = 0;
     *goal_cost = 0.0f;
     for (int i = 0; i < n; ++i) { vpar[i] = 0; order[i] = 0; }
     if (net_text && net_cap > 0) net_text[0] = 0;
     if (mode == ULG_ASTAR_GPU) return astar_gpu(c, edges, vpar, order, goal_cost, expanded);
     if (mode != ULG_ASTAR_EXACT) return set_err(c, ULG_ERR_ARG, "ulg_astar: unknown mode");
-    if ((rc = search_cost_table_host(c))) return rc;
-    HostTables T;
-    host_tables(s, T);
     std::vector<uint64_t> comps;
     const bool good = edges != nullptr;
     if (good) components(edges, n, comps);
@@ -291,6 +313,10 @@ int ulg_astar(ulg_ctx *c, const uint64_t *edges, int pd_count, int mode, uint64_
     bool hang = false;
     bool fail = false;
     for (uint64_t comp : comps) {
+        // every lookup of this component's search lies inside the component
+        if ((rc = search_ensure_scope(c, comp)) || (rc = search_cost_table_host(c))) return rc;
+        HostTables T;
+        host_tables(s, T);
         ExactResult r;
         if ((rc = astar_one(c, T, edges, good, 0, comp, expanded, &hang, r))) return rc;
         if (!r.found) { fail = true; continue; }

@@ -97,15 +97,36 @@ struct SearchDev {
     const uint64_t *support; // D_v
     const uint64_t *sets;    // per-variable lists, file order
     const int64_t *offsets;  // [n+1]
+    const float *costs;      // per-variable costs, file order
     const float *pd;         // pattern databases
     const uint64_t *gmeta;   // groups[kMaxGroups], pd_off[kMaxGroups]
+    uint64_t scope;          // the tables hold every stored set inside scope
+    int tables;              // 1 if the tables are built (for scope)
     int pd_count;
     int n;
 };
 
+// The list calculator's answer by a scan of v's list (sparse_parent_list.cpp:
+// 44-55 with the (cost, file order) tie rule): min over stored P subset of S.
+__device__ inline uint64_t bs_key_scan(const SearchDev &d, int v, uint64_t S) {
+    const int64_t b = d.offsets[v], e = d.offsets[v + 1];
+    uint64_t best = ~0ull;
+    for (int64_t i = b; i < e; ++i)
+        if ((d.sets[i] & ~S) == 0) {
+            const uint64_t k = ((uint64_t)ordkey(d.costs[i]) << 32) | (uint64_t)(i - b);
+            best = k < best ? k : best;
+        }
+    return best;
+}
+
+// One read of the lattice when S lies inside the tables' scope (every stored
+// set that can be a subset of S is in the table), else the list scan.
 __device__ inline uint64_t bs_key(const SearchDev &d, int v, uint64_t S) {
-    const uint64_t D = d.support[v];
-    return d.table[d.tb_off[v] + pext64(S & D, D)];
+    if (d.tables && (S & ~d.scope) == 0) {
+        const uint64_t D = d.support[v];
+        return d.table[d.tb_off[v] + pext64(S & D, D)];
+    }
+    return bs_key_scan(d, v, S);
 }
 
 // StaticPatternDatabase::h (static_pattern_database.cpp:145-174)
@@ -139,7 +160,9 @@ struct SearchState {
     uint64_t table_entries = 0;
     DevBuf<uint64_t> d_table, d_tb_off, d_support;
     DevBuf<int> d_mbits, d_prefix;
-    bool tables_ready = false;
+    bool lists_ready = false;   // the per-variable lists are on the device
+    bool tables_ready = false;  // the lattice tables are built for `scope`
+    uint64_t scope = 0;         // tables cover every stored set inside scope
     // host copy of the per-subset best costs (exact-order search)
     DevBuf<float> d_cost_table;
     float *host_costs = nullptr;
@@ -166,6 +189,9 @@ struct SearchState {
         d.support = d_support.p;
         d.sets = d_sets.p;
         d.offsets = d_offsets.p;
+        d.costs = d_costs.p;
+        d.scope = scope;
+        d.tables = tables_ready ? 1 : 0;
         d.pd = d_pd.p;
         d.gmeta = d_groups.p;
         d.pd_count = pd_count;
@@ -183,7 +209,11 @@ struct SearchState {
     }
 };
 
-int search_build_tables(ulg_ctx *c);
+// Builds the lattice tables over the stored sets inside `scope`; returns
+// ULG_ERR_UNSUPPORTED (tables untouched) if they would exceed the budget.
+int search_build_tables(ulg_ctx *c, uint64_t scope);
+// Tables covering `need` (rebuilt for exactly `need` if the current ones do not).
+int search_ensure_scope(ulg_ctx *c, uint64_t need);
 int search_build_pdb(ulg_ctx *c, int pd_count, uint64_t ancestors, uint64_t scc);
 int search_quantize_device(ulg_ctx *c, const float *d_scores, float *d_costs, int64_t count);
 int search_cost_table_host(ulg_ctx *c);

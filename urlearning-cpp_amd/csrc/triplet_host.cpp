@@ -67,6 +67,8 @@ struct Triplet {
 int cluster_astar(Triplet &t, uint64_t cluster, std::vector<uint64_t> &op) {
     ulg_ctx *c = t.c;
     int rc;
+    // every lookup of this search and of its PDB lies inside the cluster
+    if ((rc = search_ensure_scope(c, cluster)) || (rc = search_cost_table_host(c))) return rc;
     if ((rc = search_build_pdb(c, t.pd_count, 0, cluster))) return rc;
     HostTables T;
     host_tables(*t.s, T);
@@ -260,12 +262,11 @@ void meek(Triplet &t) {
 
 extern "C" int ulg_triplet_astar(ulg_ctx *c, const uint64_t *edges, int pd_count, int *directed_graph, int64_t *stats) {
     if (!c || !directed_graph || pd_count < 1) return ULG_ERR_ARG;
-    if (!c->search || !c->search->tables_ready) return set_err(c, ULG_ERR_STATE, "ulg_triplet_astar: no best-score tables");
+    if (!c->search || !c->search->lists_ready) return set_err(c, ULG_ERR_STATE, "ulg_triplet_astar: no parent-set lists");
     ULG_HIP(c, hipSetDevice(c->device));
     SearchState &s = *c->search;
     const int n = s.n;
     int rc;
-    if ((rc = search_cost_table_host(c))) return rc;
     Triplet t;
     t.c = c;
     t.s = &s;

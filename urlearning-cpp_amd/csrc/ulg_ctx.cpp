@@ -122,6 +122,11 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         c->score_variant = (int)value;
         return ULG_OK;
     }
+    if (std::strcmp(name, "table_budget_kb") == 0) {
+        if (value < 0) return set_err(c, ULG_ERR_ARG, "table_budget_kb must be >= 0");
+        c->table_budget_kb = (uint64_t)value;
+        return ULG_OK;
+    }
     return set_err(c, ULG_ERR_ARG, std::string("unknown option: ") + name);
 }
 

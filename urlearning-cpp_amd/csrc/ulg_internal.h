@@ -57,7 +57,8 @@ struct ulg_ctx {
     int64_t total_stored = 0;
     int64_t total_scored = 0;
     bool scored = false;
-    int score_variant = 1;  // see ScoreArgs::variant (ulg_set_option "score_variant")
+    int score_variant = 1;
+    uint64_t table_budget_kb = 0;  // best-score table budget in KiB (0 = half the free HBM)  // see ScoreArgs::variant (ulg_set_option "score_variant")
     ulg::DevBuf<float> table;
     ulg::DevBuf<uint64_t> d_tbl_off, d_work, d_blk;
     ulg::DevBuf<uint8_t> d_cand;  // [nv][64] compact index -> variable
