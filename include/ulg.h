@@ -77,6 +77,14 @@ int ulg_cbic_load(ulg_ctx *ctx, const double *data_colmajor, int64_t N, int n,
 /* Copy the device Gram matrix Z'Z (n x n, row-major) to host. */
 int ulg_cbic_gram(ulg_ctx *ctx, double *gram_out);
 
+/* The skeleton the reference expects from outside (README.md:16, read by
+ * Skeleton::read_matrix_file, base/skeleton.cpp:19-105): MMPC with Fisher-z
+ * partial-correlation tests on the loaded data's Gram matrix.  Independent
+ * iff |atanh(r)| sqrt(N - |S| - 3) <= Phi^-1(1 - alpha/2); conditioning sets
+ * of at most max_cond variables (< 0: 24); AND symmetry rule.  rows[i] bit j
+ * = edge i-j (no diagonal).  Exact rules: oracle/ora_mmpc.c. */
+int ulg_mmpc(ulg_ctx *ctx, double alpha, int max_cond, uint64_t *rows);
+
 /* Score all parent sets of size <= max_parents within each variable's
  * candidate set (candidates[i] for variable vars[i]; the variable's own bit
  * is ignored).  Runs the layer-synchronous HIP scorer; results stay on the

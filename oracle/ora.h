@@ -135,6 +135,13 @@ float ora_pdb_value(ora_search *s, int g, ora_varset R);
  * ordering and goal cost, and expansions summed over components.  The
  * netFile text (astar_main.cpp:192-212) is written to net_text if non-NULL
  * (capacity net_cap).  Returns 0, or 1 if some component found no goal. */
+/* MMPC skeleton with Fisher-z tests (ora_mmpc.c; parity unpinned: the
+ * reference takes the skeleton from outside, README.md:16).  rows[i] bit j =
+ * edge i-j (no diagonal).  max_cond < 0: no cap (24). */
+int ora_mmpc(const ora_dataset *ds, double alpha, int max_cond, ora_varset *rows);
+double ora_partial_z(const double *G, int n, double N, int X, int T, const int *S, int ns);
+double ora_norm_quantile(double p);
+
 /* get_dag_score (astar/calc_dag_score.cpp:10-119) over a parsed DAG file:
  * rows[v] (v < nrows <= variableCount) has bit i set iff |atof(token i)| >
  * 1e-5.  s == NULL means no readable score file (spgs all NULL): scores stay

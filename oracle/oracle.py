@@ -68,6 +68,11 @@ def lib():
         L.ora_pdb_value.argtypes = [P, I, U64]
         L.ora_pdb_value.restype = F
         L.ora_astar.argtypes = [P, P, I, P, P, C.POINTER(F), C.POINTER(I64), C.c_char_p, I64]
+        L.ora_mmpc.argtypes = [P, D, I, P]
+        L.ora_norm_quantile.argtypes = [D]
+        L.ora_norm_quantile.restype = D
+        L.ora_partial_z.argtypes = [P, I, D, I, I, P, I]
+        L.ora_partial_z.restype = D
         L.ora_triplet_astar.argtypes = [P, P, I, P, C.POINTER(I64), C.POINTER(I64), C.POINTER(I64)]
         _lib = L
     return _lib
@@ -108,6 +113,12 @@ class Dataset:
 
     def cbic_raw(self, lam, v, parents):
         return lib().ora_cbic_raw(self.h, float(lam), int(v), int(parents))
+
+    def mmpc(self, alpha=0.05, max_cond=-1):
+        """ora_mmpc -> skeleton rows (bit j of row i = edge i-j)."""
+        rows = np.zeros(64, dtype=np.uint64)
+        lib().ora_mmpc(self.h, float(alpha), int(max_cond), _p(rows))
+        return [int(x) for x in rows[:self.n]]
 
     def score_variable(self, lam, v, candidates, k):
         m = bin(int(candidates) & ~(1 << v)).count("1")

@@ -49,6 +49,7 @@ def lib():
         L.ulg_pdb_query.argtypes = [P, I64, P, P, P]
         L.ulg_astar.argtypes = [P, P, I, I, P, P, C.POINTER(F), C.POINTER(I64), C.c_char_p, I64]
         L.ulg_triplet_astar.argtypes = [P, P, I, P, P]
+        L.ulg_mmpc.argtypes = [P, D, I, P]
         L.ulg_pss_format.argtypes = [P, C.c_char_p, P, P, C.POINTER(C.c_void_p), C.POINTER(I64)]
         L.ulg_pss_format_lists.argtypes = [P, I, P, P, P, C.c_char_p, P, P, C.POINTER(C.c_void_p), C.POINTER(I64)]
         L.ulg_set_option.argtypes = [P, C.c_char_p, I64]
@@ -108,6 +109,12 @@ class Context:
         self._check(lib().ulg_cbic_load(self._h, _ptr(flat), N, n, float(lam)), "ulg_cbic_load")
         self.n = n
         self.N = N
+
+    def mmpc(self, alpha=0.05, max_cond=-1):
+        """ulg_mmpc on the loaded data -> skeleton rows (bit j of row i = edge i-j)."""
+        rows = np.zeros(64, dtype=np.uint64)
+        self._check(lib().ulg_mmpc(self._h, float(alpha), int(max_cond), _ptr(rows)), "ulg_mmpc")
+        return [int(x) for x in rows[:self.n]]
 
     def gram(self) -> np.ndarray:
         g = np.empty((self.n, self.n), dtype=np.float64)
