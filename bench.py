@@ -39,6 +39,9 @@ METRIC = "cBIC parent-set scores/sec + A* expansions/sec, n=25 full skeleton"
 CONFIGS = {
     "c2": dict(n=20, N=10000, k=4, lam=2.0),
     "c3": dict(n=25, N=10000, k=6, lam=2.0),
+    # BASELINE C4: n=30, N=100k, MMPC skeleton (built on the GPU from the same
+    # data, alpha 0.01), 2-hop candidate sets; k capped at the HIP scorer's 8
+    "c4": dict(n=30, N=100000, k=8, lam=2.0, skeleton="mmpc", alpha=0.01),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
@@ -112,7 +115,7 @@ def roofline(ctx, cfg, per_launch_sets):
              "fp64_tflops": sets * flops_per_set / (p["avg_ms"] * 1e-3) / 1e12}, p)
 
 
-def search_metrics(ctx, cfg, variables, cands, rank, ws, reps=3):
+def search_metrics(ctx, cfg, variables, cands, rank, ws, reps=3, edges=None, skel_note="full skeleton"):
     """Order-graph search side on this rank's scored lists: GPU best-score
     tables + pattern database + GPU layer-synchronous search at the bench
     config (A* expansions/s), then the exact-order A* (reference pop order,
@@ -120,8 +123,9 @@ def search_metrics(ctx, cfg, variables, cands, rank, ws, reps=3):
     import time as _t
     n, k = cfg["n"], cfg["k"]
     full = [(1 << n) - 1] * n
+    skel = full if edges is None else edges
     out = {}
-    ctx.score(list(range(n)), full, k)
+    ctx.score(list(range(n)), full if edges is None else ulg.candidates_from_edges(edges, n), k)
     t0 = _t.perf_counter()
     ctx.search_from_scores()
     t1 = _t.perf_counter()
@@ -130,10 +134,10 @@ def search_metrics(ctx, cfg, variables, cands, rank, ws, reps=3):
     best = None
     for _ in range(reps):
         ts = _t.perf_counter()
-        g = ctx.astar(edges=full, mode=1, net_text=False)
+        g = ctx.astar(edges=skel, mode=1, net_text=False)
         dt = _t.perf_counter() - ts
         best = dt if best is None else min(best, dt)
-    out["gpu_search"] = {"config": f"C3 lists (n={n}, k={k}), full skeleton, static PDB(2)",
+    out["gpu_search"] = {"config": f"{cfg['id'].upper()} lists (n={n}, k={k}), {skel_note}, static PDB(2)",
                          "expansions": g["expanded"], "ms": 1e3 * best,
                          "expansions_per_s": g["expanded"] / best, "goal_cost": g["cost"],
                          "tables_ms": 1e3 * (t1 - t0), "pdb_ms": 1e3 * (t2 - t1),
@@ -194,12 +198,19 @@ def main():
     ctx = ulg.Context(local)
     ctx.load(X, lam)
     cands_all = [(1 << n) - 1] * n
+    skel_note = "full n x n skeleton"
+    if cfg.get("skeleton") == "mmpc":
+        rows = ctx.mmpc(cfg["alpha"])
+        cands_all = ulg.candidates_from_edges(rows, n)
+        skel_note = (f"MMPC skeleton (ulg_mmpc, alpha {cfg['alpha']}: {sum(bin(r).count('1') for r in rows) // 2} "
+                     f"edges), 2-hop candidate sets")
     if args.mode == "shard":
         variables = shard.stripe(n, ws, rank)
     else:
         variables = list(range(n))
     cands = [cands_all[v] for v in variables]
-    units_rank = len(variables) * sum(math.comb(n - 1, L) for L in range(k + 1))
+    msz = [bin(cands_all[v] & ~(1 << v)).count("1") for v in range(n)]
+    units_rank = sum(sum(math.comb(msz[v], L) for L in range(k + 1)) for v in variables)
 
     def step():
         stored, scored = ctx.score(variables, cands, k)
@@ -240,13 +251,14 @@ def main():
         scored_all = float(scored_total)
 
     # sets in one launch of the dominant kernel (layer k, sets without variable 0)
-    per_launch = sum(math.comb(n - 1 - 1, k) for v in variables if v != 0) + (math.comb(n - 1, k) if 0 in variables else 0)
+    per_launch = sum(math.comb(msz[v] - (1 if (v != 0 and cands_all[v] & 1) else 0), k) for v in variables)
     roof, _ = roofline(ctx, cfg, per_launch)
     kernels = ctx.profile_dump()
 
     search = None
     if args.mode == "weak" and not args.no_search:
-        search = search_metrics(ctx, cfg, variables, cands, rank, ws)
+        search = search_metrics(ctx, cfg, variables, cands, rank, ws,
+                                edges=rows if cfg.get("skeleton") == "mmpc" else None, skel_note=skel_note)
 
     if rank == 0:
         res = {
@@ -261,10 +273,10 @@ def main():
             "scaling": "weak" if args.mode == "weak" else "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": f"synthetic: seeded linear-Gaussian SEM (synth.gaussian_sem, seed {9200}+rank), "
-                    f"full n x n skeleton",
-            "config": {"workload": f"C3 cBIC scoring: n={n}, N={N}, max-parents k={k}, lambda={lam}, full skeleton, "
-                                   f"all {n} variables per {'GPU' if args.mode == 'weak' else 'job'}",
+            "data": f"synthetic: seeded linear-Gaussian SEM (synth.gaussian_sem, seed {9200}+rank), {skel_note}",
+            "config": {"workload": f"{args.config.upper()} cBIC scoring: n={n}, N={N}, max-parents k={k}, "
+                                   f"lambda={lam}, {skel_note}, all {n} variables per "
+                                   f"{'GPU' if args.mode == 'weak' else 'job'}",
                        "config_id": args.config, "mode": args.mode,
                        "parent_sets_per_step_per_rank": units_rank},
             "roofline": roof,
