@@ -39,7 +39,10 @@ struct LayerArgs {
     const float *gprev;      // layer - 1
     float *gcur;             // layer
     uint8_t *leaf;           // leaf bytes of this layer
+    unsigned long long *reached;  // kCounters striped counters of reached nodes (null: the goal layer)
 };
+
+constexpr int kCounters = 256;
 
 __device__ __forceinline__ uint64_t Bn(const uint64_t *b, int a, int k) { return b[a * 33 + k]; }
 
@@ -50,8 +53,8 @@ __global__ void __launch_bounds__(kB) layer_pull_kernel(LayerArgs a) {
     for (int i = threadIdx.x; i < a.m; i += kB) cv[i] = a.comp_vars[i];
     __syncthreads();
     const uint64_t r = (uint64_t)blockIdx.x * kB + threadIdx.x;
-    if (r >= a.count) return;
     const int L = a.layer;
+    if (r >= a.count) return;
     // unrank T (colex over the component's compact bits)
     uint64_t Tc = 0;
     {
@@ -101,13 +104,12 @@ __global__ void __launch_bounds__(kB) layer_pull_kernel(LayerArgs a) {
     }
     a.gcur[r] = reached ? best : FLT_MAX;
     a.leaf[r] = (uint8_t)(reached ? bestj : 255);
-}
-
-__global__ void count_reached_kernel(const float *g, uint64_t count, unsigned long long *acc) {
-    const uint64_t r = (uint64_t)blockIdx.x * kB + threadIdx.x;
-    bool ok = r < count && g[r] < FLT_MAX;
-    const unsigned long long b = __ballot(ok);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(acc, (unsigned long long)__popcll(b));
+    if (a.reached) {
+        // nodes of this layer that are reached -- and so expanded, below the goal layer
+        const unsigned long long b = __ballot(reached);
+        if ((threadIdx.x & 63) == __ffsll((long long)__ballot(true)) - 1 && b)
+            atomicAdd(&a.reached[blockIdx.x % kCounters], (unsigned long long)__popcll(b));
+    }
 }
 
 // walk the leaf pointers from the goal back to the root (one thread)
@@ -186,13 +188,13 @@ int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, flo
     };
     int rc;
     if ((rc = ensure(c, d_bn, bn.size())) || (rc = ensure(c, d_edges, 64)) || (rc = ensure(c, d_cv, kMaxM)) ||
-        (rc = ensure(c, d_chain, kMaxM)) || (rc = ensure(c, d_acc, 1))) {
+        (rc = ensure(c, d_chain, kMaxM)) || (rc = ensure(c, d_acc, kCounters))) {
         cleanup();
         return rc;
     }
     hipError_t e = hipMemcpyAsync(d_bn.p, bn.data(), bn.size() * 8, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess && edges) e = hipMemcpyAsync(d_edges.p, edges, (size_t)n * 8, hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(d_acc.p, 0, 8, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d_acc.p, 0, kCounters * 8, c->stream);
     if (e != hipSuccess) { cleanup(); return set_err(c, ULG_ERR_HIP, hipGetErrorString(e)); }
     const SearchDev dv = s.dev();
     bool fail = false;
@@ -222,9 +224,8 @@ int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, flo
         float *gprev = d_g0.p, *gcur = d_g1.p;
         for (int d = 1; d <= m; ++d) {
             const uint64_t cnt = binom64(m, d);
-            // nodes of layer d-1 that are reached and expanded (the goal layer is not expanded)
-            count_reached_kernel<<<(unsigned)((binom64(m, d - 1) + kB - 1) / kB), kB, 0, c->stream>>>(gprev, binom64(m, d - 1), d_acc.p);
-            LayerArgs a{dv, d_bn.p, d_cv.p, d_edges.p, edges ? 1 : 0, m, d, cnt, gprev, gcur, d_leaf.p + loff[d]};
+            LayerArgs a{dv, d_bn.p, d_cv.p, d_edges.p, edges ? 1 : 0, m, d, cnt, gprev, gcur, d_leaf.p + loff[d],
+                        d < m ? d_acc.p : nullptr};
             prof_begin(c, "search_layer_pull");
             layer_pull_kernel<<<(unsigned)((cnt + kB - 1) / kB), kB, 0, c->stream>>>(a);
             prof_end(c);
@@ -258,12 +259,14 @@ int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, flo
         for (int v = 0; v < n; ++v) order[v] = total[v];
         *goal_cost = g;
     }
-    unsigned long long acc = 0;
-    e = hipMemcpy(&acc, d_acc.p, 8, hipMemcpyDeviceToHost);
+    std::vector<unsigned long long> acc(kCounters, 0);
+    e = hipMemcpy(acc.data(), d_acc.p, kCounters * 8, hipMemcpyDeviceToHost);
     prof_collect(c);
     cleanup();
     if (e != hipSuccess) return set_err(c, ULG_ERR_HIP, hipGetErrorString(e));
-    *expanded = (int64_t)acc;
+    int64_t total_reached = (int64_t)comps.size();  // every component's root (layer 0)
+    for (unsigned long long x : acc) total_reached += (int64_t)x;
+    *expanded = total_reached;
     if (fail) return set_err(c, ULG_ERR_STATE, "ulg_astar(GPU): a component has no goal");
     return ULG_OK;
 }
