@@ -180,6 +180,7 @@ def main():
     ap.add_argument("--mode", default="weak", choices=["weak", "shard"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-search", action="store_true")
+    ap.add_argument("--score-variant", type=int, default=None, help="A/B knob (ulg_set_option score_variant)")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -196,6 +197,8 @@ def main():
     seed = 9200 + (rank if args.mode == "weak" else 0)
     X, _ = synth.gaussian_sem(n, N, seed)
     ctx = ulg.Context(local)
+    if args.score_variant is not None:
+        ctx.set_option("score_variant", args.score_variant)
     ctx.load(X, lam)
     cands_all = [(1 << n) - 1] * n
     skel_note = "full n x n skeleton"

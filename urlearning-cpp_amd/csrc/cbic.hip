@@ -167,6 +167,7 @@ __device__ __forceinline__ uint64_t rank_colex(uint64_t mask, const uint32_t *bi
 // Per-lane bitset over the subsets of (P u {var 0}) in local numbering.
 template <int W>
 struct Bits {
+    static constexpr int kWords = W;
     uint64_t w[W];
     __device__ __forceinline__ void clear() {
 #pragma unroll
@@ -183,6 +184,25 @@ struct Bits {
 #pragma unroll
         for (int j = 0; j < W; ++j) w[j] |= ((int)(i >> 6) == j) ? bit : 0ull;
     }
+    __device__ __forceinline__ uint64_t word(int j) const { return w[j]; }
+};
+
+// The same bitset with its words in LDS, thread-interleaved (word j of this
+// thread at base[j * kBlock]).  For W >= 4 the compiler turns the register
+// select chains back into indexed accesses and puts the arrays in scratch
+// (global memory) -- every walk test then pays a memory round trip; LDS keeps
+// the indexing cheap.
+template <int W>
+struct BitsLds {
+    static constexpr int kWords = W;
+    uint64_t *base;
+    __device__ __forceinline__ void clear() {
+#pragma unroll
+        for (int j = 0; j < W; ++j) base[j * kBlock] = 0;
+    }
+    __device__ __forceinline__ bool test(uint32_t i) const { return (base[(i >> 6) * kBlock] >> (i & 63)) & 1ull; }
+    __device__ __forceinline__ void set(uint32_t i) { base[(i >> 6) * kBlock] |= 1ull << (i & 63); }
+    __device__ __forceinline__ uint64_t word(int j) const { return base[j * kBlock]; }
 };
 
 // find_best_subset_score (BIC_OLS.cpp:125-172) replayed on local masks.
@@ -190,9 +210,8 @@ struct Bits {
 // are 0 == variable 0, the zero-initialised arma::uvec of SURVEY N3).  Only
 // WHICH cached keys are visited matters: the return value is the max over
 // their cached values (and 0), so the recursion records them in `visited`.
-template <int M, int W>
-__device__ __forceinline__ void best_subset(uint32_t T, uint32_t pv, const Bits<W> &present, Bits<W> &checked,
-                                            Bits<W> &visited) {
+template <int M, class BS>
+__device__ __forceinline__ void best_subset(uint32_t T, uint32_t pv, const BS &present, BS &checked, BS &visited) {
 #pragma nounroll
     for (int idx = 0; idx < M; ++idx) {
         const uint32_t u = (pv >> (4 * idx)) & 15u;
@@ -211,7 +230,7 @@ __device__ __forceinline__ void best_subset(uint32_t T, uint32_t pv, const Bits<
                 if (pi == u) continue;
                 npv |= pi << (4 * j);
                 ++j;
-                best_subset<M - 1, W>(T2, npv, present, checked, visited);
+                best_subset<M - 1, BS>(T2, npv, present, checked, visited);
                 checked.set(T2);
             }
         }
@@ -230,9 +249,8 @@ __device__ __forceinline__ void best_subset(uint32_t T, uint32_t pv, const Bits<
 // little, while the extra exits cost issue slots.  An equivalent walk without
 // the reference's redundant re-tests (2.2x fewer union points per wave in a
 // host simulation) measured 5.6 ms: heavier control flow, occupancy 2.
-template <int M, int W>
-__device__ __forceinline__ bool dominated(uint32_t T, uint32_t pv, const Bits<W> &present, const Bits<W> &hi,
-                                          Bits<W> &checked) {
+template <int M, class BS>
+__device__ __forceinline__ bool dominated(uint32_t T, uint32_t pv, const BS &present, const BS &hi, BS &checked) {
 #pragma nounroll
     for (int idx = 0; idx < M; ++idx) {
         const uint32_t u = (pv >> (4 * idx)) & 15u;
@@ -251,7 +269,7 @@ __device__ __forceinline__ bool dominated(uint32_t T, uint32_t pv, const Bits<W>
                 if (pi == u) continue;
                 npv |= pi << (4 * j);
                 ++j;
-                if (dominated<M - 1, W>(T2, npv, present, hi, checked)) return true;
+                if (dominated<M - 1, BS>(T2, npv, present, hi, checked)) return true;
                 checked.set(T2);
             }
         }
@@ -266,9 +284,9 @@ __device__ __forceinline__ bool dominated(uint32_t T, uint32_t pv, const Bits<W>
 // Saved frames live in LDS, one u64 per frame, lane-interleaved
 // (stk[slot * kBlock + tid]): T | idx << 10 | j << 14 | pv << 18; the loop
 // position i and the partial vector npv are re-derived from (pv, u, j).
-template <int L, int W>
-__device__ __forceinline__ void best_subset_stack(uint32_t Ptop, uint32_t pvtop, const Bits<W> &present,
-                                                  Bits<W> &checked, Bits<W> &visited, uint64_t *stk) {
+template <int L, class BS>
+__device__ __forceinline__ void best_subset_stack(uint32_t Ptop, uint32_t pvtop, const BS &present, BS &checked,
+                                                  BS &visited, uint64_t *stk) {
     const int tid = threadIdx.x;
     uint32_t T = Ptop, pv = pvtop, npv = 0, u = 0;
     int sp = 0, m = L, idx = 0, i = 0, j = 0;
@@ -377,20 +395,36 @@ struct ScoreArgs {
     int n, nv, S;
 };
 
-// LDS carve: gram | binom | work | tbl_off | recursion stack (16-B aligned)
+// bitset words per lane over the subsets of L + 1 local bits
+__host__ __device__ constexpr int bits_words(int L) { return (L + 1) <= 6 ? 1 : (1 << ((L + 1) - 6)); }
+
+// LDS carve: gram | binom | work | tbl_off | recursion stack (variant bit 1)
+// | LDS bitsets (3 per lane when they have >= 4 words) (16-B aligned)
 struct LdsLayout {
-    int gram, binom, work, toff, stack, total;
+    int gram, binom, work, toff, stack, bits, total;
 };
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
-__host__ __device__ inline LdsLayout lds_layout(int n, int nv, int S, int L) {
+__host__ __device__ inline LdsLayout lds_layout(int n, int nv, int S, int L, int V) {
     LdsLayout l;
     l.gram = 0;
     l.binom = align16(l.gram + n * n * 8);
     l.work = align16(l.binom + 64 * kBinomK * 4);
     l.toff = align16(l.work + (nv + 1) * 8);
     l.stack = align16(l.toff + (nv * S + 1) * 8);
-    l.total = l.stack + L * kBlock * 8;
+    l.bits = align16(l.stack + ((V & 2) && !(V & 4) ? L * kBlock * 8 : 0));
+    const int W = bits_words(L);
+    l.total = l.bits + (W >= 4 ? 3 * W * kBlock * 8 : 0);
     return l;
+}
+
+template <class BS>
+__device__ __forceinline__ BS make_bits(uint64_t *lds_base) {
+    if constexpr (std::is_same<BS, Bits<BS::kWords>>::value) {
+        (void)lds_base;
+        return BS{};
+    } else {
+        return BS{lds_base};
+    }
 }
 
 // PHASE 0: sets containing variable 0; 1: the rest.  V = variant bits (see
@@ -399,7 +433,7 @@ __host__ __device__ inline LdsLayout lds_layout(int n, int nv, int S, int L) {
 template <int L, int PHASE, int V>
 __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const LdsLayout lay = lds_layout(a.n, a.nv, a.S, L);
+    const LdsLayout lay = lds_layout(a.n, a.nv, a.S, L, V);
     double *g = reinterpret_cast<double *>(smem + lay.gram);
     uint32_t *binom = reinterpret_cast<uint32_t *>(smem + lay.binom);
     uint64_t *work = reinterpret_cast<uint64_t *>(smem + lay.work);
@@ -491,7 +525,9 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         const float s = -ts;
         out = (s < 0.0f) ? s : absent_f();
     } else {
-        constexpr int W = (L + 1) <= 6 ? 1 : (1 << ((L + 1) - 6));
+        constexpr int W = bits_words(L);
+        using BS = std::conditional_t<(W >= 4), BitsLds<W>, Bits<W>>;
+        uint64_t *lds_bits = reinterpret_cast<uint64_t *>(smem + lay.bits) + threadIdx.x;
         const bool v0inP = z && (cm & 1ull);
         const uint64_t E = z ? (cm & ~1ull) : cm;
         uint64_t cpack = 0;  // local bit -> compact index, 6 bits each (bit 0 -> 0)
@@ -511,9 +547,12 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         const uint64_t vbase = (uint64_t)vi * a.S;
 
         // presence of every candidate key in the cache as it stands now
-        Bits<W> present, hi;
+        // the first LDS bitset is `present`; `hi` and `checked` share the
+        // second (only the decision-only walk uses `hi`); `visited` the third
+        BS present = make_bits<BS>(lds_bits);
+        BS hi = make_bits<BS>(lds_bits + (size_t)W * kBlock);
         present.clear();
-        hi.clear();
+        if constexpr ((V & 4) != 0) hi.clear();
         const float thr = -ts;
         if constexpr (L <= 6 && (V & 1)) {
             presence_unrolled<L, PHASE, (PHASE == 0 ? L : L + 1), W>(present, hi, thr, binom, cpack, z, a.table,
@@ -550,31 +589,32 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
             // otherwise walk until the first visited key >= -ts
             bool any = false;
 #pragma unroll
-            for (int wj = 0; wj < W; ++wj) any |= hi.w[wj] != 0ull;
+            for (int wj = 0; wj < W; ++wj) any |= hi.word(wj) != 0ull;
             bool dom = false;
             if (any) {
 #pragma unroll
                 for (int i = 0; i < L; ++i) dom |= hi.test(Plocal ^ (1u << ((pvtop >> (4 * i)) & 15u)));
                 if (!dom) {
-                    Bits<W> checked;
+                    BS checked = make_bits<BS>(lds_bits + (size_t)2 * W * kBlock);
                     checked.clear();
                     checked.set(0u);
-                    dom = dominated<L, W>(Plocal, pvtop, present, hi, checked);
+                    dom = dominated<L, BS>(Plocal, pvtop, present, hi, checked);
                 }
             }
             out = dom ? absent_f() : -ts;
         } else {
-        Bits<W> checked, visited;
+        BS checked = make_bits<BS>(lds_bits + (size_t)W * kBlock);
+        BS visited = make_bits<BS>(lds_bits + (size_t)2 * W * kBlock);
         checked.clear();
         visited.clear();
         checked.set(0u);  // checked.insert(empty_set)
-        if constexpr ((V & 2) != 0) best_subset_stack<L, W>(Plocal, pvtop, present, checked, visited, stk);
-        else best_subset<L, W>(Plocal, pvtop, present, checked, visited);
+        if constexpr ((V & 2) != 0) best_subset_stack<L, BS>(Plocal, pvtop, present, checked, visited, stk);
+        else best_subset<L, BS>(Plocal, pvtop, present, checked, visited);
 
         float best = 0.0f;
 #pragma unroll
         for (int wj = 0; wj < W; ++wj) {
-            uint64_t x = visited.w[wj];
+            uint64_t x = visited.word(wj);
             while (x) {
                 const uint32_t t = (uint32_t)(wj * 64 + __builtin_ctzll(x));
                 x &= x - 1;
@@ -917,9 +957,12 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
             sa.work = c->d_work.p + ((size_t)L * 2 + ph) * (nv + 1);
             const uint64_t blocks = (cnt + kBlock - 1) / kBlock;
             if (blocks > 0x7fffffffull) return set_err(c, ULG_ERR_UNSUPPORTED, "ulg_cbic_score: layer too large");
-            const LdsLayout lay = lds_layout(n, nv, S, L);
+            const LdsLayout lay = lds_layout(n, nv, S, L, c->score_variant);
             prof_begin(c, kLayerNames[ph][L]);
-            hipLaunchKernelGGL(layer_kernel(L, ph, c->score_variant), dim3((unsigned)blocks), dim3(kBlock), (size_t)lay.total, c->stream, sa);
+            const KernelFn kfn = layer_kernel(L, ph, c->score_variant);
+            if (lay.total > 64 * 1024)
+                ULG_HIP(c, hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, lay.total));
+            hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(kBlock), (size_t)lay.total, c->stream, sa);
             prof_end(c);
         }
     ULG_HIP(c, hipGetLastError());
