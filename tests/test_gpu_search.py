@@ -70,6 +70,29 @@ def test_bestscore_tables_heterogeneous_supports(ulg_ctx, oracle_built):
         assert int(p) == ep, (v, S, p, ep)
 
 
+@pytest.mark.parametrize("n", [16, 25])
+def test_bestscore_big_tables_register_zeta(ulg_ctx, oracle_built, n):
+    """Tables of >= 2^14 entries per variable take the sorted-entries tile
+    build and the register-blocked subset-min (pass A for every m >= 14, pass
+    B when a variable has 10 bits above bit 14: n = 25 gives m = 24)."""
+    o = oracle_built
+    X, _ = synth.gaussian_sem(n, 2000, 9303 + n)
+    offs, sets, scores, costs = _oracle_pipeline(o, X, 0.5, 2)
+    ulg_ctx.search_load(offs, sets, costs)
+    srch = o.Search(n, offs, sets, costs)
+    rng = np.random.default_rng(n)
+    vs = [int(v) for v in rng.integers(0, n, 20000)]
+    Ss = _random_subsets(rng, n, 20000)
+    # subsets near the top and the bottom of the lattice as well
+    Ss[:64] = [(1 << n) - 1 - (1 << int(b)) for b in rng.integers(0, n, 64)]
+    Ss[64:128] = [1 << int(b) for b in rng.integers(0, n, 64)]
+    gc, gp = ulg_ctx.bestscore(vs, Ss)
+    for v, S, c, p in zip(vs, Ss, gc, gp):
+        ec, ep = srch.bestscore(v, S)
+        assert np.float32(c) == np.float32(ec), (v, S, c, ec)
+        assert int(p) == ep, (v, S, p, ep)
+
+
 def test_bestscore_ties_fall_to_file_order(ulg_ctx, oracle_built):
     """Equal costs: the first set in file order wins (pinned N7)."""
     o = oracle_built

@@ -15,6 +15,8 @@
 // transform: bits 0..13 inside 128 KiB LDS tiles, the remaining bits in a
 // second pass over strided tiles whose rows are 16 contiguous entries.  Both
 // passes stream the table once (HBM-bound).  Lookup: key = T_v[pext(S, D_v)].
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
@@ -137,6 +139,142 @@ __global__ void __launch_bounds__(1024) zeta_strided_kernel(ZetaBArgs a) {
         const uint64_t hc = (uint64_t)(e >> kRowBits), lw = (uint64_t)(e & 15);
         tv[base | (hc << bit_lo) | lw] = t[e];
     }
+}
+
+// ---- register-blocked subset-min for the big tables ---------------------------
+// A 2^14-entry tile (or a 2^10-row x 16-column strided tile) is handled by 1024
+// threads holding 16 entries each: the min along 4 index bits at a time runs
+// in registers, and LDS only exchanges the entries between the 4-bit windows
+// (3 exchanges instead of one LDS sweep per bit).  The subset-min along one
+// bit is idempotent, so windows may overlap (bits 0-3, 4-7, 8-11, 10-13).
+// LDS rows of 16 entries are padded by one entry against bank conflicts.
+constexpr int kRegTileBits = 14;
+constexpr int kPadLds = (1 << kRegTileBits) + (1 << (kRegTileBits - 4));
+
+__device__ __forceinline__ int padx(int e) { return e + (e >> 4); }
+
+__device__ __forceinline__ void min4(uint64_t (&r)[16]) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (i & (1 << b)) r[i] = r[i ^ (1 << b)] < r[i] ? r[i ^ (1 << b)] : r[i];
+}
+
+// one (global table index, packed key) per stored set inside the tables' scope
+__global__ void __launch_bounds__(kB) entries_kernel(const uint64_t *sets, const float *costs, const int64_t *offsets,
+                                                     int n, const uint64_t *support, const uint64_t *tb_off,
+                                                     uint64_t *idx, uint64_t *key) {
+    const int v = blockIdx.y;
+    const int64_t b = offsets[v], e = offsets[v + 1];
+    const uint64_t D = support[v];
+    for (int64_t i = b + (int64_t)blockIdx.x * kB + threadIdx.x; i < e; i += (int64_t)gridDim.x * kB) {
+        if (sets[i] & ~D) {
+            idx[i] = ~0ull;  // outside the scope: sorts past every slot
+            key[i] = ~0ull;
+            continue;
+        }
+        idx[i] = tb_off[v] + pext64(sets[i], D);
+        key[i] = ((uint64_t)ordkey(costs[i]) << 32) | (uint64_t)(i - b);
+    }
+}
+
+__device__ __forceinline__ int64_t lower_bound_u64(const uint64_t *a, int64_t n, uint64_t x) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// pass A for tables of >= 2^14 entries: builds each tile from its sorted
+// entries (no fill, no read of the table) and writes it once
+__global__ void __launch_bounds__(1024) zeta_tile_reg_kernel(uint64_t *table, uint64_t ntiles_total,
+                                                             const uint64_t *eidx, const uint64_t *ekey,
+                                                             int64_t nent) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t *t = reinterpret_cast<uint64_t *>(smem);
+    __shared__ int64_t range[2];
+    const int tid = threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x << kRegTileBits;  // tiles are contiguous over all variables
+    if (tid == 0) {
+        range[0] = lower_bound_u64(eidx, nent, base);
+        range[1] = lower_bound_u64(eidx, nent, base + (1ull << kRegTileBits));
+    }
+    for (int i = tid; i < (1 << kRegTileBits); i += 1024) t[padx(i)] = ~0ull;
+    __syncthreads();
+    for (int64_t k = range[0] + tid; k < range[1]; k += 1024) t[padx((int)(eidx[k] - base))] = ekey[k];
+    __syncthreads();
+    uint64_t r[16];
+    // bits 0-3: entries tid*16 + i
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = t[padx(tid * 16 + i)];
+    min4(r);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t[padx(tid * 16 + i)] = r[i];
+    __syncthreads();
+    // bits 4-7
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = t[padx(((tid >> 4) << 8) | (i << 4) | (tid & 15))];
+    min4(r);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t[padx(((tid >> 4) << 8) | (i << 4) | (tid & 15))] = r[i];
+    __syncthreads();
+    // bits 8-11
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = t[padx(((tid >> 8) << 12) | (i << 8) | (tid & 255))];
+    min4(r);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t[padx(((tid >> 8) << 12) | (i << 8) | (tid & 255))] = r[i];
+    __syncthreads();
+    // bits 10-13, straight to HBM (consecutive threads, consecutive entries)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = t[padx((i << 10) | tid)];
+    min4(r);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) table[base + ((uint64_t)i << 10) + tid] = r[i];
+    (void)ntiles_total;
+}
+
+// pass B for 10 index bits [bit_lo, bit_lo + 10) of tables with m >= bit_lo + 10:
+// a tile is 1024 rows (those bits) x 16 contiguous entries (bits 0-3)
+__global__ void __launch_bounds__(1024) zeta_strided_reg_kernel(ZetaBArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t *t = reinterpret_cast<uint64_t *>(smem);
+    int lo = 0, hi = a.nvar;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (a.blocks_prefix[mid] <= (int)blockIdx.x) lo = mid; else hi = mid;
+    }
+    const int v = lo;
+    const int bit_lo = a.bit_lo;
+    const int nlow = bit_lo - kRowBits;
+    const uint64_t bid = blockIdx.x - a.blocks_prefix[v];
+    uint64_t *tv = a.table + a.tb_off[v];
+    const uint64_t base = ((bid & ((1ull << nlow) - 1)) << kRowBits) | ((bid >> nlow) << (bit_lo + 10));
+    const int tid = threadIdx.x, c = tid & 15, q = tid >> 4;
+    uint64_t r[16];
+    // row bits 0-3: rows (q << 4) | i
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = tv[base | ((uint64_t)((q << 4) | i) << bit_lo) | c];
+    min4(r);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t[padx((((q << 4) | i) << 4) | c)] = r[i];
+    __syncthreads();
+    // row bits 4-7: rows ((q >> 4) << 8) | (i << 4) | (q & 15)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = t[padx(((((q >> 4) << 8) | (i << 4) | (q & 15)) << 4) | c)];
+    min4(r);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t[padx(((((q >> 4) << 8) | (i << 4) | (q & 15)) << 4) | c)] = r[i];
+    __syncthreads();
+    // row bits 6-9: rows (i << 6) | q, back to HBM
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = t[padx((((i << 6) | q) << 4) | c)];
+    min4(r);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) tv[base | ((uint64_t)((i << 6) | q) << bit_lo) | c] = r[i];
 }
 
 __global__ void __launch_bounds__(kB) cost_table_kernel(const uint64_t *table, uint64_t total, float *costs) {
@@ -264,6 +402,38 @@ int search_build_tables(ulg_ctx *c, uint64_t scope) {
         return rc;
     ULG_HIP(c, hipMemcpyAsync(s.d_tb_off.p, s.tb_off.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, c->stream));
     ULG_HIP(c, hipMemcpyAsync(s.d_mbits.p, s.mbits.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+    const int minm = *std::min_element(s.mbits.begin(), s.mbits.end());
+    std::vector<int> tiles_prefix(n + 1, 0), blocks_prefix(n + 1, 0);
+    if ((rc = ensure(c, s.d_prefix, (size_t)2 * (n + 1)))) return rc;
+    if (minm >= kRegTileBits) {
+        // every table is whole 2^14-entry tiles: sort the stored sets by table
+        // index once and build each tile from its entries (no fill, no read)
+        const int64_t nsets = s.offsets[n];
+        if ((rc = ensure(c, s.e_idx, (size_t)nsets)) || (rc = ensure(c, s.e_key, (size_t)nsets)) ||
+            (rc = ensure(c, s.e_idx2, (size_t)nsets)) || (rc = ensure(c, s.e_key2, (size_t)nsets)))
+            return rc;
+        prof_begin(c, "bs_entries");
+        entries_kernel<<<dim3(gx, n), kB, 0, c->stream>>>(s.d_sets.p, s.d_costs.p, s.d_offsets.p, n, s.d_support.p,
+                                                         s.d_tb_off.p, s.e_idx.p, s.e_key.p);
+        prof_end(c);
+        int end_bit = 1;
+        while (end_bit < 64 && (1ull << (end_bit - 1)) <= total) ++end_bit;  // ~0 sorts past every slot
+        size_t tmp = 0;
+        ULG_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, s.e_idx.p, s.e_idx2.p, s.e_key.p, s.e_key2.p,
+                                                      (int)nsets, 0, end_bit, c->stream));
+        if ((rc = ensure(c, s.sort_tmp, tmp))) return rc;
+        prof_begin(c, "bs_sort");
+        ULG_HIP(c, hipcub::DeviceRadixSort::SortPairs(s.sort_tmp.p, tmp, s.e_idx.p, s.e_idx2.p, s.e_key.p, s.e_key2.p,
+                                                      (int)nsets, 0, end_bit, c->stream));
+        prof_end(c);
+        ULG_HIP(c, hipFuncSetAttribute((const void *)zeta_tile_reg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       kPadLds * 8));
+        prof_begin(c, "bs_zeta_tile");
+        zeta_tile_reg_kernel<<<(unsigned)(total >> kRegTileBits), 1024, (size_t)kPadLds * 8, c->stream>>>(
+            s.d_table.p, total >> kRegTileBits, s.e_idx2.p, s.e_key2.p, nsets);
+        prof_end(c);
+        ULG_HIP(c, hipGetLastError());
+    } else {
     prof_begin(c, "bs_fill");
     ULG_HIP(c, hipMemsetAsync(s.d_table.p, 0xff, total * 8, c->stream));
     prof_end(c);
@@ -272,20 +442,20 @@ int search_build_tables(ulg_ctx *c, uint64_t scope) {
                                                      s.d_tb_off.p, s.d_table.p);
     prof_end(c);
     // pass A tiles
-    std::vector<int> tiles_prefix(n + 1, 0), blocks_prefix(n + 1, 0);
     for (int v = 0; v < n; ++v) {
         const int m = s.mbits[v];
         tiles_prefix[v + 1] = tiles_prefix[v] + (m <= kTileBits ? 1 : (1 << (m - kTileBits)));
     }
-    if ((rc = ensure(c, s.d_prefix, (size_t)2 * (n + 1)))) return rc;
     ULG_HIP(c, hipMemcpyAsync(s.d_prefix.p, tiles_prefix.data(), (size_t)(n + 1) * 4, hipMemcpyHostToDevice, c->stream));
-    const int maxm = *std::max_element(s.mbits.begin(), s.mbits.end());
-    const size_t ldsA = (size_t)8 << std::min(maxm, kTileBits);
+    const int maxm0 = *std::max_element(s.mbits.begin(), s.mbits.end());
+    const size_t ldsA = (size_t)8 << std::min(maxm0, kTileBits);
     ULG_HIP(c, hipFuncSetAttribute((const void *)zeta_tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(8 << kTileBits)));
     prof_begin(c, "bs_zeta_tile");
     zeta_tile_kernel<<<tiles_prefix[n], 1024, ldsA, c->stream>>>(s.d_table.p, s.d_tb_off.p, s.d_prefix.p, s.d_mbits.p, n);
     prof_end(c);
     ULG_HIP(c, hipGetLastError());
+    }
+    const int maxm = *std::max_element(s.mbits.begin(), s.mbits.end());
     // pass B over the remaining high bits, kColBits at a time
     ULG_HIP(c, hipFuncSetAttribute((const void *)zeta_strided_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(8 << (kColBits + kRowBits))));
     for (int bit_lo = kTileBits; bit_lo < maxm; bit_lo += kColBits) {
@@ -300,8 +470,17 @@ int search_build_tables(ulg_ctx *c, uint64_t scope) {
         ULG_HIP(c, hipMemcpyAsync(s.d_prefix.p + (n + 1), blocks_prefix.data(), (size_t)(n + 1) * 4, hipMemcpyHostToDevice, c->stream));
         ZetaBArgs za{s.d_table.p, s.d_tb_off.p, s.d_prefix.p + (n + 1), s.d_mbits.p, n, bit_lo};
         const int G = std::min(kColBits, maxm - bit_lo);
+        bool full_window = kColBits == 10;
+        for (int v = 0; v < n; ++v)
+            if (s.mbits[v] > bit_lo && s.mbits[v] - bit_lo < 10) full_window = false;
         prof_begin(c, "bs_zeta_strided");
-        zeta_strided_kernel<<<blocks_prefix[n], 1024, (size_t)8 << (G + kRowBits), c->stream>>>(za);
+        if (full_window) {
+            ULG_HIP(c, hipFuncSetAttribute((const void *)zeta_strided_reg_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kPadLds * 8));
+            zeta_strided_reg_kernel<<<blocks_prefix[n], 1024, (size_t)kPadLds * 8, c->stream>>>(za);
+        } else {
+            zeta_strided_kernel<<<blocks_prefix[n], 1024, (size_t)8 << (G + kRowBits), c->stream>>>(za);
+        }
         prof_end(c);
         ULG_HIP(c, hipGetLastError());
         // host copy of blocks_prefix must stay valid until the copy ran

@@ -159,6 +159,8 @@ struct SearchState {
     std::vector<int> mbits;
     uint64_t table_entries = 0;
     DevBuf<uint64_t> d_table, d_tb_off, d_support;
+    DevBuf<uint64_t> e_idx, e_key, e_idx2, e_key2;  // sorted (table index, key) of the stored sets
+    DevBuf<unsigned char> sort_tmp;
     DevBuf<int> d_mbits, d_prefix;
     bool lists_ready = false;   // the per-variable lists are on the device
     bool tables_ready = false;  // the lattice tables are built for `scope`
@@ -201,6 +203,7 @@ struct SearchState {
     void release_all() {
         release(d_sets); release(d_costs); release(d_scores_tmp); release(d_offsets);
         release(d_table); release(d_tb_off); release(d_support); release(d_mbits); release(d_prefix);
+        release(e_idx); release(e_key); release(e_idx2); release(e_key2); release(sort_tmp);
         release(d_cost_table); release(d_pd); release(d_bsv); release(d_bitpos); release(d_groups);
         release(q_vars); release(q_sets); release(q_par); release(q_costs);
         if (host_costs) (void)hipHostFree(host_costs);
