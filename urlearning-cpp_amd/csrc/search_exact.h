@@ -44,6 +44,7 @@ struct HostTables {
         return g_have_bmi2 ? pext_bmi2(S, D) : pext64(S, D);
     }
     inline float bs(int v, uint64_t S) const { return cost[tb_off[v] + index(v, S)]; }
+    inline void prefetch_bs(int v, uint64_t S) const { __builtin_prefetch(&cost[tb_off[v] + index(v, S)]); }
     inline uint64_t gidx(uint64_t vs, uint64_t grp) const { return g_have_bmi2 ? pext_bmi2(vs, grp) : pext64(vs, grp); }
     // StaticPatternDatabase::h (static_pattern_database.cpp:145-174)
     inline float h(uint64_t S, bool *complete) const {
@@ -62,7 +63,12 @@ struct HostTables {
     }
 };
 
-// generatedNodes (NodeMap): open addressing u64 -> node index
+// generatedNodes (NodeMap) over the subsets of one scope: a dense array
+// indexed by pext(S, scope) while 2^|scope| x 4 B stays small (one cached
+// read per probe, no hashing), else open addressing.
+struct SubsetIndex;
+
+// open addressing u64 -> node index
 struct NodeIndex {
     std::vector<uint64_t> keys;
     std::vector<uint32_t> vals;
@@ -105,6 +111,33 @@ struct NodeIndex {
         if (keys[i] == kEmpty) ++size;
         keys[i] = k;
         vals[i] = v;
+    }
+};
+
+struct SubsetIndex {
+    static constexpr int kDenseBits = 27;  // 512 MB of u32
+    uint64_t scope = 0;
+    bool dense = false;
+    std::vector<uint32_t> slots;
+    NodeIndex hash;
+    void init(uint64_t the_scope) {
+        scope = the_scope;
+        dense = __builtin_popcountll(scope) <= kDenseBits;
+        if (dense) slots.assign((size_t)1 << __builtin_popcountll(scope), UINT32_MAX);
+        else hash.init(1 << 16);
+    }
+    inline uint64_t slot(uint64_t S) const { return g_have_bmi2 ? pext_bmi2(S, scope) : pext64(S, scope); }
+    inline int64_t find(uint64_t S) const {
+        if (!dense) return hash.find(S);
+        const uint32_t v = slots[slot(S)];
+        return v == UINT32_MAX ? -1 : (int64_t)v;
+    }
+    inline void insert(uint64_t S, uint32_t v) {
+        if (dense) slots[slot(S)] = v;
+        else hash.insert(S, v);
+    }
+    inline void prefetch(uint64_t S) const {
+        if (dense) __builtin_prefetch(&slots[slot(S)]);
     }
 };
 

@@ -63,8 +63,8 @@ int astar_one(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool skele
     const int n = T.n;
     std::vector<Node> nodes;
     nodes.reserve(1 << 16);
-    NodeIndex generated;
-    generated.init(1 << 16);
+    SubsetIndex generated;
+    generated.init(ancestors | the_scc);
     Heap open;
     open.nodes = &nodes;
     const uint64_t r1 = the_scc >> 1;
@@ -82,10 +82,23 @@ int astar_one(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool skele
         if (nodes[ui].g + nodes[ui].h > upperBound) break;
         nodes[ui].pq = -2;
         const float ug = nodes[ui].g;
-        for (int leaf = 0; leaf < n; ++leaf) {
-            if ((variables >> leaf) & 1ull) continue;
-            if (!((the_scc >> leaf) & 1ull)) continue;
-            if (skeleton_good && variables != 0 && (variables & edges[leaf]) == 0) continue;
+        // the successors' index slots and lattice entries are independent
+        // cache misses: issue them all before the first use
+        // (bs(leaf, S u {leaf}) and bs(leaf, S) share one entry: leaf is
+        // never in its own support)
+        uint64_t leaves = the_scc & ~variables;
+        if (skeleton_good && variables != 0)
+            for (uint64_t x = leaves; x; x &= x - 1) {
+                const int leaf = __builtin_ctzll(x);
+                if ((variables & edges[leaf]) == 0) leaves &= ~(1ull << leaf);
+            }
+        for (uint64_t x = leaves; x; x &= x - 1) {
+            const int leaf = __builtin_ctzll(x);
+            generated.prefetch(variables | (1ull << leaf));
+            T.prefetch_bs(leaf, variables);
+        }
+        for (uint64_t x = leaves; x; x &= x - 1) {
+            const int leaf = __builtin_ctzll(x);
             const uint64_t nv = variables | (1ull << leaf);
             const int64_t si = generated.find(nv);
             if (si < 0) {

@@ -76,8 +76,8 @@ int cluster_astar(Triplet &t, uint64_t cluster, std::vector<uint64_t> &op) {
     op.assign(n, 0);
     std::vector<Node> nodes;
     nodes.reserve(1024);
-    NodeIndex generated;
-    generated.init(1024);
+    SubsetIndex generated;
+    generated.init(cluster);
     Heap open;
     open.nodes = &nodes;
     const uint64_t r1 = cluster >> 1;
@@ -94,6 +94,11 @@ int cluster_astar(Triplet &t, uint64_t cluster, std::vector<uint64_t> &op) {
         nodes[ui].pq = -2;
         const float ug = nodes[ui].g;
         uint64_t cand = cluster & ~variables;
+        for (uint64_t x = cand; x; x &= x - 1) {
+            const int leaf = __builtin_ctzll(x);
+            generated.prefetch(variables | (1ull << leaf));
+            T.prefetch_bs(leaf, variables);
+        }
         while (cand) {
             const int leaf = __builtin_ctzll(cand);
             cand &= cand - 1;
