@@ -142,25 +142,37 @@ struct SubsetIndex {
 };
 
 // PriorityQueue with the reference's heap algorithms and pqPos bookkeeping.
+// Heap entries carry their node's f = g + h and layer, so a comparison reads
+// the (mostly contiguous) heap array instead of two random Node records.
+// Invariant: every entry's f is its node's current g + h -- what the
+// reference's comparator reads through the node pointer.  A decrease-key
+// refreshes the entry at the node's recorded position; when that position is
+// stale (the reference's __down_heap does not record moves), the node's own
+// entry is found by a scan and refreshed, and the stale slot is sifted as the
+// reference sifts it.
+struct HeapEnt {
+    float f;
+    int32_t layer;
+    uint32_t idx;
+};
+
 struct Heap {
-    std::vector<uint32_t> a;
+    std::vector<HeapEnt> a;
     std::vector<Node> *nodes;
     bool hang = false;
 
+    inline HeapEnt ent(uint32_t x) const {
+        const Node &N = (*nodes)[x];
+        return HeapEnt{N.g + N.h, __builtin_popcountll(N.sub) & 0xff, x};
+    }
     // CompareNodeStar: true if x has LOWER priority than y
-    inline bool cns(uint32_t x, uint32_t y) const {
-        const Node &A = (*nodes)[x], &B = (*nodes)[y];
-        const float fa = A.g + A.h;
-        const float fb = B.g + B.h;
-        const float diff = fa - fb;
-        if (std::fabs(diff) < FLT_EPSILON) {
-            const int la = __builtin_popcountll(A.sub) & 0xff, lb = __builtin_popcountll(B.sub) & 0xff;
-            return (lb - la) > 0;
-        }
+    static inline bool cns(const HeapEnt &A, const HeapEnt &B) {
+        const float diff = A.f - B.f;
+        if (std::fabs(diff) < FLT_EPSILON) return (B.layer - A.layer) > 0;
         return diff > 0;
     }
-    inline void setpos(uint32_t x, int64_t p) { (*nodes)[x].pq = (int32_t)p; }
-    void push_hole(int64_t hole, int64_t top, uint32_t value) {
+    inline void setpos(const HeapEnt &e, int64_t p) { (*nodes)[e.idx].pq = (int32_t)p; }
+    void push_hole(int64_t hole, int64_t top, HeapEnt value) {
         int64_t parent = (hole - 1) / 2;
         while (hole > top && cns(a[parent], value)) {
             a[hole] = a[parent];
@@ -172,10 +184,11 @@ struct Heap {
         setpos(value, hole);
     }
     void push(uint32_t x) {
-        a.push_back(x);
-        push_hole((int64_t)a.size() - 1, 0, x);
+        const HeapEnt e = ent(x);
+        a.push_back(e);
+        push_hole((int64_t)a.size() - 1, 0, e);
     }
-    void adjust(int64_t hole, int64_t len, uint32_t value) {
+    void adjust(int64_t hole, int64_t len, HeapEnt value) {
         const int64_t top = hole;
         int64_t second = hole;
         while (second < (len - 1) / 2) {
@@ -194,9 +207,9 @@ struct Heap {
         push_hole(hole, top, value);
     }
     uint32_t pop() {
-        const uint32_t ret = a[0];
+        const uint32_t ret = a[0].idx;
         const int64_t last = (int64_t)a.size() - 1;
-        const uint32_t value = a[last];
+        const HeapEnt value = a[last];
         a[last] = a[0];
         adjust(0, last, value);
         a.pop_back();
@@ -204,8 +217,19 @@ struct Heap {
     }
     void update(uint32_t x) {
         const int64_t pos = (*nodes)[x].pq;
+        const float fx = (*nodes)[x].g + (*nodes)[x].h;
+        // the reference reads whatever node sits at the recorded position
+        // (capacity memory included, as the vector keeps it)
+        HeapEnt value = a.data()[pos];
+        if (value.idx == x && pos < (int64_t)a.size()) {
+            value.f = fx;
+            a[pos].f = fx;
+        } else {
+            for (HeapEnt &e : a)
+                if (e.idx == x) e.f = fx;
+            value.f = (*nodes)[value.idx].g + (*nodes)[value.idx].h;
+        }
         const int64_t parent = (pos - 1) / 2;
-        const uint32_t value = a[pos];
         if (pos > 0 && cns(a[parent], value)) {
             int64_t par = (pos - 1) / 2, index = pos;
             while (index > 0 && cns(a[par], value)) {
