@@ -135,6 +135,15 @@ float ora_pdb_value(ora_search *s, int g, ora_varset R);
  * ordering and goal cost, and expansions summed over components.  The
  * netFile text (astar_main.cpp:192-212) is written to net_text if non-NULL
  * (capacity net_cap).  Returns 0, or 1 if some component found no goal. */
+/* One set's store decision under calculateScore (BIC_OLS.cpp:174-276) and
+ * score_calculator.cpp:111-115, against the cache of a finished run as it
+ * stood when the set was scored (SURVEY N4 two-phase order).  Returns 1 if P
+ * is stored; *value = -ts.  Used to check a full-size GPU run set by set. */
+typedef struct ora_cache ora_cache;
+ora_cache *ora_cache_create(const ora_varset *sets, const float *scores, int64_t count);
+void ora_cache_free(ora_cache *c);
+int ora_decide(const ora_dataset *ds, double lambda, int v, ora_varset P, const ora_cache *cache, float *value);
+
 /* MMPC skeleton with Fisher-z tests (ora_mmpc.c; parity unpinned: the
  * reference takes the skeleton from outside, README.md:16).  rows[i] bit j =
  * edge i-j (no diagonal).  max_cond < 0: no cap (24). */

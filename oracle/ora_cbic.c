@@ -350,6 +350,73 @@ static float fbss(vs_t parents, const omap *cache, const int *pv, int m, omap *c
     return best;
 }
 
+/* fbss over a cache of a finished run, seen as it stood when P (|P| = L) was
+ * scored under the two-phase layer order: every stored set of a
+ * smaller layer, plus -- when P lacks variable 0 -- the same layer's sets that
+ * contain variable 0. */
+static int cache_at(const omap *cache, vs_t K, int L, int p_has0, float *val) {
+    uint64_t bits;
+    if (!omap_get(cache, K, &bits)) return 0;
+    const int pc = popc64(K);
+    if (pc > L || (pc == L && (p_has0 || !(K & 1ULL)))) return 0;
+    *val = u2f(bits);
+    return 1;
+}
+
+static float fbss_at(vs_t parents, const omap *cache, int L, int p_has0, const int *pv, int m, omap *checked) {
+    float best = 0.0f;
+    for (int idx = 0; idx < m; idx++) {
+        const int u = pv[idx];
+        const vs_t thin = parents ^ (1ULL << u);
+        if (omap_get(checked, thin, NULL)) continue;
+        float val;
+        if (cache_at(cache, thin, L, p_has0, &val)) {
+            if (val > best) best = val;
+        } else {
+            int npv[64];
+            memset(npv, 0, sizeof(int) * (size_t)(m > 1 ? m - 1 : 1));
+            int j = 0;
+            for (int i = 0; i < m; i++) {
+                if (u == pv[i]) continue;
+                npv[j++] = pv[i];
+                float s = fbss_at(thin, cache, L, p_has0, npv, m - 1, checked);
+                omap_put(checked, thin, 1);
+                if (s > best) best = s;
+            }
+        }
+    }
+    return best;
+}
+
+ora_cache *ora_cache_create(const ora_varset *sets, const float *scores, int64_t count) {
+    omap *m = (omap *)malloc(sizeof(omap));
+    omap_init(m, (size_t)(count > 16 ? count : 16));
+    for (int64_t i = 0; i < count; i++) omap_put(m, sets[i], f2u(scores[i]));
+    return (ora_cache *)m;
+}
+
+void ora_cache_free(ora_cache *c) {
+    omap_free((omap *)c);
+    free(c);
+}
+
+int ora_decide(const ora_dataset *ds, double lambda, int v, ora_varset P, const ora_cache *cache, float *value) {
+    int pv[64] = {0};
+    const int np = parent_vec(ds->n, v, P, pv);
+    ols_ws w = {0};
+    const float the_score = cbic_raw_ws(ds, lambda, v, pv, np, &w);
+    free(w.X); free(w.Y); free(w.tmp);
+    *value = -the_score;
+    if (np == 0) return 1;                       /* cache[empty] = -0.0f */
+    if (the_score >= 0.0f) return -the_score < 0.0f;  /* stored by the caller iff < 0 */
+    omap checked;
+    omap_init(&checked, 64);
+    omap_put(&checked, 0ULL, 1);
+    const float best = fbss_at(P, (const omap *)cache, popc64(P), (int)(P & 1ULL), pv, np, &checked);
+    omap_free(&checked);
+    return !((double)best + 0.0 >= (double)(-the_score));
+}
+
 /* ---- calculateScore (BIC_OLS.cpp:174-276) ------------------------------ */
 static float calculate_score(const ora_dataset *ds, double lambda, int v, vs_t P,
                              omap *cache, omap *checked, ols_ws *w) {

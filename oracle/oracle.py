@@ -69,6 +69,10 @@ def lib():
         L.ora_pdb_value.restype = F
         L.ora_astar.argtypes = [P, P, I, P, P, C.POINTER(F), C.POINTER(I64), C.c_char_p, I64]
         L.ora_mmpc.argtypes = [P, D, I, P]
+        L.ora_cache_create.argtypes = [P, P, I64]
+        L.ora_cache_create.restype = P
+        L.ora_cache_free.argtypes = [P]
+        L.ora_decide.argtypes = [P, D, I, U64, P, C.POINTER(F)]
         L.ora_norm_quantile.argtypes = [D]
         L.ora_norm_quantile.restype = D
         L.ora_partial_z.argtypes = [P, I, D, I, I, P, I]
@@ -113,6 +117,12 @@ class Dataset:
 
     def cbic_raw(self, lam, v, parents):
         return lib().ora_cbic_raw(self.h, float(lam), int(v), int(parents))
+
+    def decide(self, lam, v, P, cache):
+        """ora_decide -> (stored, value) for one set against a cache handle."""
+        val = C.c_float()
+        st = lib().ora_decide(self.h, float(lam), int(v), int(P), cache.h, C.byref(val))
+        return bool(st), val.value
 
     def mmpc(self, alpha=0.05, max_cond=-1):
         """ora_mmpc -> skeleton rows (bit j of row i = edge i-j)."""
@@ -271,6 +281,20 @@ def read_pss(path):
     costs = np.array([p.costs[i] for i in range(tot)], dtype=np.float32)
     L.ora_pss_free(C.byref(p))
     return names, offs, sets, costs
+
+
+class Cache:
+    """ora_cache over one variable's stored (set, score) list."""
+
+    def __init__(self, sets, scores):
+        self._s = np.ascontiguousarray(sets, dtype=np.uint64)
+        self._f = np.ascontiguousarray(scores, dtype=np.float32)
+        self.h = lib().ora_cache_create(_p(self._s), _p(self._f), len(self._s))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().ora_cache_free(self.h)
+            self.h = None
 
 
 def dag_matrix(vpar, n):

@@ -149,3 +149,26 @@ def test_oracle_triplet_api_memoizes_clusters(oracle_built):
     res = o.triplet(o.Search(4, offs, sets, costs), edges=[0xF] * 4)
     assert res["rc"] == 0 and res["distinct"] == 1 and res["runs"] > 1
     assert res["mec"].tolist() == fig_mec(1)
+
+
+def test_single_set_decision_matches_full_runs(oracle_built):
+    """ora_decide (one set against a finished run's cache, seen as it stood
+    under the two-phase layer order) reproduces every store decision and value
+    of the oracle's own sequential runs -- the check the full-size GPU test
+    applies to a C3 run."""
+    from itertools import combinations
+    o = oracle_built
+    n = 10
+    X, _ = synth.gaussian_sem(n, 2000, 9900)
+    ds = o.Dataset(X)
+    for v in (0, 3, 9):
+        sets, scores = ds.score_variable(2.0, v, ((1 << n) - 1) & ~(1 << v), 5)
+        cache = o.Cache(sets, scores)
+        stored = {int(s): np.float32(f) for s, f in zip(sets, scores)}
+        for L in range(6):
+            for comb in combinations([u for u in range(n) if u != v], L):
+                P = sum(1 << u for u in comb)
+                st, val = ds.decide(2.0, v, P, cache)
+                assert st == (P in stored), (v, P)
+                if st:
+                    assert np.float32(val).tobytes() == stored[P].tobytes()
