@@ -169,6 +169,15 @@ int ulg_pdb_query(ulg_ctx *ctx, int64_t count, const uint64_t *S, float *h,
 int ulg_astar(ulg_ctx *ctx, const uint64_t *edges, int pd_count, int mode,
               uint64_t *vpar, int *order, float *goal_cost, int64_t *expanded,
               char *net_text, int64_t net_cap);
+/* astar() with the -p / -s options (astar_main.cpp:590-644, UAI '14): the
+ * heuristic is built over (ancestors, scc); each skeleton component (all
+ * variables without a skeleton) is searched from the root `ancestors` to
+ * ancestors | component.  ulg_astar = ancestors 0, scc all.  Ancestors must
+ * not overlap scc; the GPU mode takes no ancestors. */
+int ulg_astar_scc(ulg_ctx *ctx, const uint64_t *edges, int pd_count, int mode,
+                  uint64_t ancestors, uint64_t scc, uint64_t *vpar, int *order,
+                  float *goal_cost, int64_t *expanded, char *net_text,
+                  int64_t net_cap);
 
 /* triplet_astar's astar() (astar/triplet_astar.cpp:991-1622): for every
  * variable i and pair of its skeleton neighbours, an exact-order A* with

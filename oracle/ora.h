@@ -163,6 +163,9 @@ void ora_dag_score(ora_search *s, int variableCount, int nrows, const ora_varset
 int ora_astar(ora_search *s, const ora_varset *edges, int pd_count,
               ora_varset *vpar, int *order, float *goal_cost,
               int64_t *expanded, char *net_text, int64_t net_cap);
+int ora_astar_scc(ora_search *s, const ora_varset *edges, int pd_count, ora_varset ancestors, ora_varset scc,
+                  ora_varset *vpar, int *order, float *goal_cost,
+                  int64_t *expanded, char *net_text, int64_t net_cap);
 
 /* triplet_astar's astar() (astar/triplet_astar.cpp:991-1622): A* (with
  * closed-node re-opening and a PDB per cluster) on every triple's cluster,

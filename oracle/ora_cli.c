@@ -122,24 +122,56 @@ int main(int argc, char **argv) {
 #endif
 
 #ifdef ORA_ASTAR
+/* setFromCsv (typedefs.h:737-754): comma-separated variable indices */
+static int set_from_csv(const char *csv, ora_varset *vs) {
+    /* boost::split with token_compress_on: runs of ',' are one separator, a
+       leading or trailing ',' leaves an empty token (which fails the check) */
+    const char *p = csv;
+    if (!*p) return 0;
+    for (;;) {
+        const char *q = strchr(p, ',');
+        const size_t len = q ? (size_t)(q - p) : strlen(p);
+        char tok[64];
+        snprintf(tok, sizeof tok, "%.*s", (int)(len < 63 ? len : 63), p);
+        const int var = atoi(tok);
+        if ((var == 0 && tok[0] != '0') || var < 0 || var >= 64) return -1;
+        *vs |= 1ULL << var;
+        if (!q) break;
+        while (*q == ',') q++;
+        p = q;
+    }
+    return 0;
+}
+
 int main(int argc, char **argv) {
-    const char *pss = NULL, *skel = "", *net = "";
+    const char *pss = NULL, *skel = "", *net = "", *anc_arg = "", *scc_arg = "";
     int pd = 2;
     for (int i = 1; i < argc; i++) {
         const char *a = argv[i];
         if (!strcmp(a, "-k") || !strncmp(a, "--skeleton", 10)) skel = opt_val(argc, argv, &i);
         else if (!strcmp(a, "-n") || !strncmp(a, "--netFile", 9)) net = opt_val(argc, argv, &i);
         else if (!strcmp(a, "-a") || !strncmp(a, "--argument", 10)) pd = atoi(opt_val(argc, argv, &i));
+        else if (!strcmp(a, "-p")) anc_arg = opt_val(argc, argv, &i);
+        else if (!strcmp(a, "-s")) scc_arg = opt_val(argc, argv, &i);
         else if (!strcmp(a, "-i") || !strcmp(a, "-f") || !strcmp(a, "-l") || !strcmp(a, "-b") ||
-                 !strcmp(a, "-e") || !strcmp(a, "-r") || !strcmp(a, "-w") || !strcmp(a, "-p") || !strcmp(a, "-s"))
+                 !strcmp(a, "-e") || !strcmp(a, "-r") || !strcmp(a, "-w"))
             (void)opt_val(argc, argv, &i);
         else if (a[0] == '-' && a[1]) fprintf(stderr, "ref_astar: option %s ignored\n", a);
         else if (!pss) pss = a;
     }
-    if (!pss) { fprintf(stderr, "usage: ref_astar in.pss [-k skel] [-n netFile] [-a 2]\n"); return 2; }
+    if (!pss) { fprintf(stderr, "usage: ref_astar in.pss [-k skel] [-n netFile] [-a 2] [-p anc] [-s scc]\n"); return 2; }
     ora_pss p;
     if (ora_pss_read(pss, &p) != 0) { fprintf(stderr, "ref_astar: cannot read %s\n", pss); return 1; }
     const int n = p.n;
+    /* astar_main.cpp:590-598: no -s -> every variable, -p ignored */
+    ora_varset ancestors = 0, scc = (n >= 64) ? ~0ULL : ((1ULL << n) - 1ULL);
+    if (*scc_arg) {
+        scc = 0;
+        if (set_from_csv(scc_arg, &scc) || set_from_csv(anc_arg, &ancestors)) {
+            fprintf(stderr, "ref_astar: Invalid csv string\n");
+            return 1;
+        }
+    }
     ora_search *s = ora_search_create(n, p.offsets, p.sets, p.costs);
     ora_varset edges[64];
     int good = 0;
@@ -150,7 +182,7 @@ int main(int argc, char **argv) {
     int64_t expanded = 0;
     char *text = (char *)malloc(1 << 20);
     double t0 = now_s();
-    int rc = ora_astar(s, good ? edges : NULL, pd, vpar, order, &cost, &expanded, text, 1 << 20);
+    int rc = ora_astar_scc(s, good ? edges : NULL, pd, ancestors, scc, vpar, order, &cost, &expanded, text, 1 << 20);
     double t1 = now_s();
     printf("Found solution: %f\nNodes expanded: %lld\nref_astar: time=%.6fs\n", (double)cost, (long long)expanded, t1 - t0);
     if (rc == 2) fprintf(stderr, "ref_astar: reference heap __down_heap would not terminate\n");

@@ -527,8 +527,18 @@ int ora_astar(ora_search *s, const ora_varset *edges, int pd_count,
               int64_t *expanded, char *net_text, int64_t net_cap) {
     const int n = s->n;
     const vs_t all = (n >= 64) ? ~0ULL : ((1ULL << n) - 1ULL);
-    /* astar(): heuristic over all variables, ancestors empty (:590-611) */
-    if (ora_pdb_build(s, pd_count, 0ULL, all) != 0) return -1;
+    return ora_astar_scc(s, edges, pd_count, 0ULL, all, vpar, order, goal_cost, expanded, net_text, net_cap);
+}
+
+/* astar() with -p / -s (astar_main.cpp:590-644): the heuristic is built over
+ * (ancestors, scc); every skeleton component (all variables without a
+ * skeleton) is searched from the root `ancestors` to ancestors | component. */
+int ora_astar_scc(ora_search *s, const ora_varset *edges, int pd_count, ora_varset ancestors, ora_varset scc,
+                  ora_varset *vpar, int *order, float *goal_cost,
+                  int64_t *expanded, char *net_text, int64_t net_cap) {
+    const int n = s->n;
+    const vs_t all = (n >= 64) ? ~0ULL : ((1ULL << n) - 1ULL);
+    if (ora_pdb_build(s, pd_count, ancestors, scc) != 0) return -1;
     vs_t comps[64];
     int nc;
     int skeleton_good = edges != NULL;
@@ -540,7 +550,7 @@ int ora_astar(ora_search *s, const ora_varset *edges, int pd_count,
     *goal_cost = 0.0f;
     if (net_text && net_cap > 0) net_text[0] = 0;
     for (int c = 0; c < nc; c++) {
-        if (!run_astar_one(s, edges, skeleton_good, 0ULL, comps[c], vpar, order,
+        if (!run_astar_one(s, edges, skeleton_good, ancestors, comps[c], vpar, order,
                            goal_cost, expanded, net_text, net_cap, &hang))
             fail = 1;
     }

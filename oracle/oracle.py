@@ -68,6 +68,7 @@ def lib():
         L.ora_pdb_value.argtypes = [P, I, U64]
         L.ora_pdb_value.restype = F
         L.ora_astar.argtypes = [P, P, I, P, P, C.POINTER(F), C.POINTER(I64), C.c_char_p, I64]
+        L.ora_astar_scc.argtypes = [P, P, I, U64, U64, P, P, C.POINTER(F), C.POINTER(I64), C.c_char_p, I64]
         L.ora_mmpc.argtypes = [P, D, I, P]
         L.ora_cache_create.argtypes = [P, P, I64]
         L.ora_cache_create.restype = P
@@ -212,7 +213,7 @@ class Search:
         k = lib().ora_pdb_groups(self.h, _p(g), 64)
         return [int(x) for x in g[:k]]
 
-    def astar(self, edges=None, pd_count=2):
+    def astar(self, edges=None, pd_count=2, ancestors=None, scc=None):
         n = self.n
         vpar = np.zeros(n, dtype=np.uint64)
         order = np.zeros(n, dtype=np.int32)
@@ -222,8 +223,13 @@ class Search:
         e = None
         if edges is not None:
             e = np.ascontiguousarray(edges, dtype=np.uint64)
-        rc = lib().ora_astar(self.h, _p(e) if e is not None else None, pd_count, _p(vpar), _p(order),
-                             C.byref(cost), C.byref(exp), buf, len(buf))
+        if ancestors is None and scc is None:
+            rc = lib().ora_astar(self.h, _p(e) if e is not None else None, pd_count, _p(vpar), _p(order),
+                                 C.byref(cost), C.byref(exp), buf, len(buf))
+        else:
+            rc = lib().ora_astar_scc(self.h, _p(e) if e is not None else None, pd_count, int(ancestors or 0),
+                                     int(scc) if scc is not None else (1 << n) - 1, _p(vpar), _p(order),
+                                     C.byref(cost), C.byref(exp), buf, len(buf))
         return {"rc": rc, "vpar": vpar, "order": order, "cost": cost.value, "expanded": exp.value,
                 "net_text": buf.value.decode()}
 

@@ -80,6 +80,37 @@ def test_cli_end_to_end_matches_oracle_and_golden(tmp_path, oracle_built, fig, l
             assert net.read_text() == ref_net.read_text()
 
 
+@pytest.mark.parametrize("bad", ["1,x", ",1", "1,", "a"])
+def test_astar_invalid_csv_fails_before_gpu(tmp_path, oracle_built, bad):
+    """setFromCsv (typedefs.h:737-754) rejects a token atoi reads as 0 that
+    does not start with '0'; both command lines refuse it before any search."""
+    o = oracle_built
+    pss = tmp_path / "x.pss"
+    o.write_pss(str(pss), ["a", "b", "c"], [1, 1, 1], [0, 1, 2, 3], [0, 0, 0], [0.0, 0.0, 0.0])
+    r = _run([ASTAR, str(pss), "-s", bad, "-p", "0"])
+    assert r.returncode == 1 and "Invalid csv string" in r.stderr
+    r = _run([o.REF_ASTAR, str(pss), "-s", "1,2", "-p", bad])
+    assert r.returncode == 1 and "Invalid csv string" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fig", [1, 2])
+@pytest.mark.parametrize("ps", [("0", "1,2,3"), ("", "0,,2"), ("2", "0,1")])
+def test_astar_cli_ancestors_scc_matches_oracle(tmp_path, oracle_built, fig, ps):
+    o = oracle_built
+    csv = os.path.join(GOLDEN, FIG_CSV[fig])
+    pss = tmp_path / "gpu.pss"
+    r = _run([SCORE, csv, str(pss), "-f", "cBIC", "--lambda", "1"])
+    assert r.returncode == 0, r.stderr
+    net, ref_net = tmp_path / "net", tmp_path / "ref_net"
+    r = _run([ASTAR, str(pss), "-n", str(net), "-p", ps[0], "-s", ps[1]])
+    assert r.returncode == 0, r.stderr
+    subprocess.run([o.REF_ASTAR, str(pss), "-n", str(ref_net), "-p", ps[0], "-s", ps[1]], check=True,
+                   stdout=subprocess.DEVNULL)
+    assert net.read_text() == ref_net.read_text()
+    assert read_matrix(str(net) + ".csv") == read_matrix(str(ref_net) + ".csv")
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("fig", [1, 2])
 @pytest.mark.parametrize("lam", ["0.5", "1", "2"])

@@ -212,3 +212,43 @@ def test_c2_end_to_end_bit_exact(ulg_ctx, oracle_built):
     assert res["expanded"] == ref["expanded"]
     gres = ulg_ctx.astar(edges=full, mode=1)
     assert abs(gres["cost"] - ref["cost"]) <= 1e-6 * abs(ref["cost"])
+
+
+@pytest.mark.parametrize("anc,scc", [(0b111, 0b111111111000), (0, 0b111111000000), (0b1, 0b110),
+                                     (0b11110000, 0b1111)])
+@pytest.mark.parametrize("sparse", [False, True])
+def test_exact_astar_ancestors_and_scc(ulg_ctx, oracle_built, anc, scc, sparse):
+    """astar -p/-s (astar_main.cpp:590-598,607): the pattern database over
+    (ancestors, scc) and the per-component search started from the ancestors
+    reproduce the oracle's DAG, cost, expansions and netFile text."""
+    import ulg
+    o = oracle_built
+    n = 12
+    X, W = synth.gaussian_sem(n, 3000, 9330)
+    full = [(1 << n) - 1] * n
+    rows = synth.true_skeleton_edges(W) if sparse else full
+    cands = ulg.candidates_from_edges(rows, n) if sparse else None
+    offs, sets, scores, costs = _oracle_pipeline(o, X, 2.0, 3, cands)
+    ulg_ctx.search_load(offs, sets, costs)
+    res = ulg_ctx.astar(edges=rows, mode=0, ancestors=anc, scc=scc)
+    ref = o.Search(n, offs, sets, costs).astar(edges=rows, ancestors=anc, scc=scc)
+    assert ref["rc"] == 0
+    assert [int(x) for x in res["vpar"]] == [int(x) for x in ref["vpar"]]
+    assert np.float32(res["cost"]).tobytes() == np.float32(ref["cost"]).tobytes()
+    assert res["expanded"] == ref["expanded"]
+    assert res["net_text"] == ref["net_text"]
+    # back to the whole lattice on the same context: the PDB is rebuilt
+    res2 = ulg_ctx.astar(edges=rows, mode=0)
+    ref2 = o.Search(n, offs, sets, costs).astar(edges=rows)
+    assert [int(x) for x in res2["vpar"]] == [int(x) for x in ref2["vpar"]]
+    assert res2["expanded"] == ref2["expanded"]
+
+
+def test_gpu_mode_rejects_ancestors(ulg_ctx, oracle_built):
+    o = oracle_built
+    n = 8
+    X, _ = synth.gaussian_sem(n, 1000, 9331)
+    offs, sets, scores, costs = _oracle_pipeline(o, X, 2.0, 2)
+    ulg_ctx.search_load(offs, sets, costs)
+    with pytest.raises(RuntimeError):
+        ulg_ctx.astar(edges=[(1 << n) - 1] * n, mode=1, ancestors=0b1, scc=0b110)

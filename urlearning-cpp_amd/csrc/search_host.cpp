@@ -298,20 +298,33 @@ int ulg_pdb_query(ulg_ctx *c, int64_t count, const uint64_t *S, float *h, int *c
 
 int ulg_astar(ulg_ctx *c, const uint64_t *edges, int pd_count, int mode, uint64_t *vpar, int *order,
               float *goal_cost, int64_t *expanded, char *net_text, int64_t net_cap) {
+    if (!c) return ULG_ERR_ARG;
+    const int n = c->search ? c->search->n : 0;
+    return ulg_astar_scc(c, edges, pd_count, mode, 0, all_vars(n), vpar, order, goal_cost, expanded, net_text,
+                         net_cap);
+}
+
+int ulg_astar_scc(ulg_ctx *c, const uint64_t *edges, int pd_count, int mode, uint64_t ancestors, uint64_t scc,
+                  uint64_t *vpar, int *order, float *goal_cost, int64_t *expanded, char *net_text,
+                  int64_t net_cap) {
     if (!c || !vpar || !order || !goal_cost || !expanded) return ULG_ERR_ARG;
     if (!c->search || !c->search->lists_ready) return set_err(c, ULG_ERR_STATE, "ulg_astar: no parent-set lists");
     ULG_HIP(c, hipSetDevice(c->device));
     SearchState &s = *c->search;
     const int n = s.n;
     const uint64_t all = all_vars(n);
+    if ((ancestors | scc) & ~all) return set_err(c, ULG_ERR_ARG, "ulg_astar: ancestors / scc outside the variables");
     int rc;
-    if (mode == ULG_ASTAR_GPU && (rc = search_ensure_scope(c, all))) return rc;  // the whole lattice
-    // astar(): the heuristic covers all variables, no ancestors (astar_main.cpp:590-611)
-    if (!s.pdb_ready || s.pd_count != pd_count || s.scc != all || s.ancestors != 0) {
-        rc = search_ensure_scope(c, all);
+    if (mode == ULG_ASTAR_GPU) {
+        if (ancestors) return set_err(c, ULG_ERR_UNSUPPORTED, "ulg_astar(GPU): ancestors need the exact-order search");
+        if ((rc = search_ensure_scope(c, all))) return rc;  // the whole lattice
+    }
+    // astar(): the heuristic is built over (ancestors, scc) (astar_main.cpp:590-611)
+    if (!s.pdb_ready || s.pd_count != pd_count || s.scc != scc || s.ancestors != ancestors) {
+        rc = search_ensure_scope(c, ancestors | scc);
         if (rc == ULG_ERR_UNSUPPORTED) c->err.clear();  // the PDB build scans the lists
         else if (rc) return rc;
-        if ((rc = search_build_pdb(c, pd_count, 0, all))) return rc;
+        if ((rc = search_build_pdb(c, pd_count, ancestors, scc))) return rc;
     }
     *expanded = 0;
     *goal_cost = 0.0f;
@@ -326,12 +339,12 @@ int ulg_astar(ulg_ctx *c, const uint64_t *edges, int pd_count, int mode, uint64_
     bool hang = false;
     bool fail = false;
     for (uint64_t comp : comps) {
-        // every lookup of this component's search lies inside the component
-        if ((rc = search_ensure_scope(c, comp)) || (rc = search_cost_table_host(c))) return rc;
+        // every lookup of this component's search lies inside ancestors | component
+        if ((rc = search_ensure_scope(c, ancestors | comp)) || (rc = search_cost_table_host(c))) return rc;
         HostTables T;
         host_tables(s, T);
         ExactResult r;
-        if ((rc = astar_one(c, T, edges, good, 0, comp, expanded, &hang, r))) return rc;
+        if ((rc = astar_one(c, T, edges, good, ancestors, comp, expanded, &hang, r))) return rc;
         if (!r.found) { fail = true; continue; }
         // each component rewrites netFile and netFile.csv (astar_main.cpp:470,519)
         for (int v = 0; v < n; ++v) vpar[v] = 0;

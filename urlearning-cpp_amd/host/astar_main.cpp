@@ -31,8 +31,8 @@ int main(int argc, char **argv) {
             {"b", "bestScore", true, "list", "BestScore calculator: list, bitwise or tree"},
             {"e", "heuristic", true, "static", "Heuristic type: static"},
             {"a", "argument", true, "2", "Number of static pattern databases"},
-            {"p", "pc_{i-1}", true, "", "Ancestor-only variables (unsupported)"},
-            {"s", "scc_i", true, "", "Variables to add in the search (unsupported)"},
+            {"p", "pc_{i-1}", true, "", "Variables which can only be used as ancestors (CSV of indices; with -s)"},
+            {"s", "scc_i", true, "", "Variables which will be added in the search (CSV of indices; blank: all)"},
             {"r", "runningTime", true, "0", "Maximum running time (not applied)"},
             {"n", "netFile", true, "", "The file to which the learned network is written."},
             {"", "mode", true, "exact", "exact (reference pop order) or gpu (GPU order-graph search)"},
@@ -58,10 +58,6 @@ int main(int argc, char **argv) {
         std::fprintf(stderr, "astar: only the static pattern database heuristic is on this path\n");
         return 2;
     }
-    if (!args.get("pc_{i-1}").empty() || !args.get("scc_i").empty()) {
-        std::fprintf(stderr, "astar: -p/-s (ancestor / scc subsets) are not supported on this path\n");
-        return 2;
-    }
     const std::string mode = args.get("mode");
     if (mode != "exact" && mode != "gpu") {
         std::fprintf(stderr, "astar: --mode must be exact or gpu\n");
@@ -78,6 +74,16 @@ int main(int argc, char **argv) {
     if (n < 1) {
         std::fprintf(stderr, "astar: no variables in '%s'\n", args.get("scoreFile").c_str());
         return 1;
+    }
+    // astar_main.cpp:590-598: no -s means every variable (and -p is ignored)
+    uint64_t ancestors = 0, scc = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+    if (!args.get("scc_i").empty()) {
+        scc = 0;
+        if (!ulgcli::set_from_csv(args.get("scc_i"), scc) || !ulgcli::set_from_csv(args.get("pc_{i-1}"), ancestors)) {
+            std::fprintf(stderr, "astar: Invalid csv string: '%s' / '%s'\n", args.get("scc_i").c_str(),
+                         args.get("pc_{i-1}").c_str());
+            return 1;
+        }
     }
     std::vector<uint64_t> rows;
     bool good = false;
@@ -103,8 +109,9 @@ int main(int argc, char **argv) {
     int64_t expanded = 0;
     std::vector<char> text(1 << 20);
     if (rc == ULG_OK)
-        rc = ulg_astar(ctx, good ? rows.data() : nullptr, pd, mode == "gpu" ? ULG_ASTAR_GPU : ULG_ASTAR_EXACT, vpar.data(),
-                       order.data(), &cost, &expanded, text.data(), (int64_t)text.size());
+        rc = ulg_astar_scc(ctx, good ? rows.data() : nullptr, pd, mode == "gpu" ? ULG_ASTAR_GPU : ULG_ASTAR_EXACT,
+                           ancestors, scc, vpar.data(), order.data(), &cost, &expanded, text.data(),
+                           (int64_t)text.size());
     const double t3 = ulgcli::now_s();
     if (rc != ULG_OK) {
         std::fprintf(stderr, "astar: %s\n", ulg_last_error(ctx));

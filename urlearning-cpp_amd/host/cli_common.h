@@ -5,6 +5,7 @@
 
 #include <chrono>
 #include <cstdio>
+#include <cstdint>
 #include <cstdlib>
 #include <map>
 #include <set>
@@ -102,6 +103,25 @@ private:
     std::map<std::string, std::string> vals_;
     std::set<std::string> seen_;
 };
+
+// setFromCsv (typedefs.h:737-754): comma-separated variable indices, split
+// with adjacent separators compressed; a token that atoi reads as 0 without
+// starting with '0' (an empty leading/trailing token included) is an error.
+inline bool set_from_csv(const std::string &csv, uint64_t &vs) {
+    if (csv.empty()) return true;
+    size_t i = 0;
+    while (true) {
+        size_t j = csv.find(',', i);
+        const std::string tok = csv.substr(i, j == std::string::npos ? std::string::npos : j - i);
+        const int var = std::atoi(tok.c_str());
+        if ((var == 0 && (tok.empty() || tok[0] != '0')) || var < 0 || var >= 64) return false;
+        vs |= 1ull << var;
+        if (j == std::string::npos) break;
+        while (j < csv.size() && csv[j] == ',') ++j;
+        i = j;
+    }
+    return true;
+}
 
 inline double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();

@@ -52,6 +52,8 @@ def lib():
         L.ulg_mmpc.argtypes = [P, D, I, P]
         L.ulg_pss_format.argtypes = [P, C.c_char_p, P, P, C.POINTER(C.c_void_p), C.POINTER(I64)]
         L.ulg_pss_format_lists.argtypes = [P, I, P, P, P, C.c_char_p, P, P, C.POINTER(C.c_void_p), C.POINTER(I64)]
+        L.ulg_astar_scc.argtypes = [P, P, I, I, C.c_uint64, C.c_uint64, P, P, C.POINTER(F), C.POINTER(I64),
+                                    C.c_char_p, I64]
         L.ulg_set_option.argtypes = [P, C.c_char_p, I64]
         L.ulg_profile_enable.argtypes = [P, I]
         L.ulg_profile_get.argtypes = [P, C.c_char_p, C.POINTER(D), C.POINTER(I64), C.POINTER(D)]
@@ -192,7 +194,7 @@ class Context:
         self._check(lib().ulg_pdb_query(self._h, len(s), _ptr(s), _ptr(h), _ptr(comp)), "ulg_pdb_query")
         return h, comp
 
-    def astar(self, edges=None, pd_count=2, mode=0, net_text=True):
+    def astar(self, edges=None, pd_count=2, mode=0, net_text=True, ancestors=None, scc=None):
         n = self.search_n
         vpar = np.zeros(n, dtype=np.uint64)
         order = np.zeros(n, dtype=np.int32)
@@ -202,9 +204,16 @@ class Context:
         e = None
         if edges is not None:
             e = np.ascontiguousarray([int(x) for x in edges], dtype=np.uint64)
-        self._check(lib().ulg_astar(self._h, _ptr(e) if e is not None else None, int(pd_count), int(mode),
-                                    _ptr(vpar), _ptr(order), C.byref(cost), C.byref(exp), buf,
-                                    len(buf) if buf is not None else 0), "ulg_astar")
+        if ancestors is None and scc is None:
+            self._check(lib().ulg_astar(self._h, _ptr(e) if e is not None else None, int(pd_count), int(mode),
+                                        _ptr(vpar), _ptr(order), C.byref(cost), C.byref(exp), buf,
+                                        len(buf) if buf is not None else 0), "ulg_astar")
+        else:
+            anc = int(ancestors or 0)
+            sc = int(scc) if scc is not None else (1 << n) - 1
+            self._check(lib().ulg_astar_scc(self._h, _ptr(e) if e is not None else None, int(pd_count), int(mode),
+                                            anc, sc, _ptr(vpar), _ptr(order), C.byref(cost), C.byref(exp), buf,
+                                            len(buf) if buf is not None else 0), "ulg_astar_scc")
         return {"vpar": vpar, "order": order, "cost": cost.value, "expanded": exp.value,
                 "net_text": buf.value.decode() if buf is not None else None}
 
