@@ -80,7 +80,7 @@ def cpu_baseline(cfg, X, target_s=15.0):
 PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1", "pmc_traffic.json")
 
 
-def pmc_traffic(cfg, sets):
+def pmc_traffic(cfg, sets, label):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3
     PMC passes of the same config (scripts/pmc_round.sh + pmc_summarize.py);
     None if there is no summary for this config and launch size."""
@@ -88,28 +88,37 @@ def pmc_traffic(cfg, sets):
         t = json.load(open(PMC_TRAFFIC))
     except (OSError, ValueError):
         return None, None
-    if t.get("config_id") != cfg["id"] or int(t.get("sets_per_launch", -1)) != int(sets):
+    if (t.get("config_id") != cfg["id"] or int(t.get("sets_per_launch", -1)) != int(sets)
+            or t.get("label") != label):
         return None, None
     return t["traffic_bytes_per_launch"], "profiles/r1/pmc_traffic.json"
 
 
 def roofline(ctx, cfg, per_launch_sets):
-    """Dominant kernel = the layer-k 'rest' launch (sets without variable 0)."""
+    """Dominant unit = the layer-k 'rest' launch (sets without variable 0): the
+    scoring kernel plus, with the two-pass scorer (score_variant bit 4), the
+    walk kernel over the sets it queued -- both are one layer's decision, so
+    their average durations are summed (rocprof lists them separately)."""
     k = cfg["k"]
-    name = f"score_layer_{k}_rest"
-    p = ctx.profile_get(name)
-    if p is None:
+    names = [f"score_layer_{k}_rest", f"walk_{k}_rest"]
+    ps = [ctx.profile_get(nm) for nm in names]
+    if ps[0] is None:
         return None, None
+    if ps[1] is None:
+        names, ps = names[:1], ps[:1]
+    name = " + ".join(names)
+    p = {"avg_ms": sum(q["avg_ms"] for q in ps), "count": ps[0]["count"]}
     sets = per_launch_sets
     # SURVEY 8d: compulsory HBM bytes per scored set = 4 (k direct-subset score reads) + 4 (score write)
     bytes_per_set = 4 * (k + 1)
     achieved = sets * bytes_per_set / (p["avg_ms"] * 1e-3) / 1e9
     flops_per_set = 2 * k ** 3 / 3 + 2 * k * k + 2 * k
-    traffic, traffic_src = pmc_traffic(cfg, sets)
+    traffic, traffic_src = pmc_traffic(cfg, sets, name)
     return ({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per launch",
              "traffic_source": traffic_src, "kernel": name,
-             "avg_launch_ms": p["avg_ms"], "launches": p["count"], "sets_per_launch": sets,
+             "avg_launch_ms": p["avg_ms"], "avg_launch_ms_each": [q["avg_ms"] for q in ps],
+             "launches": p["count"], "sets_per_launch": sets,
              "bytes_per_set": bytes_per_set,
              "fp64_flops_per_set": flops_per_set,
              "fp64_tflops": sets * flops_per_set / (p["avg_ms"] * 1e-3) / 1e12}, p)

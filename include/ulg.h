@@ -195,9 +195,14 @@ int ulg_triplet_astar(ulg_ctx *ctx, const uint64_t *edges, int pd_count,
                       int *directed_graph, int64_t *stats);
 
 /* ---- tuning knobs -------------------------------------------------------
- * "score_variant" (0..7, default 1): bit 0 = fully unrolled presence gather
- * in the scorer (layers <= 6), bit 1 = stack-machine dominance recursion,
- * bit 2 = decision-only walk (stops at the first visited key >= -ts).
+ * "score_variant" (0..7, 13, 16, 17; default 17): bit 0 = fully unrolled
+ * presence gather in the scorer (layers <= 6), bit 1 = stack-machine
+ * dominance recursion, bit 2 = decision-only walk (stops at the first
+ * visited key >= -ts), bit 4 = two-pass layers: the scoring kernel settles
+ * every set it can without a walk and queues the rest for a dense walk
+ * kernel with the hi-cover prune (overrides bits 1-2).  13 = bit 2 plus
+ * per-launch decision statistics on stderr (and, with ULG_DUMP_DIR set, the
+ * walking lanes' presence words); diagnostics only, it synchronises.
  * "table_budget_kb" (KiB; default 0 = half the free HBM): memory for the dense
  * best-score tables (16 B per entry incl. the host cost copy).  Lists whose
  * tables over all variables exceed it (e.g. n = 32 with a full skeleton) are

@@ -18,10 +18,12 @@ for rnd in range(5):
         ctx.profile(True); ctx.profile_reset()
         t = time.perf_counter(); st, sc = ctx.score(list(range(n)), full, k); dt = time.perf_counter() - t
         prof = ctx.profile_dump(); ctx.profile(False)
-        res[v].append({"ms": dt * 1e3, f"L{k}rest_ms": prof.get(f"score_layer_{k}_rest", {}).get("total_ms")})
+        res[v].append({"ms": dt * 1e3, f"L{k}rest_ms": prof.get(f"score_layer_{k}_rest", {}).get("total_ms"),
+                       "prof": {kk: round(vv.get("total_ms", 0), 4) for kk, vv in prof.items() if vv.get("total_ms", 0) > 0.05}})
         out = ctx.fetch(st)
         h = (out[1].tobytes(), out[2].tobytes())
         if ref is None: ref = h
         assert h == ref, f"variant {v} differs"
 print(json.dumps({v: {"median_ms": float(np.median([r["ms"] for r in res[v]])),
-                      "median_layer_ms": float(np.median([r[f"L{k}rest_ms"] for r in res[v]]))} for v in variants}))
+                      "median_layer_ms": float(np.median([r[f"L{k}rest_ms"] for r in res[v]])),
+                      "last_profile": res[v][-1]["prof"]} for v in variants}, indent=1))

@@ -4,8 +4,11 @@
 reports half the bytes of wide coalesced reads, so it is doubled; WRITE_SIZE
 is taken as is.  Both are in KiB per dispatch.
 
-  python scripts/pmc_summarize.py <fetch_pass.csv> <write_pass.csv> <kernel substring> \
-      <config_id> <sets_per_launch> <out.json>
+  python scripts/pmc_summarize.py <fetch_pass.csv> <write_pass.csv> <kernel substrings, ";"-separated> \
+      <config_id> <sets_per_launch> <out.json> [label]
+
+With several kernels (the scoring kernel and the walk kernel of one layer),
+the per-dispatch averages are summed: one layer launch = one dispatch of each.
 """
 import csv
 import json
@@ -21,15 +24,21 @@ def per_dispatch(path, counter, kernel):
 
 
 def main():
-    fetch_csv, write_csv, kernel, config_id, sets, out = sys.argv[1:7]
-    f = per_dispatch(fetch_csv, "FETCH_SIZE", kernel)
-    w = per_dispatch(write_csv, "WRITE_SIZE", kernel)
-    if not f or not w:
-        sys.exit(f"no {kernel} dispatches with FETCH_SIZE/WRITE_SIZE in {fetch_csv} / {write_csv}")
-    fetch_kib = sum(f) / len(f)
-    write_kib = sum(w) / len(w)
+    fetch_csv, write_csv, kernels, config_id, sets, out = sys.argv[1:7]
+    label = sys.argv[7] if len(sys.argv) > 7 else kernels
+    fetch_kib = write_kib = 0.0
+    disp = []
+    for kernel in kernels.split(";"):
+        f = per_dispatch(fetch_csv, "FETCH_SIZE", kernel)
+        w = per_dispatch(write_csv, "WRITE_SIZE", kernel)
+        if not f or not w:
+            sys.exit(f"no {kernel} dispatches with FETCH_SIZE/WRITE_SIZE in {fetch_csv} / {write_csv}")
+        fetch_kib += sum(f) / len(f)
+        write_kib += sum(w) / len(w)
+        disp.append([len(f), len(w)])
     traffic = 2.0 * fetch_kib * 1024.0 + write_kib * 1024.0
-    res = {"kernel": kernel, "config_id": config_id, "sets_per_launch": int(sets), "dispatches": [len(f), len(w)],
+    res = {"kernel": kernels, "label": label, "config_id": config_id, "sets_per_launch": int(sets),
+           "dispatches": disp,
            "fetch_kib_avg": fetch_kib, "write_kib_avg": write_kib, "traffic_bytes_per_launch": traffic,
            "correction": "2 x FETCH_SIZE (gfx950 reports half of wide reads) + WRITE_SIZE",
            "sources": [fetch_csv, write_csv]}

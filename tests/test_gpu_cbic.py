@@ -139,7 +139,7 @@ def test_rescoring_is_deterministic(ulg_ctx):
         assert x.tobytes() == y.tobytes()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 16, 17])
 def test_scorer_variants_identical(ulg_ctx, oracle_built, variant):
     """Every scorer variant (presence gather x recursion form x decision-only
     walk) stores exactly the oracle's sets (k=6 exercises the unrolled
@@ -156,4 +156,4 @@ def test_scorer_variants_identical(ulg_ctx, oracle_built, variant):
             o = _oracle_lists(oracle_built, X, 2.0, variables, cands, k)
             _compare_lists(*o, *g, variables, ctx=f"variant {variant} k={k}")
     finally:
-        ulg_ctx.set_option("score_variant", 1)
+        ulg_ctx.set_option("score_variant", 17)

@@ -20,6 +20,7 @@
 //   * every (variable, layer) owns a dense float slab indexed by the colex
 //     rank of the set inside the variable's candidate list (= the Gosper
 //     enumeration index), holding the stored score or an absent sentinel.
+#include <cstdio>
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -250,9 +251,11 @@ __device__ __forceinline__ void best_subset(uint32_t T, uint32_t pv, const BS &p
 // the reference's redundant re-tests (2.2x fewer union points per wave in a
 // host simulation) measured 5.6 ms: heavier control flow, occupancy 2.
 template <int M, class BS>
-__device__ __forceinline__ bool dominated(uint32_t T, uint32_t pv, const BS &present, const BS &hi, BS &checked) {
+__device__ __forceinline__ bool dominated(uint32_t T, uint32_t pv, const BS &present, const BS &hi, BS &checked,
+                                          uint32_t &steps) {
 #pragma nounroll
     for (int idx = 0; idx < M; ++idx) {
+        ++steps;
         const uint32_t u = (pv >> (4 * idx)) & 15u;
         const uint32_t T2 = T ^ (1u << u);
         if (checked.test(T2)) continue;
@@ -269,12 +272,70 @@ __device__ __forceinline__ bool dominated(uint32_t T, uint32_t pv, const BS &pre
                 if (pi == u) continue;
                 npv |= pi << (4 * j);
                 ++j;
-                if (dominated<M - 1, BS>(T2, npv, present, hi, checked)) return true;
+                if (dominated<M - 1, BS>(T2, npv, present, hi, checked, steps)) return true;
                 checked.set(T2);
             }
         }
     }
     return false;
+}
+
+// dominated() with the hi-cover prune: an absent node T2 is expanded only if
+// some key >= -ts lies in U(T2) = subsets of T2 u {var 0} (`cover`, tested at
+// T2 without var 0).  Skipping an expansion changes `checked` only inside
+// U(T2); a later test that sees the difference expands a node of U(T2), whose
+// own expansion again stays inside U(T2) -- so every difference stays within
+// keys none of which is >= -ts, and the first such key the walk visits, if
+// any, is the same.  (The queued lanes of C3 layer 6 walk 13 steps instead of
+// 220 when stored, 113 instead of 194 when pruned.)
+template <int M, class BS>
+__device__ __forceinline__ bool dominated_cov(uint32_t T, uint32_t pv, const BS &present, const BS &hi,
+                                              const BS &cover, BS &checked) {
+#pragma nounroll
+    for (int idx = 0; idx < M; ++idx) {
+        const uint32_t u = (pv >> (4 * idx)) & 15u;
+        const uint32_t T2 = T ^ (1u << u);
+        if (checked.test(T2)) continue;
+        if (present.test(T2)) {
+            if (hi.test(T2)) return true;
+            continue;
+        }
+        if constexpr (M > 1) {
+            if (!cover.test(T2 & ~1u)) continue;
+            uint32_t npv = 0;
+            int j = 0;
+#pragma nounroll
+            for (int i = 0; i < M; ++i) {
+                const uint32_t pi = (pv >> (4 * i)) & 15u;
+                if (pi == u) continue;
+                npv |= pi << (4 * j);
+                ++j;
+                if (dominated_cov<M - 1, BS>(T2, npv, present, hi, cover, checked)) return true;
+                checked.set(T2);
+            }
+        }
+    }
+    return false;
+}
+
+// cover = { T : some key of hi, without var 0, is a subset of T }: drop bit 0
+// of every key, then close upwards over bits 1 .. q-1 (in-word shifts for
+// bits 1..5, word ORs for the bits that index words).
+template <int W>
+__device__ __forceinline__ void cover_words(uint64_t *w) {
+    constexpr uint64_t kM[6] = {0xAAAAAAAAAAAAAAAAull, 0xCCCCCCCCCCCCCCCCull, 0xF0F0F0F0F0F0F0F0ull,
+                                0xFF00FF00FF00FF00ull, 0xFFFF0000FFFF0000ull, 0xFFFFFFFF00000000ull};
+#pragma unroll
+    for (int j = 0; j < W; ++j) w[j] |= (w[j] & kM[0]) >> 1;
+#pragma unroll
+    for (int b = 1; b < 6; ++b)
+#pragma unroll
+        for (int j = 0; j < W; ++j) w[j] |= (w[j] & ~kM[b]) << (1 << b);
+#pragma unroll
+    for (int c = 1; c < W; c <<= 1)
+#pragma unroll
+        for (int j = 0; j < W; ++j)
+            if (j & c) w[j] |= w[j ^ c];
 }
 
 // Same recursion as an explicit stack machine: one loop iteration advances
@@ -390,6 +451,11 @@ struct ScoreArgs {
     const uint64_t *tbl_off; // [nv*S + 1] start of (vi, layer) slab
     const uint64_t *work;    // [nv + 1] prefix of this launch's sets
     float *table;
+    unsigned long long *stats;  // variant bit 3: per-launch decision statistics
+    uint64_t *dump;             // variant bit 3: presence words of the walking lanes
+    uint64_t dump_cap;
+    uint64_t *queue;            // variant bit 4: lanes left for walk_kernel
+    unsigned long long *qcount;
     double N;
     double lambda;
     int n, nv, S;
@@ -520,6 +586,9 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
     const float ts = (float)the_score;
 
     float out;
+    bool queued = false;  // variant bit 4: left for walk_kernel
+    int cat = 1;          // variant bit 3 statistics: 1 ts >= 0, 2 no key >= -ts,
+    uint32_t steps = 0;   // 3 direct child >= -ts, 4 walk -> dominated, 5 walk -> stored
     if (ts >= 0.0f) {
         // returned -ts; the caller stores it iff it is < 0 (score_calculator.cpp:111)
         const float s = -ts;
@@ -552,7 +621,7 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         BS present = make_bits<BS>(lds_bits);
         BS hi = make_bits<BS>(lds_bits + (size_t)W * kBlock);
         present.clear();
-        if constexpr ((V & 4) != 0) hi.clear();
+        if constexpr ((V & 20) != 0) hi.clear();
         const float thr = -ts;
         if constexpr (L <= 6 && (V & 1)) {
             presence_unrolled<L, PHASE, (PHASE == 0 ? L : L + 1), W>(present, hi, thr, binom, cpack, z, a.table,
@@ -583,10 +652,16 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         uint32_t pvtop = 0;
 #pragma unroll
         for (int i = 0; i < L; ++i) pvtop |= (uint32_t)(i + (v0inP ? 0 : 1)) << (4 * i);
-        if constexpr ((V & 4) != 0) {
-            // decision-only walk: no key >= -ts at all -> stored; a direct
-            // child >= -ts (always visited at the top level) -> not stored;
-            // otherwise walk until the first visited key >= -ts
+        if constexpr ((V & 16) != 0) {
+            // Decide what needs no walk; queue the rest for walk_kernel.
+            //  * no present key >= -ts: nothing the walk visits can prune P;
+            //  * a present direct child >= -ts: always visited at the top;
+            //  * (P without var 0) a present P\{a,b} or P\{a}+{0} >= -ts
+            //    with P\{a} absent: P\{a} is first reached at the top
+            //    level (nothing below P\{a'} contains a' != 0 again), so it
+            //    is expanded with the full list, and its j = L-1 call tests
+            //    every P\{a,b}, its j = 1 call (L >= 3) the toggle of var 0.
+            //    Present keys never enter `checked`, so those are visited.
             bool any = false;
 #pragma unroll
             for (int wj = 0; wj < W; ++wj) any |= hi.word(wj) != 0ull;
@@ -594,11 +669,67 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
             if (any) {
 #pragma unroll
                 for (int i = 0; i < L; ++i) dom |= hi.test(Plocal ^ (1u << ((pvtop >> (4 * i)) & 15u)));
+                if constexpr (PHASE == 1) {
+                    constexpr uint32_t P1 = ((1u << L) - 1u) << 1;
+#pragma unroll
+                    for (int ea = 1; ea <= L; ++ea) {
+                        const uint32_t Ta = P1 ^ (1u << ea);
+                        bool d2 = false;
+#pragma unroll
+                        for (int eb = 1; eb <= L; ++eb)
+                            if (eb != ea) d2 |= hi.test(Ta ^ (1u << eb));
+                        if constexpr (L >= 3) d2 |= hi.test(Ta | 1u);
+                        dom |= d2 && !present.test(Ta);
+                    }
+                }
+                queued = !dom;
+            }
+            if (queued) {
+                // wave-aggregated append: one atomic per wave
+                const unsigned long long act = __ballot(1);
+                const int lane = threadIdx.x & 63;
+                const int leader = __ffsll((long long)act) - 1;
+                unsigned long long base = 0;
+                if (lane == leader) base = atomicAdd(a.qcount, (unsigned long long)__popcll(act));
+                base = __shfl(base, leader);
+                const uint64_t pos = base + (uint64_t)__popcll(act & ((1ull << lane) - 1ull));
+                uint64_t *e = a.queue + pos * (uint64_t)(2 + 2 * W);
+                e[0] = toff[(uint64_t)vi * a.S + L] + rankP;
+                e[1] = (uint64_t)fbits(ts);
+#pragma unroll
+                for (int wj = 0; wj < W; ++wj) e[2 + wj] = present.word(wj);
+#pragma unroll
+                for (int wj = 0; wj < W; ++wj) e[2 + W + wj] = hi.word(wj);
+            }
+            out = dom ? absent_f() : -ts;
+        } else if constexpr ((V & 4) != 0) {
+            // decision-only walk: no key >= -ts at all -> stored; a direct
+            // child >= -ts (always visited at the top level) -> not stored;
+            // otherwise walk until the first visited key >= -ts
+            bool any = false;
+#pragma unroll
+            for (int wj = 0; wj < W; ++wj) any |= hi.word(wj) != 0ull;
+            bool dom = false;
+            cat = 2;
+            if (any) {
+                cat = 3;
+#pragma unroll
+                for (int i = 0; i < L; ++i) dom |= hi.test(Plocal ^ (1u << ((pvtop >> (4 * i)) & 15u)));
                 if (!dom) {
                     BS checked = make_bits<BS>(lds_bits + (size_t)2 * W * kBlock);
                     checked.clear();
                     checked.set(0u);
-                    dom = dominated<L, BS>(Plocal, pvtop, present, hi, checked);
+                    dom = dominated<L, BS>(Plocal, pvtop, present, hi, checked, steps);
+                    cat = dom ? 4 : 5;
+                    if constexpr ((V & 8) != 0) {
+                        const uint64_t di = atomicAdd(&a.stats[9], 1ull);
+                        if (di < a.dump_cap) {
+                            for (int wj = 0; wj < W; ++wj) a.dump[di * (2 * W + 1) + wj] = present.word(wj);
+                            for (int wj = 0; wj < W; ++wj) a.dump[di * (2 * W + 1) + W + wj] = hi.word(wj);
+                            a.dump[di * (2 * W + 1) + 2 * W] = (uint64_t)dom | ((uint64_t)v0inP << 1) |
+                                                               ((uint64_t)steps << 8);
+                        }
+                    }
                 }
             }
             out = dom ? absent_f() : -ts;
@@ -635,7 +766,75 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         out = ((double)best + 0.0 >= (double)(-ts)) ? absent_f() : -ts;
         }
     }
-    a.table[toff[(uint64_t)vi * a.S + L] + rankP] = out;
+    if (!queued) a.table[toff[(uint64_t)vi * a.S + L] + rankP] = out;
+    if constexpr ((V & 8) != 0) {
+        // per wave: lanes per category, waves with any walking lane, walk
+        // steps summed over lanes and the wave's max (what the wave pays)
+        const int lane = threadIdx.x & 63;
+        uint32_t mx = steps;
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+        uint32_t sum = steps;
+        for (int o = 32; o > 0; o >>= 1) sum += (uint32_t)__shfl_xor((int)sum, o);
+        const unsigned long long walkers = __ballot(cat >= 4);
+        for (int k = 1; k <= 5; ++k) {
+            const unsigned long long b = __ballot(cat == k);
+            if (lane == 0 && b) atomicAdd(&a.stats[k], (unsigned long long)__popcll(b));
+        }
+        if (lane == 0) {
+            atomicAdd(&a.stats[0], 1ull);
+            if (walkers) atomicAdd(&a.stats[6], 1ull);
+            atomicAdd(&a.stats[7], (unsigned long long)sum);
+            atomicAdd(&a.stats[8], (unsigned long long)mx);
+        }
+    }
+}
+
+// Second half of a queued layer (variant bit 4): one lane per parent set the
+// score kernel could not decide, packed densely so a wave's lanes all walk.
+// Entry: table slot | ts bits | W presence words | W `hi` words.
+template <int L, int PHASE>
+__global__ void __launch_bounds__(kBlock) walk_kernel(const uint64_t *queue, const unsigned long long *qcount,
+                                                      float *table) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int W = bits_words(L);
+    using BS = std::conditional_t<(W >= 4), BitsLds<W>, Bits<W>>;
+    const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (gid >= *qcount) return;
+    const uint64_t *e = queue + gid * (uint64_t)(2 + 2 * W);
+    uint64_t *lds_bits = reinterpret_cast<uint64_t *>(smem) + threadIdx.x;
+    BS present = make_bits<BS>(lds_bits);
+    BS hi = make_bits<BS>(lds_bits + (size_t)W * kBlock);
+    BS checked = make_bits<BS>(lds_bits + (size_t)2 * W * kBlock);
+    BS cover = make_bits<BS>(lds_bits + (size_t)3 * W * kBlock);
+    uint64_t cw[W];
+#pragma unroll
+    for (int wj = 0; wj < W; ++wj) cw[wj] = e[2 + W + wj];
+    cover_words<W>(cw);
+    if constexpr (W >= 4) {
+#pragma unroll
+        for (int wj = 0; wj < W; ++wj) {
+            lds_bits[wj * kBlock] = e[2 + wj];
+            lds_bits[(W + wj) * kBlock] = e[2 + W + wj];
+            lds_bits[(3 * W + wj) * kBlock] = cw[wj];
+        }
+    } else {
+#pragma unroll
+        for (int wj = 0; wj < W; ++wj) {
+            present.w[wj] = e[2 + wj];
+            hi.w[wj] = e[2 + W + wj];
+            cover.w[wj] = cw[wj];
+        }
+    }
+    const float ts = __uint_as_float((uint32_t)e[1]);
+    constexpr bool v0inP = PHASE == 0;
+    constexpr uint32_t Plocal = v0inP ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
+    uint32_t pvtop = 0;
+#pragma unroll
+    for (int i = 0; i < L; ++i) pvtop |= (uint32_t)(i + (v0inP ? 0 : 1)) << (4 * i);
+    checked.clear();
+    checked.set(0u);
+    const bool dom = dominated_cov<L, BS>(Plocal, pvtop, present, hi, cover, checked);
+    table[e[0]] = dom ? absent_f() : -ts;
 }
 
 __global__ void empty_set_kernel(const uint64_t *tbl_off, int nv, int S, float *table) {
@@ -783,9 +982,36 @@ KernelFn pick(int phase, int variant) {
         case 3: return pick_phase<L, 3>(phase);
         case 4: case 6: return pick_phase<L, 4>(phase);
         case 5: case 7: return pick_phase<L, 5>(phase);
+        case 13: return pick_phase<L, 13>(phase);
+        case 16: return pick_phase<L, 16>(phase);
+        case 17: return pick_phase<L, 17>(phase);
         default: return nullptr;
     }
 }
+using WalkFn = void (*)(const uint64_t *, const unsigned long long *, float *);
+template <int L>
+WalkFn walk_pick(int phase) {
+    return phase == 0 ? walk_kernel<L, 0> : walk_kernel<L, 1>;
+}
+WalkFn walk_fn(int L, int phase) {
+    switch (L) {
+        case 1: return walk_pick<1>(phase);
+        case 2: return walk_pick<2>(phase);
+        case 3: return walk_pick<3>(phase);
+        case 4: return walk_pick<4>(phase);
+        case 5: return walk_pick<5>(phase);
+        case 6: return walk_pick<6>(phase);
+        case 7: return walk_pick<7>(phase);
+        case 8: return walk_pick<8>(phase);
+        default: return nullptr;
+    }
+}
+const char *kWalkNames[2][kMaxL + 1] = {
+    {"", "walk_1_var0", "walk_2_var0", "walk_3_var0", "walk_4_var0", "walk_5_var0", "walk_6_var0", "walk_7_var0",
+     "walk_8_var0"},
+    {"", "walk_1_rest", "walk_2_rest", "walk_3_rest", "walk_4_rest", "walk_5_rest", "walk_6_rest", "walk_7_rest",
+     "walk_8_rest"}};
+
 KernelFn layer_kernel(int L, int phase, int variant) {
     switch (L) {
         case 1: return pick<1>(phase, variant);
@@ -944,11 +1170,28 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     sa.meta = c->d_meta.p;
     sa.tbl_off = c->d_tbl_off.p;
     sa.table = c->table.p;
+    sa.stats = nullptr;
+    sa.dump = nullptr;
+    sa.dump_cap = 0;
+    sa.queue = nullptr;
+    sa.qcount = nullptr;
     sa.N = (double)c->N;
     sa.lambda = c->lambda;
     sa.n = n;
     sa.nv = nv;
     sa.S = S;
+    if (c->score_variant & 16) {
+        // queue sized for the largest launch: every lane may be left undecided
+        uint64_t qwords = 0;
+        for (int L = 1; L <= kmax; ++L)
+            for (int ph = 0; ph < 2; ++ph)
+                qwords = std::max<uint64_t>(qwords, work[((size_t)L * 2 + ph) * (nv + 1) + nv] *
+                                                        (uint64_t)(2 + 2 * bits_words(L)));
+        if ((rc = ensure(c, c->d_queue, (size_t)qwords)) || (rc = ensure(c, c->d_qcount, (size_t)2 * (kmax + 1))))
+            return rc;
+        ULG_HIP(c, hipMemsetAsync(c->d_qcount.p, 0, sizeof(unsigned long long) * 2 * (kmax + 1), c->stream));
+        sa.queue = c->d_queue.p;
+    }
     for (int L = 1; L <= kmax; ++L)
         for (int ph = 0; ph < 2; ++ph) {
             const uint64_t *w = &work[((size_t)L * 2 + ph) * (nv + 1)];
@@ -962,8 +1205,50 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
             const KernelFn kfn = layer_kernel(L, ph, c->score_variant);
             if (lay.total > 64 * 1024)
                 ULG_HIP(c, hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, lay.total));
+            if (c->score_variant & 8) {
+                if ((rc = ensure(c, c->d_stats, 16))) return rc;
+                ULG_HIP(c, hipMemsetAsync(c->d_stats.p, 0, 16 * 8, c->stream));
+                sa.stats = c->d_stats.p;
+                sa.dump_cap = 4u << 20;
+                if ((rc = ensure(c, c->d_dump, (size_t)sa.dump_cap * (2 * bits_words(L) + 1)))) return rc;
+                sa.dump = c->d_dump.p;
+            }
+            if (c->score_variant & 16) sa.qcount = c->d_qcount.p + (L * 2 + ph);
             hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(kBlock), (size_t)lay.total, c->stream, sa);
             prof_end(c);
+            if (c->score_variant & 16) {
+                // the undecided lanes of this launch, densely packed
+                const WalkFn wfn = walk_fn(L, ph);
+                const int W = bits_words(L);
+                const size_t wl = W >= 4 ? (size_t)4 * W * kBlock * 8 : 0;
+                if (wl > 64 * 1024)
+                    ULG_HIP(c, hipFuncSetAttribute((const void *)wfn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   (int)wl));
+                prof_begin(c, kWalkNames[ph][L]);
+                hipLaunchKernelGGL(wfn, dim3((unsigned)blocks), dim3(kBlock), wl, c->stream, c->d_queue.p,
+                                   c->d_qcount.p + (L * 2 + ph), c->table.p);
+                prof_end(c);
+            }
+            if (c->score_variant & 8) {
+                unsigned long long st[16];
+                ULG_HIP(c, hipMemcpyAsync(st, c->d_stats.p, sizeof st, hipMemcpyDeviceToHost, c->stream));
+                ULG_HIP(c, hipStreamSynchronize(c->stream));
+                std::fprintf(stderr,
+                             "score_stats L=%d phase=%d waves=%llu lanes: ts>=0 %llu, no-hi %llu, direct-hi %llu, "
+                             "walk-dom %llu, walk-stored %llu; walking waves %llu; steps lane-sum %llu wave-max-sum %llu\n",
+                             L, ph, st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8]);
+                if (const char *dd = std::getenv("ULG_DUMP_DIR")) {
+                    const uint64_t cntd = std::min<uint64_t>(st[9], sa.dump_cap);
+                    std::vector<uint64_t> hd((size_t)cntd * (2 * bits_words(L) + 1));
+                    ULG_HIP(c, hipMemcpy(hd.data(), c->d_dump.p, hd.size() * 8, hipMemcpyDeviceToHost));
+                    char fn[512];
+                    std::snprintf(fn, sizeof fn, "%s/walk_L%d_p%d.bin", dd, L, ph);
+                    if (FILE *f = std::fopen(fn, "wb")) {
+                        std::fwrite(hd.data(), 8, hd.size(), f);
+                        std::fclose(f);
+                    }
+                }
+            }
         }
     ULG_HIP(c, hipGetLastError());
 

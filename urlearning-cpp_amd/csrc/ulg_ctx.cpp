@@ -100,7 +100,7 @@ void ulg_destroy(ulg_ctx *c) {
     prof_collect(c);
     release(c->raw); release(c->z); release(c->gram); release(c->partials); release(c->colstat);
     release(c->table); release(c->d_tbl_off); release(c->d_work); release(c->d_blk);
-    release(c->d_cand); release(c->d_meta); release(c->d_binom);
+    release(c->d_cand); release(c->d_meta); release(c->d_binom); release(c->d_stats); release(c->d_dump); release(c->d_queue); release(c->d_qcount);
     release(c->out_sets); release(c->out_scores); release(c->out_offsets);
     release(c->qbuf_in); release(c->qbuf_out);
     pss_release(c);
@@ -118,7 +118,8 @@ const char *ulg_last_error(const ulg_ctx *c) { return c ? c->err.c_str() : "null
 int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
     if (!c || !name) return ULG_ERR_ARG;
     if (std::strcmp(name, "score_variant") == 0) {
-        if (value < 0 || value > 7) return set_err(c, ULG_ERR_ARG, "score_variant must be 0..7");
+        if (value < 0 || (value > 7 && value != 13 && value != 16 && value != 17))
+            return set_err(c, ULG_ERR_ARG, "score_variant must be 0..7, 13, 16 or 17");
         c->score_variant = (int)value;
         return ULG_OK;
     }

@@ -57,13 +57,17 @@ struct ulg_ctx {
     int64_t total_stored = 0;
     int64_t total_scored = 0;
     bool scored = false;
-    int score_variant = 1;
+    int score_variant = 17;
     uint64_t table_budget_kb = 0;  // best-score table budget in KiB (0 = half the free HBM)  // see ScoreArgs::variant (ulg_set_option "score_variant")
     ulg::DevBuf<float> table;
     ulg::DevBuf<uint64_t> d_tbl_off, d_work, d_blk;
     ulg::DevBuf<uint8_t> d_cand;  // [nv][64] compact index -> variable
     ulg::DevBuf<int> d_meta;      // [nv][4]: var, m, var0in, pad
     ulg::DevBuf<uint32_t> d_binom;
+    ulg::DevBuf<unsigned long long> d_stats;  // score_variant 13 statistics
+    ulg::DevBuf<uint64_t> d_dump;
+    ulg::DevBuf<uint64_t> d_queue;                // score_variant bit 4: undecided lanes
+    ulg::DevBuf<unsigned long long> d_qcount;
     ulg::DevBuf<uint64_t> out_sets;
     ulg::DevBuf<float> out_scores;
     ulg::DevBuf<int64_t> out_offsets;
