@@ -1151,14 +1151,13 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
             w[nv] = s;
         }
     int rc;
-    if ((rc = ensure(c, c->table, total_slots)) || (rc = ensure(c, c->d_tbl_off, toff.size())) ||
-        (rc = ensure(c, c->d_work, work.size())) || (rc = ensure(c, c->d_cand, cand.size())) ||
-        (rc = ensure(c, c->d_meta, meta.size())))
+    // the output lists are sized for every slot, so the compaction needs no
+    // mid-call sync for the stored count
+    if ((rc = ensure(c, c->table, total_slots)) || (rc = upload(c, c->d_tbl_off, c->mir_tbl_off, toff)) ||
+        (rc = upload(c, c->d_work, c->mir_work, work)) || (rc = upload(c, c->d_cand, c->mir_cand, cand)) ||
+        (rc = upload(c, c->d_meta, c->mir_meta, meta)) || (rc = ensure(c, c->out_sets, total_slots)) ||
+        (rc = ensure(c, c->out_scores, total_slots)) || (rc = ensure(c, c->out_offsets, (size_t)nv + 1)))
         return rc;
-    ULG_HIP(c, hipMemcpyAsync(c->d_tbl_off.p, toff.data(), toff.size() * 8, hipMemcpyHostToDevice, c->stream));
-    ULG_HIP(c, hipMemcpyAsync(c->d_work.p, work.data(), work.size() * 8, hipMemcpyHostToDevice, c->stream));
-    ULG_HIP(c, hipMemcpyAsync(c->d_cand.p, cand.data(), cand.size(), hipMemcpyHostToDevice, c->stream));
-    ULG_HIP(c, hipMemcpyAsync(c->d_meta.p, meta.data(), meta.size() * 4, hipMemcpyHostToDevice, c->stream));
 
     prof_begin(c, "empty_set");
     empty_set_kernel<<<(nv + 63) / 64, 64, 0, c->stream>>>(c->d_tbl_off.p, nv, S, c->table.p);
@@ -1261,12 +1260,6 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     prof_begin(c, "scan_stored");
     scan_kernel<<<1, 1024, 0, c->stream>>>(c->d_blk.p, nb);
     prof_end(c);
-    uint64_t stored = 0;
-    ULG_HIP(c, hipMemcpyAsync(&stored, c->d_blk.p + nb, 8, hipMemcpyDeviceToHost, c->stream));
-    ULG_HIP(c, hipStreamSynchronize(c->stream));
-    if ((rc = ensure(c, c->out_sets, stored)) || (rc = ensure(c, c->out_scores, stored)) ||
-        (rc = ensure(c, c->out_offsets, (size_t)nv + 1)))
-        return rc;
     WriteArgs wa;
     wa.table = c->table.p;
     wa.blk = c->d_blk.p;
@@ -1285,6 +1278,8 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     prof_end(c);
     set_total_kernel<<<1, 1, 0, c->stream>>>(c->d_blk.p, nb, nv, c->out_offsets.p);
     ULG_HIP(c, hipGetLastError());
+    uint64_t stored = 0;
+    ULG_HIP(c, hipMemcpyAsync(&stored, c->d_blk.p + nb, 8, hipMemcpyDeviceToHost, c->stream));
     ULG_HIP(c, hipStreamSynchronize(c->stream));
     prof_collect(c);
 

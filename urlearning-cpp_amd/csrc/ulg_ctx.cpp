@@ -36,8 +36,16 @@ void prof_begin(ulg_ctx *c, const char *name) {
     if (!c->prof) return;
     ProfRec r;
     r.name = name;
-    (void)hipEventCreate(&r.start);
-    (void)hipEventCreate(&r.stop);
+    // events come from a per-context pool: creating two per kernel costs more
+    // than the small layers' kernels themselves
+    for (hipEvent_t *e : {&r.start, &r.stop}) {
+        if (!c->event_pool.empty()) {
+            *e = c->event_pool.back();
+            c->event_pool.pop_back();
+        } else {
+            (void)hipEventCreate(e);
+        }
+    }
     (void)hipEventRecord(r.start, c->stream);
     c->pending.push_back(r);
 }
@@ -52,8 +60,8 @@ void prof_collect(ulg_ctx *c) {
         float ms = 0.f;
         if (hipEventSynchronize(r.stop) == hipSuccess && hipEventElapsedTime(&ms, r.start, r.stop) == hipSuccess)
             c->prof_ms[r.name].push_back(ms);
-        (void)hipEventDestroy(r.start);
-        (void)hipEventDestroy(r.stop);
+        c->event_pool.push_back(r.start);
+        c->event_pool.push_back(r.stop);
     }
     c->pending.clear();
 }
@@ -98,6 +106,8 @@ void ulg_destroy(ulg_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     prof_collect(c);
+    for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
+    c->event_pool.clear();
     release(c->raw); release(c->z); release(c->gram); release(c->partials); release(c->colstat);
     release(c->table); release(c->d_tbl_off); release(c->d_work); release(c->d_blk);
     release(c->d_cand); release(c->d_meta); release(c->d_binom); release(c->d_stats); release(c->d_dump); release(c->d_queue); release(c->d_qcount);

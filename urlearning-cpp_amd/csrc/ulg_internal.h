@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <map>
 #include <string>
+#include <cstring>
 #include <vector>
 
 #include "../../include/ulg.h"
@@ -30,6 +31,13 @@ struct PssState;
 struct ProfRec {
     std::string name;
     hipEvent_t start, stop;
+};
+
+// Host copy of what was last uploaded into a device buffer: repeated calls
+// with the same layout metadata skip the pageable H2D copies.
+struct Mirror {
+    const void *dev = nullptr;
+    std::vector<unsigned char> bytes;
 };
 
 }  // namespace ulg
@@ -83,6 +91,8 @@ struct ulg_ctx {
     // ---- profiling ----
     bool prof = false;
     std::vector<ulg::ProfRec> pending;
+    std::vector<hipEvent_t> event_pool;
+    ulg::Mirror mir_tbl_off, mir_work, mir_cand, mir_meta;
     std::map<std::string, std::vector<double>> prof_ms;
 };
 
@@ -110,6 +120,19 @@ int ensure(ulg_ctx *c, DevBuf<T> &b, size_t elems) {
     if (e != hipSuccess)
         return set_err(c, ULG_ERR_HIP, std::string("hipMalloc failed: ") + hipGetErrorString(e));
     b.cap = elems;
+    return ULG_OK;
+}
+
+template <typename T>
+int upload(ulg_ctx *c, DevBuf<T> &b, Mirror &m, const std::vector<T> &h) {
+    const size_t nbytes = h.size() * sizeof(T);
+    if (int rc = ensure(c, b, h.size())) return rc;
+    if (m.dev == b.p && m.bytes.size() == nbytes && std::memcmp(m.bytes.data(), h.data(), nbytes) == 0) return ULG_OK;
+    hipError_t e = hipMemcpyAsync(b.p, h.data(), nbytes, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return set_err(c, ULG_ERR_HIP, std::string("hipMemcpyAsync failed: ") + hipGetErrorString(e));
+    m.dev = b.p;
+    m.bytes.assign(reinterpret_cast<const unsigned char *>(h.data()),
+                   reinterpret_cast<const unsigned char *>(h.data()) + nbytes);
     return ULG_OK;
 }
 
