@@ -221,6 +221,10 @@ int ulg_profile_get(ulg_ctx *ctx, const char *name, double *avg_ms,
 /* Writes a newline-separated "name count total_ms" listing into buf. */
 int ulg_profile_dump(ulg_ctx *ctx, char *buf, int64_t cap);
 int ulg_profile_reset(ulg_ctx *ctx);
+/* Time only the kernels named in the comma-separated list (NULL or "" = all):
+ * each timed kernel costs two event records on the host, which the small
+ * launches of a scoring call notice. */
+int ulg_profile_select(ulg_ctx *ctx, const char *names);
 
 #ifdef __cplusplus
 }

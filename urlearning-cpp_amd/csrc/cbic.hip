@@ -185,6 +185,11 @@ struct Bits {
 #pragma unroll
         for (int j = 0; j < W; ++j) w[j] |= ((int)(i >> 6) == j) ? bit : 0ull;
     }
+    __device__ __forceinline__ void reset(uint32_t i) {
+        const uint64_t bit = 1ull << (i & 63);
+#pragma unroll
+        for (int j = 0; j < W; ++j) w[j] &= ((int)(i >> 6) == j) ? ~bit : ~0ull;
+    }
     __device__ __forceinline__ uint64_t word(int j) const { return w[j]; }
 };
 
@@ -203,6 +208,7 @@ struct BitsLds {
     }
     __device__ __forceinline__ bool test(uint32_t i) const { return (base[(i >> 6) * kBlock] >> (i & 63)) & 1ull; }
     __device__ __forceinline__ void set(uint32_t i) { base[(i >> 6) * kBlock] |= 1ull << (i & 63); }
+    __device__ __forceinline__ void reset(uint32_t i) { base[(i >> 6) * kBlock] &= ~(1ull << (i & 63)); }
     __device__ __forceinline__ uint64_t word(int j) const { return base[j * kBlock]; }
 };
 
@@ -312,6 +318,37 @@ __device__ __forceinline__ bool dominated_cov(uint32_t T, uint32_t pv, const BS 
                 ++j;
                 if (dominated_cov<M - 1, BS>(T2, npv, present, hi, cover, checked)) return true;
                 checked.set(T2);
+            }
+        }
+    }
+    return false;
+}
+
+// dominated_cov() with its three per-node tests folded into one: `open` =
+// absent & hi-cover & not yet checked, so a tested node is a hit (hi), an
+// expansion (open) or nothing; clearing its open bit after the first call
+// returns is the reference's checked.insert (present nodes never enter
+// `checked`, so testing hi before `checked` changes nothing).
+template <int M, class BS, bool DIAG = false>
+__device__ __forceinline__ bool walk_open(uint32_t T, uint32_t pv, const BS &hi, BS &open, uint32_t &steps) {
+#pragma nounroll
+    for (int idx = 0; idx < M; ++idx) {
+        if constexpr (DIAG) ++steps;
+        const uint32_t u = (pv >> (4 * idx)) & 15u;
+        const uint32_t T2 = T ^ (1u << u);
+        if (hi.test(T2)) return true;
+        if constexpr (M > 1) {
+            if (!open.test(T2)) continue;
+            uint32_t npv = 0;
+            int j = 0;
+#pragma nounroll
+            for (int i = 0; i < M; ++i) {
+                const uint32_t pi = (pv >> (4 * i)) & 15u;
+                if (pi == u) continue;
+                npv |= pi << (4 * j);
+                ++j;
+                if (walk_open<M - 1, BS, DIAG>(T2, npv, hi, open, steps)) return true;
+                open.reset(T2);
             }
         }
     }
@@ -681,6 +718,46 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
                         if constexpr (L >= 3) d2 |= hi.test(Ta | 1u);
                         dom |= d2 && !present.test(Ta);
                     }
+                    // One level further: X = P\{a,b} (a < b), absent, is first
+                    // tested below P\{a} if that is absent (in its j = b-1
+                    // call), else below P\{b} if absent (in its j = a call),
+                    // else never.  Its expansion list holds the entries before
+                    // the removed one: {1..b-1}\{a} in the first case, {1..a-1}
+                    // in the second, plus zeros (the var-0 toggle, L >= 4).
+                    if constexpr (L >= 3) {
+#pragma unroll
+                        for (int ea = 1; ea <= L; ++ea)
+#pragma unroll
+                            for (int eb = ea + 1; eb <= L; ++eb) {
+                                const uint32_t X = P1 ^ (1u << ea) ^ (1u << eb);
+                                bool h1 = false, h2 = false;
+#pragma unroll
+                                for (int ec = 1; ec < eb; ++ec) {
+                                    if (ec == ea) continue;
+                                    const bool hc = hi.test(X ^ (1u << ec));
+                                    h1 |= hc;
+                                    if (ec < ea) h2 |= hc;
+                                }
+                                if constexpr (L >= 4) {
+                                    const bool ht = hi.test(X | 1u);
+                                    h1 |= ht;
+                                    h2 |= ht;
+                                }
+                                const bool pa = present.test(P1 ^ (1u << ea));
+                                const bool pb = present.test(P1 ^ (1u << eb));
+                                const bool hx = pa ? (!pb && h2) : h1;
+                                dom |= hx && !present.test(X);
+                            }
+                    }
+                } else {
+                    // P\{0} is the very first node tested; if absent it is
+                    // expanded with every list (1..j) + zeros, so each present
+                    // P\{0,c} is visited.
+                    constexpr uint32_t P0 = (1u << L) - 1u;
+                    bool d2 = false;
+#pragma unroll
+                    for (int ec = 1; ec < L; ++ec) d2 |= hi.test(P0 ^ 1u ^ (1u << ec));
+                    dom |= d2 && !present.test(P0 ^ 1u);
                 }
                 queued = !dom;
             }
@@ -693,13 +770,23 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
                 if (lane == leader) base = atomicAdd(a.qcount, (unsigned long long)__popcll(act));
                 base = __shfl(base, leader);
                 const uint64_t pos = base + (uint64_t)__popcll(act & ((1ull << lane) - 1ull));
-                uint64_t *e = a.queue + pos * (uint64_t)(2 + 2 * W);
-                e[0] = toff[(uint64_t)vi * a.S + L] + rankP;
-                e[1] = (uint64_t)fbits(ts);
+                // open = absent & cover(T without var 0) & not checked
+                // (checked = {empty})
+                uint64_t ow[W];
 #pragma unroll
-                for (int wj = 0; wj < W; ++wj) e[2 + wj] = present.word(wj);
+                for (int wj = 0; wj < W; ++wj) ow[wj] = hi.word(wj);
+                cover_words<W>(ow);
 #pragma unroll
-                for (int wj = 0; wj < W; ++wj) e[2 + W + wj] = hi.word(wj);
+                for (int wj = 0; wj < W; ++wj) {
+                    const uint64_t ce = ow[wj] & 0x5555555555555555ull;
+                    ow[wj] = (ce | (ce << 1)) & ~present.word(wj) & (wj == 0 ? ~1ull : ~0ull);
+                }
+                uint64_t *e = a.queue + pos * (uint64_t)(1 + 2 * W);
+                e[0] = (toff[(uint64_t)vi * a.S + L] + rankP) | ((uint64_t)fbits(ts) << 32);
+#pragma unroll
+                for (int wj = 0; wj < W; ++wj) e[1 + wj] = hi.word(wj);
+#pragma unroll
+                for (int wj = 0; wj < W; ++wj) e[1 + W + wj] = ow[wj];
             }
             out = dom ? absent_f() : -ts;
         } else if constexpr ((V & 4) != 0) {
@@ -791,50 +878,207 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
 
 // Second half of a queued layer (variant bit 4): one lane per parent set the
 // score kernel could not decide, packed densely so a wave's lanes all walk.
-// Entry: table slot | ts bits | W presence words | W `hi` words.
+// Entry: table slot (low 32 bits) | ts bits (high 32) , W presence words, W
+// `hi` words.
 template <int L, int PHASE>
 __global__ void __launch_bounds__(kBlock) walk_kernel(const uint64_t *queue, const unsigned long long *qcount,
-                                                      float *table) {
+                                                      float *table, uint64_t *wclock) {
+    const uint64_t t_start = wclock ? wall_clock64() : 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int W = bits_words(L);
     using BS = std::conditional_t<(W >= 4), BitsLds<W>, Bits<W>>;
     const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (gid >= *qcount) return;
-    const uint64_t *e = queue + gid * (uint64_t)(2 + 2 * W);
+    const uint64_t q = gid;
+    const uint64_t *e = queue + q * (uint64_t)(1 + 2 * W);
     uint64_t *lds_bits = reinterpret_cast<uint64_t *>(smem) + threadIdx.x;
-    BS present = make_bits<BS>(lds_bits);
-    BS hi = make_bits<BS>(lds_bits + (size_t)W * kBlock);
-    BS checked = make_bits<BS>(lds_bits + (size_t)2 * W * kBlock);
-    BS cover = make_bits<BS>(lds_bits + (size_t)3 * W * kBlock);
-    uint64_t cw[W];
-#pragma unroll
-    for (int wj = 0; wj < W; ++wj) cw[wj] = e[2 + W + wj];
-    cover_words<W>(cw);
+    BS hi = make_bits<BS>(lds_bits);
+    BS open = make_bits<BS>(lds_bits + (size_t)W * kBlock);
     if constexpr (W >= 4) {
 #pragma unroll
         for (int wj = 0; wj < W; ++wj) {
-            lds_bits[wj * kBlock] = e[2 + wj];
-            lds_bits[(W + wj) * kBlock] = e[2 + W + wj];
-            lds_bits[(3 * W + wj) * kBlock] = cw[wj];
+            lds_bits[wj * kBlock] = e[1 + wj];
+            lds_bits[(W + wj) * kBlock] = e[1 + W + wj];
         }
     } else {
 #pragma unroll
         for (int wj = 0; wj < W; ++wj) {
-            present.w[wj] = e[2 + wj];
-            hi.w[wj] = e[2 + W + wj];
-            cover.w[wj] = cw[wj];
+            hi.w[wj] = e[1 + wj];
+            open.w[wj] = e[1 + W + wj];
         }
     }
-    const float ts = __uint_as_float((uint32_t)e[1]);
+    const float ts = __uint_as_float((uint32_t)(e[0] >> 32));
     constexpr bool v0inP = PHASE == 0;
     constexpr uint32_t Plocal = v0inP ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
     uint32_t pvtop = 0;
 #pragma unroll
     for (int i = 0; i < L; ++i) pvtop |= (uint32_t)(i + (v0inP ? 0 : 1)) << (4 * i);
-    checked.clear();
-    checked.set(0u);
-    const bool dom = dominated_cov<L, BS>(Plocal, pvtop, present, hi, cover, checked);
-    table[e[0]] = dom ? absent_f() : -ts;
+    uint32_t steps = 0;
+    bool dom;
+    if (wclock) dom = walk_open<L, BS, true>(Plocal, pvtop, hi, open, steps);
+    else dom = walk_open<L, BS>(Plocal, pvtop, hi, open, steps);
+    table[(uint32_t)e[0]] = dom ? absent_f() : -ts;
+    if (wclock) {
+        // per lane: steps | dom << 31 | open count << 32 (at the queue index)
+        int pc = 0;
+#pragma unroll
+        for (int wj = 0; wj < W; ++wj) pc += __popcll(e[1 + W + wj]);
+        wclock[2 * ((uint64_t)gridDim.x * kBlock / 64 + 1) + q] =
+            (uint64_t)steps | ((uint64_t)dom << 31) | ((uint64_t)pc << 32);
+        // diagnostics (ULG_WALK_CLOCK): per wave start / end wall clock
+        const uint64_t t_end = wall_clock64();
+        const uint64_t w = gid >> 6;
+        if ((threadIdx.x & 63) == 0) {
+            wclock[2 * w] = t_start;
+        }
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0) wclock[2 * w + 1] = t_end;
+    }
+}
+
+// ---- bit-sliced walk (score_variant bit 5) ----------------------------------
+// The walk's tree (T, pv, idx, i) never depends on the data: only which
+// subtrees a set enters does.  So one wave walks the union tree ONCE for 64*K
+// sets with scalar control flow, and every per-set test becomes a K-bit mask
+// operation: lane l holds sets l*K .. l*K+K-1, and for every local subset t
+// the K bits "set k has t in hi / open" sit in K-bit fields of register
+// vectors indexed by the (uniform) t.  The union of K*64 walks grows slowly
+// with the set count (host model over the dumped C3 patterns: 706 points for
+// 64 sets, 1076 for 512), so the work per set drops by an order of
+// magnitude against one set per lane.  Same decisions: each set still takes
+// exactly its own walk's steps, in its order; sets never interact.
+template <int L, int K_>
+struct Sliced {
+    static constexpr int Q = L + 1;                   // local bits (phase 0 uses L)
+    static constexpr int K = K_;                      // sets per lane
+    static constexpr int E = 32 / K;                  // subsets per register
+    static constexpr int NV0 = (1 << Q) / E;
+    static constexpr int NV = NV0 < 2 ? 2 : NV0;      // registers per bitset vector
+    static constexpr uint32_t KM = (1u << K) - 1u;
+    typedef uint32_t Vec __attribute__((ext_vector_type(NV)));
+};
+
+template <int L, int K>
+__device__ __forceinline__ uint32_t sl_get(const typename Sliced<L, K>::Vec &v, uint32_t t) {
+    using S = Sliced<L, K>;
+    return (v[t / S::E] >> (S::K * (t % S::E))) & S::KM;
+}
+template <int L, int K>
+__device__ __forceinline__ void sl_clear(typename Sliced<L, K>::Vec &v, uint32_t t, uint32_t m) {
+    using S = Sliced<L, K>;
+    v[t / S::E] &= ~(m << (S::K * (t % S::E)));
+}
+__device__ __forceinline__ bool wave_any(uint32_t x) { return __ballot(x != 0u) != 0ull; }
+
+template <int L, int K, int M, bool DIAG = false>
+__device__ __forceinline__ void walk_sliced(uint32_t T, uint32_t pv, uint32_t act, const typename Sliced<L, K>::Vec &hiV,
+                                            typename Sliced<L, K>::Vec &openV, uint32_t &alive, uint32_t &dom,
+                                            uint32_t &pts) {
+#pragma nounroll
+    for (int idx = 0; idx < M; ++idx) {
+        act &= alive;
+        if (!wave_any(act)) return;
+        if constexpr (DIAG) ++pts;
+        const uint32_t u = (pv >> (4 * idx)) & 15u;
+        const uint32_t T2 = T ^ (1u << u);
+        // a hit ends that set's walk (the reference returns up the recursion)
+        const uint32_t h = sl_get<L, K>(hiV, T2) & act;
+        dom |= h;
+        alive &= ~h;
+        act &= ~h;
+        if constexpr (M > 1) {
+            uint32_t x = sl_get<L, K>(openV, T2) & act;
+            if (!wave_any(x)) continue;
+            uint32_t npv = 0;
+            int j = 0;
+#pragma nounroll
+            for (int i = 0; i < M; ++i) {
+                const uint32_t pi = (pv >> (4 * i)) & 15u;
+                if (pi == u) continue;
+                npv |= pi << (4 * j);
+                ++j;
+                walk_sliced<L, K, M - 1, DIAG>(T2, npv, x, hiV, openV, alive, dom, pts);
+                sl_clear<L, K>(openV, T2, x);  // checked.insert(T2) for the sets that ran the call
+                x &= alive;
+                if (!wave_any(x)) break;
+            }
+        }
+    }
+}
+
+// one wave (64 threads) per 64*K queued sets; entries as walk_kernel's
+template <int L, int PHASE, int K>
+__global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, const unsigned long long *qcount,
+                                                         float *table, uint64_t *wclock) {
+    using S = Sliced<L, K>;
+    const uint64_t t_start = wclock ? wall_clock64() : 0;
+    constexpr int W = bits_words(L);
+    const uint64_t qn = *qcount;
+    const uint64_t first = (uint64_t)blockIdx.x * 64 * S::K;
+    if (first >= qn) return;
+    const uint64_t mine = first + (uint64_t)threadIdx.x * S::K;
+    typename S::Vec hiV, openV;
+#pragma unroll
+    for (int r = 0; r < S::NV; ++r) {
+        hiV[r] = 0u;
+        openV[r] = 0u;
+    }
+    uint32_t alive = 0u;
+#pragma nounroll
+    for (int k = 0; k < S::K; ++k) {
+        if (mine + k >= qn) break;
+        alive |= 1u << k;
+        const uint64_t *e = queue + (mine + k) * (uint64_t)(1 + 2 * W);
+        uint64_t hw[W], ow[W];
+#pragma unroll
+        for (int wj = 0; wj < W; ++wj) {
+            hw[wj] = e[1 + wj];
+            ow[wj] = e[1 + W + wj];
+        }
+        // transpose: register r, field f <- subset r*E + f of set k
+#pragma unroll
+        for (int r = 0; r < S::NV0; ++r) {
+            const int t0 = r * S::E;
+            const uint32_t hb = (uint32_t)(hw[t0 >> 6] >> (t0 & 63)) & ((1u << S::E) - 1u);
+            const uint32_t ob = (uint32_t)(ow[t0 >> 6] >> (t0 & 63)) & ((1u << S::E) - 1u);
+            uint32_t hs, os;
+            if constexpr (S::K == 8) {
+                // 4 bits -> bytes 0..3 (non-overlapping partial products)
+                hs = (hb * 0x00204081u) & 0x01010101u;
+                os = (ob * 0x00204081u) & 0x01010101u;
+            } else {
+                hs = os = 0u;
+#pragma unroll
+                for (int f = 0; f < S::E; ++f) {
+                    hs |= ((hb >> f) & 1u) << (S::K * f);
+                    os |= ((ob >> f) & 1u) << (S::K * f);
+                }
+            }
+            hiV[r] |= hs << k;
+            openV[r] |= os << k;
+        }
+    }
+    constexpr bool v0inP = PHASE == 0;
+    constexpr uint32_t Plocal = v0inP ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
+    uint32_t pvtop = 0;
+#pragma unroll
+    for (int i = 0; i < L; ++i) pvtop |= (uint32_t)(i + (v0inP ? 0 : 1)) << (4 * i);
+    uint32_t dom = 0u, pts = 0u;
+    if (wclock) walk_sliced<L, K, L, true>(Plocal, pvtop, alive, hiV, openV, alive, dom, pts);
+    else walk_sliced<L, K, L>(Plocal, pvtop, alive, hiV, openV, alive, dom, pts);
+    if (wclock && threadIdx.x == 0) {
+        // diagnostics (ULG_WALK_CLOCK): start, end, union points of this wave
+        wclock[3 * blockIdx.x] = t_start;
+        wclock[3 * blockIdx.x + 1] = wall_clock64();
+        wclock[3 * blockIdx.x + 2] = pts;
+    }
+#pragma nounroll
+    for (int k = 0; k < S::K; ++k) {
+        if (mine + k >= qn) break;
+        const uint64_t e0 = queue[(mine + k) * (uint64_t)(1 + 2 * W)];
+        const float ts = __uint_as_float((uint32_t)(e0 >> 32));
+        table[(uint32_t)e0] = ((dom >> k) & 1u) ? absent_f() : -ts;
+    }
 }
 
 __global__ void empty_set_kernel(const uint64_t *tbl_off, int nv, int S, float *table) {
@@ -983,12 +1227,12 @@ KernelFn pick(int phase, int variant) {
         case 4: case 6: return pick_phase<L, 4>(phase);
         case 5: case 7: return pick_phase<L, 5>(phase);
         case 13: return pick_phase<L, 13>(phase);
-        case 16: return pick_phase<L, 16>(phase);
-        case 17: return pick_phase<L, 17>(phase);
+        case 16: case 48: return pick_phase<L, 16>(phase);
+        case 17: case 49: return pick_phase<L, 17>(phase);
         default: return nullptr;
     }
 }
-using WalkFn = void (*)(const uint64_t *, const unsigned long long *, float *);
+using WalkFn = void (*)(const uint64_t *, const unsigned long long *, float *, uint64_t *);
 template <int L>
 WalkFn walk_pick(int phase) {
     return phase == 0 ? walk_kernel<L, 0> : walk_kernel<L, 1>;
@@ -1006,6 +1250,39 @@ WalkFn walk_fn(int L, int phase) {
         default: return nullptr;
     }
 }
+using SlicedFn = void (*)(const uint64_t *, const unsigned long long *, float *, uint64_t *);
+template <int L, int K>
+SlicedFn sliced_pick(int phase) {
+    return phase == 0 ? walk_sliced_kernel<L, 0, K> : walk_sliced_kernel<L, 1, K>;
+}
+template <int K>
+SlicedFn sliced_fn_k(int L, int phase) {
+    switch (L) {
+        case 1: return sliced_pick<1, K>(phase);
+        case 2: return sliced_pick<2, K>(phase);
+        case 3: return sliced_pick<3, K>(phase);
+        case 4: return sliced_pick<4, K>(phase);
+        case 5: return sliced_pick<5, K>(phase);
+        case 6: return sliced_pick<6, K>(phase);
+        default: return nullptr;  // L = 7, 8: the vectors no longer fit in registers
+    }
+}
+// sets per lane: more sets share one walk of the union tree, fewer give more
+// waves to hide the walk's latency
+int sliced_k(int L) {
+    (void)L;
+    const char *e = std::getenv("ULG_SLICED_K");
+    const int k = e ? std::atoi(e) : 4;
+    return (k == 2 || k == 8) ? k : 4;
+}
+SlicedFn sliced_fn(int L, int phase) {
+    switch (sliced_k(L)) {
+        case 2: return sliced_fn_k<2>(L, phase);
+        case 4: return sliced_fn_k<4>(L, phase);
+        default: return sliced_fn_k<8>(L, phase);
+    }
+}
+
 const char *kWalkNames[2][kMaxL + 1] = {
     {"", "walk_1_var0", "walk_2_var0", "walk_3_var0", "walk_4_var0", "walk_5_var0", "walk_6_var0", "walk_7_var0",
      "walk_8_var0"},
@@ -1179,76 +1456,171 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     sa.n = n;
     sa.nv = nv;
     sa.S = S;
-    if (c->score_variant & 16) {
-        // queue sized for the largest launch: every lane may be left undecided
-        uint64_t qwords = 0;
-        for (int L = 1; L <= kmax; ++L)
-            for (int ph = 0; ph < 2; ++ph)
-                qwords = std::max<uint64_t>(qwords, work[((size_t)L * 2 + ph) * (nv + 1) + nv] *
-                                                        (uint64_t)(2 + 2 * bits_words(L)));
-        if ((rc = ensure(c, c->d_queue, (size_t)qwords)) || (rc = ensure(c, c->d_qcount, (size_t)2 * (kmax + 1))))
+    // queue entries address the table with 32 bits; beyond that the one-pass
+    // form (identical results) is used
+    const int variant = (c->score_variant & 16) && (total_slots >> 32) ? 1 : c->score_variant;
+    const char *wck = std::getenv("ULG_WALK_CLOCK");  // walk diagnostics (synchronising)
+    // Variables never read each other's slabs, so they are striped over G
+    // groups on concurrent streams: a group's latency-bound walk kernels
+    // overlap the other groups' scoring kernels.  Diagnostics run on one.
+    const int G = ((variant & 16) && !(variant & 8) && !wck) ? std::max(1, std::min(c->score_streams, nv)) : 1;
+    while ((int)c->aux_streams.size() < G - 1) {
+        hipStream_t st;
+        ULG_HIP(c, hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        c->aux_streams.push_back(st);
+    }
+    while ((int)c->sync_events.size() < 2 * G) {
+        hipEvent_t ev;
+        ULG_HIP(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        c->sync_events.push_back(ev);
+    }
+    std::vector<hipStream_t> gst(G);
+    gst[0] = c->stream;
+    for (int g = 1; g < G; ++g) gst[g] = c->aux_streams[g - 1];
+    // per group work prefixes (variables outside the group count 0 sets)
+    const size_t wstride = (size_t)(kmax + 1) * 2 * (nv + 1);
+    std::vector<uint64_t> workg(G == 1 ? 0 : (size_t)G * wstride, 0);
+    if (G > 1) {
+        for (int g = 0; g < G; ++g)
+            for (int L = 1; L <= kmax; ++L)
+                for (int ph = 0; ph < 2; ++ph) {
+                    const uint64_t *w = &work[((size_t)L * 2 + ph) * (nv + 1)];
+                    uint64_t *wg = &workg[(size_t)g * wstride + ((size_t)L * 2 + ph) * (nv + 1)];
+                    uint64_t acc2 = 0;
+                    for (int i = 0; i < nv; ++i) {
+                        wg[i] = acc2;
+                        if (i % G == g) acc2 += w[i + 1] - w[i];
+                    }
+                    wg[nv] = acc2;
+                }
+        if ((rc = upload(c, c->d_workg, c->mir_workg, workg))) return rc;
+    }
+    const uint64_t *d_wk = G > 1 ? c->d_workg.p : c->d_work.p;
+    const std::vector<uint64_t> &h_wk = G > 1 ? workg : work;
+    uint64_t qwords = 0;  // per group: every lane of its largest launch may be queued
+    if (variant & 16) {
+        for (int g = 0; g < G; ++g)
+            for (int L = 1; L <= kmax; ++L)
+                for (int ph = 0; ph < 2; ++ph)
+                    qwords = std::max<uint64_t>(qwords, h_wk[(size_t)g * wstride + ((size_t)L * 2 + ph) * (nv + 1) + nv] *
+                                                            (uint64_t)(1 + 2 * bits_words(L)));
+        if ((rc = ensure(c, c->d_queue, (size_t)G * qwords)) || (rc = ensure(c, c->d_qcount, (size_t)G * 2 * (kmax + 1))))
             return rc;
-        ULG_HIP(c, hipMemsetAsync(c->d_qcount.p, 0, sizeof(unsigned long long) * 2 * (kmax + 1), c->stream));
-        sa.queue = c->d_queue.p;
+        ULG_HIP(c, hipMemsetAsync(c->d_qcount.p, 0, sizeof(unsigned long long) * G * 2 * (kmax + 1), c->stream));
+    }
+    // fork: the side streams start after the uploads / empty-set kernel
+    if (G > 1) {
+        ULG_HIP(c, hipEventRecord(c->sync_events[0], c->stream));
+        for (int g = 1; g < G; ++g) ULG_HIP(c, hipStreamWaitEvent(gst[g], c->sync_events[0], 0));
     }
     for (int L = 1; L <= kmax; ++L)
-        for (int ph = 0; ph < 2; ++ph) {
-            const uint64_t *w = &work[((size_t)L * 2 + ph) * (nv + 1)];
-            const uint64_t cnt = w[nv];
-            if (cnt == 0) continue;
-            sa.work = c->d_work.p + ((size_t)L * 2 + ph) * (nv + 1);
-            const uint64_t blocks = (cnt + kBlock - 1) / kBlock;
-            if (blocks > 0x7fffffffull) return set_err(c, ULG_ERR_UNSUPPORTED, "ulg_cbic_score: layer too large");
-            const LdsLayout lay = lds_layout(n, nv, S, L, c->score_variant);
-            prof_begin(c, kLayerNames[ph][L]);
-            const KernelFn kfn = layer_kernel(L, ph, c->score_variant);
-            if (lay.total > 64 * 1024)
-                ULG_HIP(c, hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, lay.total));
-            if (c->score_variant & 8) {
-                if ((rc = ensure(c, c->d_stats, 16))) return rc;
-                ULG_HIP(c, hipMemsetAsync(c->d_stats.p, 0, 16 * 8, c->stream));
-                sa.stats = c->d_stats.p;
-                sa.dump_cap = 4u << 20;
-                if ((rc = ensure(c, c->d_dump, (size_t)sa.dump_cap * (2 * bits_words(L) + 1)))) return rc;
-                sa.dump = c->d_dump.p;
-            }
-            if (c->score_variant & 16) sa.qcount = c->d_qcount.p + (L * 2 + ph);
-            hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(kBlock), (size_t)lay.total, c->stream, sa);
-            prof_end(c);
-            if (c->score_variant & 16) {
-                // the undecided lanes of this launch, densely packed
-                const WalkFn wfn = walk_fn(L, ph);
-                const int W = bits_words(L);
-                const size_t wl = W >= 4 ? (size_t)4 * W * kBlock * 8 : 0;
-                if (wl > 64 * 1024)
-                    ULG_HIP(c, hipFuncSetAttribute((const void *)wfn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                   (int)wl));
-                prof_begin(c, kWalkNames[ph][L]);
-                hipLaunchKernelGGL(wfn, dim3((unsigned)blocks), dim3(kBlock), wl, c->stream, c->d_queue.p,
-                                   c->d_qcount.p + (L * 2 + ph), c->table.p);
-                prof_end(c);
-            }
-            if (c->score_variant & 8) {
-                unsigned long long st[16];
-                ULG_HIP(c, hipMemcpyAsync(st, c->d_stats.p, sizeof st, hipMemcpyDeviceToHost, c->stream));
-                ULG_HIP(c, hipStreamSynchronize(c->stream));
-                std::fprintf(stderr,
-                             "score_stats L=%d phase=%d waves=%llu lanes: ts>=0 %llu, no-hi %llu, direct-hi %llu, "
-                             "walk-dom %llu, walk-stored %llu; walking waves %llu; steps lane-sum %llu wave-max-sum %llu\n",
-                             L, ph, st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8]);
-                if (const char *dd = std::getenv("ULG_DUMP_DIR")) {
-                    const uint64_t cntd = std::min<uint64_t>(st[9], sa.dump_cap);
-                    std::vector<uint64_t> hd((size_t)cntd * (2 * bits_words(L) + 1));
-                    ULG_HIP(c, hipMemcpy(hd.data(), c->d_dump.p, hd.size() * 8, hipMemcpyDeviceToHost));
-                    char fn[512];
-                    std::snprintf(fn, sizeof fn, "%s/walk_L%d_p%d.bin", dd, L, ph);
-                    if (FILE *f = std::fopen(fn, "wb")) {
-                        std::fwrite(hd.data(), 8, hd.size(), f);
-                        std::fclose(f);
+        for (int ph = 0; ph < 2; ++ph)
+            for (int g = 0; g < G; ++g) {
+                const size_t wo = (size_t)g * (G > 1 ? wstride : 0) + ((size_t)L * 2 + ph) * (nv + 1);
+                const uint64_t cnt = h_wk[wo + nv];
+                if (cnt == 0) continue;
+                hipStream_t st = gst[g];
+                sa.work = d_wk + wo;
+                unsigned long long *qc = (variant & 16) ? c->d_qcount.p + (size_t)g * 2 * (kmax + 1) + (L * 2 + ph) : nullptr;
+                sa.queue = (variant & 16) ? c->d_queue.p + (size_t)g * qwords : nullptr;
+                sa.qcount = qc;
+                const uint64_t blocks = (cnt + kBlock - 1) / kBlock;
+                if (blocks > 0x7fffffffull) return set_err(c, ULG_ERR_UNSUPPORTED, "ulg_cbic_score: layer too large");
+                const LdsLayout lay = lds_layout(n, nv, S, L, variant);
+                const KernelFn kfn = layer_kernel(L, ph, variant);
+                if (lay.total > 64 * 1024)
+                    ULG_HIP(c, hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, lay.total));
+                if (variant & 8) {
+                    if ((rc = ensure(c, c->d_stats, 16))) return rc;
+                    ULG_HIP(c, hipMemsetAsync(c->d_stats.p, 0, 16 * 8, st));
+                    sa.stats = c->d_stats.p;
+                    sa.dump_cap = 4u << 20;
+                    if ((rc = ensure(c, c->d_dump, (size_t)sa.dump_cap * (2 * bits_words(L) + 1)))) return rc;
+                    sa.dump = c->d_dump.p;
+                }
+                prof_begin_s(c, kLayerNames[ph][L], st);
+                hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(kBlock), (size_t)lay.total, st, sa);
+                prof_end_s(c, st);
+                if (variant & 16) {
+                    // the undecided lanes of this launch, densely packed
+                    if ((variant & 32) && sliced_fn(L, ph)) {
+                        const uint64_t per = 64ull * (uint64_t)sliced_k(L);
+                        const uint64_t sb = (cnt + per - 1) / per;
+                        if (wck && (rc = ensure(c, c->d_dump, (size_t)3 * sb))) return rc;
+                        if (wck) ULG_HIP(c, hipMemsetAsync(c->d_dump.p, 0, 24 * sb, st));
+                        prof_begin_s(c, kWalkNames[ph][L], st);
+                        hipLaunchKernelGGL(sliced_fn(L, ph), dim3((unsigned)sb), dim3(64), 0, st, sa.queue, qc,
+                                           c->table.p, wck ? c->d_dump.p : nullptr);
+                        prof_end_s(c, st);
+                        if (wck) {
+                            std::vector<uint64_t> hw((size_t)3 * sb);
+                            ULG_HIP(c, hipMemcpyAsync(hw.data(), c->d_dump.p, hw.size() * 8, hipMemcpyDeviceToHost, st));
+                            ULG_HIP(c, hipStreamSynchronize(st));
+                            char fn[512];
+                            std::snprintf(fn, sizeof fn, "%s/sliced_L%d_p%d.bin", wck, L, ph);
+                            if (FILE *f = std::fopen(fn, "wb")) {
+                                std::fwrite(hw.data(), 8, hw.size(), f);
+                                std::fclose(f);
+                            }
+                        }
+                    } else {
+                        const WalkFn wfn = walk_fn(L, ph);
+                        const int W = bits_words(L);
+                        const size_t wl = W >= 4 ? (size_t)2 * W * kBlock * 8 : 0;
+                        if (wl > 64 * 1024)
+                            ULG_HIP(c, hipFuncSetAttribute((const void *)wfn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                           (int)wl));
+                        // per wave start/end (2 words x waves+1), then one record per queued lane
+                        const size_t wck_words = (size_t)2 * (blocks * kBlock / 64 + 1) + (size_t)blocks * kBlock;
+                        if (wck && (rc = ensure(c, c->d_dump, wck_words))) return rc;
+                        if (wck) ULG_HIP(c, hipMemsetAsync(c->d_dump.p, 0, 8 * wck_words, st));
+                        prof_begin_s(c, kWalkNames[ph][L], st);
+                        hipLaunchKernelGGL(wfn, dim3((unsigned)blocks), dim3(kBlock), wl, st, sa.queue, qc, c->table.p,
+                                           wck ? c->d_dump.p : nullptr);
+                        prof_end_s(c, st);
+                        if (wck) {
+                            std::vector<uint64_t> hw(wck_words);
+                            unsigned long long qn = 0;
+                            ULG_HIP(c, hipMemcpyAsync(hw.data(), c->d_dump.p, hw.size() * 8, hipMemcpyDeviceToHost, st));
+                            ULG_HIP(c, hipMemcpyAsync(&qn, qc, 8, hipMemcpyDeviceToHost, st));
+                            ULG_HIP(c, hipStreamSynchronize(st));
+                            char fn[512];
+                            std::snprintf(fn, sizeof fn, "%s/wclock_L%d_p%d.bin", wck, L, ph);
+                            if (FILE *f = std::fopen(fn, "wb")) {
+                                std::fwrite(&qn, 8, 1, f);
+                                std::fwrite(hw.data(), 8, hw.size(), f);
+                                std::fclose(f);
+                            }
+                        }
+                    }
+                }
+                if (variant & 8) {
+                    unsigned long long stt[16];
+                    ULG_HIP(c, hipMemcpyAsync(stt, c->d_stats.p, sizeof stt, hipMemcpyDeviceToHost, st));
+                    ULG_HIP(c, hipStreamSynchronize(st));
+                    std::fprintf(stderr,
+                                 "score_stats L=%d phase=%d waves=%llu lanes: ts>=0 %llu, no-hi %llu, direct-hi %llu, "
+                                 "walk-dom %llu, walk-stored %llu; walking waves %llu; steps lane-sum %llu wave-max-sum %llu\n",
+                                 L, ph, stt[0], stt[1], stt[2], stt[3], stt[4], stt[5], stt[6], stt[7], stt[8]);
+                    if (const char *dd = std::getenv("ULG_DUMP_DIR")) {
+                        const uint64_t cntd = std::min<uint64_t>(stt[9], sa.dump_cap);
+                        std::vector<uint64_t> hd((size_t)cntd * (2 * bits_words(L) + 1));
+                        ULG_HIP(c, hipMemcpyAsync(hd.data(), c->d_dump.p, hd.size() * 8, hipMemcpyDeviceToHost, st));
+                        ULG_HIP(c, hipStreamSynchronize(st));
+                        char fn[512];
+                        std::snprintf(fn, sizeof fn, "%s/walk_L%d_p%d.bin", dd, L, ph);
+                        if (FILE *f = std::fopen(fn, "wb")) {
+                            std::fwrite(hd.data(), 8, hd.size(), f);
+                            std::fclose(f);
+                        }
                     }
                 }
             }
-        }
+    // join: the compaction on the context stream waits for every group
+    for (int g = 1; g < G; ++g) {
+        ULG_HIP(c, hipEventRecord(c->sync_events[g], gst[g]));
+        ULG_HIP(c, hipStreamWaitEvent(c->stream, c->sync_events[g], 0));
+    }
     ULG_HIP(c, hipGetLastError());
 
     // compaction

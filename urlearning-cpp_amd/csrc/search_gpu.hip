@@ -260,7 +260,8 @@ int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, flo
         *goal_cost = g;
     }
     std::vector<unsigned long long> acc(kCounters, 0);
-    e = hipMemcpy(acc.data(), d_acc.p, kCounters * 8, hipMemcpyDeviceToHost);
+    e = hipMemcpyAsync(acc.data(), d_acc.p, kCounters * 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     prof_collect(c);
     cleanup();
     if (e != hipSuccess) return set_err(c, ULG_ERR_HIP, hipGetErrorString(e));

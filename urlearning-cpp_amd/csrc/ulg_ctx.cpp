@@ -32,8 +32,12 @@ uint64_t binom64(int a, int b) {
     return r > ~0ull ? ~0ull : (uint64_t)r;
 }
 
-void prof_begin(ulg_ctx *c, const char *name) {
-    if (!c->prof) return;
+void prof_begin(ulg_ctx *c, const char *name) { prof_begin_s(c, name, c->stream); }
+void prof_end(ulg_ctx *c) { prof_end_s(c, c->stream); }
+
+void prof_begin_s(ulg_ctx *c, const char *name, hipStream_t stream) {
+    c->prof_skip = !c->prof || (!c->prof_only.empty() && !c->prof_only.count(name));
+    if (c->prof_skip) return;
     ProfRec r;
     r.name = name;
     // events come from a per-context pool: creating two per kernel costs more
@@ -46,13 +50,13 @@ void prof_begin(ulg_ctx *c, const char *name) {
             (void)hipEventCreate(e);
         }
     }
-    (void)hipEventRecord(r.start, c->stream);
+    (void)hipEventRecord(r.start, stream);
     c->pending.push_back(r);
 }
 
-void prof_end(ulg_ctx *c) {
-    if (!c->prof || c->pending.empty()) return;
-    (void)hipEventRecord(c->pending.back().stop, c->stream);
+void prof_end_s(ulg_ctx *c, hipStream_t stream) {
+    if (c->prof_skip || c->pending.empty()) return;
+    (void)hipEventRecord(c->pending.back().stop, stream);
 }
 
 void prof_collect(ulg_ctx *c) {
@@ -108,9 +112,13 @@ void ulg_destroy(ulg_ctx *c) {
     prof_collect(c);
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
     c->event_pool.clear();
+    for (hipStream_t s : c->aux_streams) (void)hipStreamDestroy(s);
+    c->aux_streams.clear();
+    for (hipEvent_t e : c->sync_events) (void)hipEventDestroy(e);
+    c->sync_events.clear();
     release(c->raw); release(c->z); release(c->gram); release(c->partials); release(c->colstat);
     release(c->table); release(c->d_tbl_off); release(c->d_work); release(c->d_blk);
-    release(c->d_cand); release(c->d_meta); release(c->d_binom); release(c->d_stats); release(c->d_dump); release(c->d_queue); release(c->d_qcount);
+    release(c->d_cand); release(c->d_meta); release(c->d_binom); release(c->d_stats); release(c->d_dump); release(c->d_queue); release(c->d_qcount); release(c->d_workg);
     release(c->out_sets); release(c->out_scores); release(c->out_offsets);
     release(c->qbuf_in); release(c->qbuf_out);
     pss_release(c);
@@ -127,9 +135,14 @@ const char *ulg_last_error(const ulg_ctx *c) { return c ? c->err.c_str() : "null
 
 int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
     if (!c || !name) return ULG_ERR_ARG;
+    if (std::strcmp(name, "score_streams") == 0) {
+        if (value < 1 || value > 4) return set_err(c, ULG_ERR_ARG, "score_streams must be 1..4");
+        c->score_streams = (int)value;
+        return ULG_OK;
+    }
     if (std::strcmp(name, "score_variant") == 0) {
-        if (value < 0 || (value > 7 && value != 13 && value != 16 && value != 17))
-            return set_err(c, ULG_ERR_ARG, "score_variant must be 0..7, 13, 16 or 17");
+        if (value < 0 || (value > 7 && value != 13 && value != 16 && value != 17 && value != 48 && value != 49))
+            return set_err(c, ULG_ERR_ARG, "score_variant must be 0..7, 13, 16, 17, 48 or 49");
         c->score_variant = (int)value;
         return ULG_OK;
     }
@@ -144,6 +157,24 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
 int ulg_profile_enable(ulg_ctx *c, int on) {
     if (!c) return ULG_ERR_ARG;
     c->prof = on != 0;
+    return ULG_OK;
+}
+
+int ulg_profile_select(ulg_ctx *c, const char *names) {
+    if (!c) return ULG_ERR_ARG;
+    c->prof_only.clear();
+    if (names) {
+        std::string cur;
+        for (const char *p = names;; ++p) {
+            if (*p == ',' || *p == 0) {
+                if (!cur.empty()) c->prof_only.insert(cur);
+                cur.clear();
+                if (*p == 0) break;
+            } else {
+                cur += *p;
+            }
+        }
+    }
     return ULG_OK;
 }
 

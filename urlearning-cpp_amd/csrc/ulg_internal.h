@@ -7,6 +7,7 @@
 #include <map>
 #include <string>
 #include <cstring>
+#include <set>
 #include <vector>
 
 #include "../../include/ulg.h"
@@ -65,7 +66,10 @@ struct ulg_ctx {
     int64_t total_stored = 0;
     int64_t total_scored = 0;
     bool scored = false;
-    int score_variant = 17;
+    int score_variant = 49;
+    int score_streams = 3;                  // scorer variable groups on concurrent streams
+    std::vector<hipStream_t> aux_streams;   // created on first use
+    std::vector<hipEvent_t> sync_events;
     uint64_t table_budget_kb = 0;  // best-score table budget in KiB (0 = half the free HBM)  // see ScoreArgs::variant (ulg_set_option "score_variant")
     ulg::DevBuf<float> table;
     ulg::DevBuf<uint64_t> d_tbl_off, d_work, d_blk;
@@ -76,6 +80,7 @@ struct ulg_ctx {
     ulg::DevBuf<uint64_t> d_dump;
     ulg::DevBuf<uint64_t> d_queue;                // score_variant bit 4: undecided lanes
     ulg::DevBuf<unsigned long long> d_qcount;
+    ulg::DevBuf<uint64_t> d_workg;                // per stream-group work prefixes
     ulg::DevBuf<uint64_t> out_sets;
     ulg::DevBuf<float> out_scores;
     ulg::DevBuf<int64_t> out_offsets;
@@ -91,8 +96,10 @@ struct ulg_ctx {
     // ---- profiling ----
     bool prof = false;
     std::vector<ulg::ProfRec> pending;
+    std::set<std::string> prof_only;  // ulg_profile_select: time only these kernels
+    bool prof_skip = false;
     std::vector<hipEvent_t> event_pool;
-    ulg::Mirror mir_tbl_off, mir_work, mir_cand, mir_meta;
+    ulg::Mirror mir_tbl_off, mir_work, mir_cand, mir_meta, mir_workg;
     std::map<std::string, std::vector<double>> prof_ms;
 };
 
@@ -146,6 +153,8 @@ void release(DevBuf<T> &b) {
 // profiling: bracket a launch with events when enabled
 void prof_begin(ulg_ctx *c, const char *name);
 void prof_end(ulg_ctx *c);
+void prof_begin_s(ulg_ctx *c, const char *name, hipStream_t stream);
+void prof_end_s(ulg_ctx *c, hipStream_t stream);
 void prof_collect(ulg_ctx *c);  // after a stream sync
 void pss_release(ulg_ctx *c);    // pss.hip
 

@@ -59,6 +59,7 @@ def lib():
         L.ulg_profile_get.argtypes = [P, C.c_char_p, C.POINTER(D), C.POINTER(I64), C.POINTER(D)]
         L.ulg_profile_dump.argtypes = [P, C.c_char_p, I64]
         L.ulg_profile_reset.argtypes = [P]
+        L.ulg_profile_select.argtypes = [P, C.c_char_p]
         _lib = L
     return _lib
 
@@ -260,6 +261,11 @@ class Context:
     # ---- profiling ----------------------------------------------------------
     def profile(self, on: bool = True):
         self._check(lib().ulg_profile_enable(self._h, 1 if on else 0), "ulg_profile_enable")
+
+    def profile_select(self, names=None):
+        """Time only these kernels (None = all)."""
+        arg = ",".join(names).encode() if names else None
+        self._check(lib().ulg_profile_select(self._h, arg), "ulg_profile_select")
 
     def profile_reset(self):
         self._check(lib().ulg_profile_reset(self._h), "ulg_profile_reset")
