@@ -55,9 +55,13 @@ typedef struct ulg_ctx ulg_ctx;
 #define ULG_ERR_STATE 3
 #define ULG_ERR_UNSUPPORTED 4
 
-/* Largest parent-set size the HIP scorer handles (compile-time unrolled
- * Cholesky + dominance recursion per layer). */
-#define ULG_MAX_PARENTS_GPU 8
+/* Largest parent-set size the HIP scorer handles.  Layers up to
+ * ULG_UNROLLED_PARENTS_GPU run fully unrolled kernels (register Cholesky,
+ * bitset dominance walk); larger layers (the reference's default -p = n-1 on
+ * small n, e.g. data/hepatitis.clean.csv) run the wide-layer kernels, whose
+ * find_best_subset_score walk keeps a 2^(k+1)-bit checked set per set. */
+#define ULG_MAX_PARENTS_GPU 31
+#define ULG_UNROLLED_PARENTS_GPU 8
 
 /* ---- context --------------------------------------------------------- */
 /* One device per context: ndev must be 1 (multi-GPU = one process per GPU). */

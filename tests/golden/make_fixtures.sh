@@ -16,3 +16,6 @@ mkdir -p "$D/fig3"
 for s in $(seq 9200 9229); do cp "$R/Figure_3/learned_result/astar2_N10000_$s.csv" "$D/fig3/"; done
 cp "$R/Figure_4/edge_true_astar_ges_10k_group2_lambda1.csv" "$D/fig4_edge_true_astar_ges_10k_group2_lambda1.csv"
 chmod 644 "$D"/*.csv "$D"/fig3/*.csv
+# Config C1's data (BASELINE.json configs[0]): the reference's data/hepatitis.clean.csv
+cp "${1:-/root/reference}/data/hepatitis.clean.csv" "$D/hepatitis.clean.csv"
+chmod 644 "$D/hepatitis.clean.csv"

@@ -131,3 +131,43 @@ def test_triplet_cli_reproduces_mec(tmp_path, oracle_built, fig, lam):
     assert net.read_text() == ""
     subprocess.run([o.REF_TRIPLET, str(pss), "-k", str(skel), "-n", str(ref_net)], check=True, stdout=subprocess.DEVNULL)
     assert (tmp_path / "net.csv").read_text() == (tmp_path / "ref_net.csv").read_text()
+
+
+@pytest.mark.gpu
+def test_cli_c1_hepatitis_default_parent_limit(tmp_path):
+    """Config C1 (BASELINE.json configs[0]) through the drop-in command lines
+    on the GPU: data/hepatitis.clean.csv, --lambda 2, full skeleton, default
+    -p = n - 1 = 19 (score_main.cpp:296-298; the scorer's wide layers).  The
+    1.26 GB .pss must be byte-identical to the oracle's command line output
+    and the netFile / netFile.csv identical to its A*
+    (tests/golden/make_c1_cli.sh wrote the fixture)."""
+    import hashlib
+    import json
+    with open(os.path.join(GOLDEN, "c1_hepatitis_cli.json")) as f:
+        ref = json.load(f)
+    skel = tmp_path / "full20.csv"
+    skel.write_text("\n".join([",".join(["1"] * 20)] * 20) + "\n")
+    pss = tmp_path / "c1.pss"
+    r = _run([SCORE, ref["csv"], str(pss), "-f", "cBIC", "--lambda", ref["lambda"], "-k", str(skel)],
+             cwd=GOLDEN)  # relative input path, as the fixture was made (the header records it)
+    assert r.returncode == 0, r.stderr
+    assert os.path.getsize(pss) == ref["pss_bytes"]
+    h = hashlib.sha256()
+    with open(pss, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 24), b""):
+            h.update(chunk)
+    assert h.hexdigest() == ref["pss_sha256"]
+    for mode in ("exact", "gpu"):
+        net = tmp_path / f"net_{mode}"
+        r = _run([ASTAR, str(pss), "-k", str(skel), "-n", str(net), "--mode", mode])
+        assert r.returncode == 0, r.stderr
+        cost = float(r.stdout.split("Found solution:")[1].split()[0])
+        ref_cost = float(ref["solution"].split(":")[1])
+        # the batched search sums g in layer order, not the reference's path
+        # order: the optimal cost up to float rounding (1e-6 relative)
+        assert abs(cost - ref_cost) <= 1e-6 * abs(ref_cost), (mode, cost, ref_cost)
+        if mode == "exact":  # the exact-order replay: the reference's DAG and its printed cost (SURVEY N10)
+            assert ref["solution"] in r.stdout
+            assert net.read_text() == ref["net"]
+            assert (tmp_path / "net_exact.csv").read_text() == ref["net_csv"]
+    os.remove(pss)

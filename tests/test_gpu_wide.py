@@ -1,0 +1,95 @@
+"""GPU parity of the wide scorer layers (parent sets larger than
+ULG_UNROLLED_PARENTS_GPU = 8, up to ULG_MAX_PARENTS_GPU = 31).
+
+The reference's default parent limit is n - 1 (score_main.cpp:296-298), so
+config C1 (data/hepatitis.clean.csv, n = 20) scores layers 1..19.  Layers
+above 8 run the runtime-L kernels of cbic.hip (score_wide_kernel +
+walk_wide_kernel, the explicit-stack replay of find_best_subset_score,
+BIC_OLS.cpp:125-172).
+
+Bar as in test_gpu_cbic.py: stored sets bit-exact, scores within 1e-6
+relative.  Small configurations compare against the oracle run here; C1
+compares against tests/golden/c1_hepatitis_digest.json, the oracle's full run
+reduced to per-variable digests by tests/golden/make_c1_digest.py (the oracle
+needs tens of CPU-minutes for it)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from test_gpu_cbic import _compare_lists, _oracle_lists, REL_TOL
+import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def load_csv_ascii(path):
+    """Armadillo csv_ascii as the reference loads it: rows = lines,
+    a non-numeric token (the header) reads as 0.  Same rule as host/io.cpp."""
+    with open(path) as f:
+        lines = [ln.rstrip("\r\n") for ln in f]
+    n = max(ln.count(",") + 1 for ln in lines)
+    X = np.zeros((len(lines), n), dtype=np.float64)
+    for r, ln in enumerate(lines):
+        for c, tok in enumerate(ln.split(",")):
+            try:
+                X[r, c] = float(tok)
+            except ValueError:
+                pass
+    return X
+
+
+@pytest.mark.parametrize("seed,n,N,k", [(9210, 11, 2000, 10), (9211, 12, 1500, 11), (9212, 13, 3000, 9),
+                                        (9213, 14, 1000, 13)])
+def test_wide_layers_full_skeleton_match_oracle(ulg_ctx, oracle_built, seed, n, N, k):
+    X, _ = synth.gaussian_sem(n, N, seed)
+    variables = list(range(n))
+    cands = [(1 << n) - 1] * n
+    ulg_ctx.load(X, 2.0)
+    g = ulg_ctx.score_all(variables, cands, k)
+    o = _oracle_lists(oracle_built, X, 2.0, variables, cands, k)
+    _compare_lists(*o, *g, variables, ctx=f"seed {seed} k={k}")
+
+
+@pytest.mark.parametrize("lam", [0.5, 2.0])
+def test_wide_layers_hepatitis_prefix_match_oracle(ulg_ctx, oracle_built, lam):
+    """The C1 data on its first 13 columns at k = 12: weak-signal data where
+    many large sets survive (the walk-heavy case)."""
+    X = load_csv_ascii(os.path.join(GOLDEN, "hepatitis.clean.csv"))[:, :13]
+    n = X.shape[1]
+    variables = list(range(n))
+    cands = [(1 << n) - 1] * n
+    ulg_ctx.load(X, lam)
+    g = ulg_ctx.score_all(variables, cands, n - 1)
+    o = _oracle_lists(oracle_built, X, lam, variables, cands, n - 1)
+    _compare_lists(*o, *g, variables, ctx=f"hepatitis[:, :13] lam={lam}")
+
+
+def test_c1_hepatitis_default_parent_limit_matches_digest(ulg_ctx):
+    """Config C1 (BASELINE.json configs[0]) on the GPU: all 20 variables, full
+    skeleton, -p default n - 1 = 19, against the oracle's digest."""
+    with open(os.path.join(GOLDEN, "c1_hepatitis_digest.json")) as f:
+        dig = json.load(f)
+    X = load_csv_ascii(os.path.join(GOLDEN, dig["csv"]))
+    n = X.shape[1]
+    assert (X.shape[0], n) == (dig["N"], dig["n"])
+    variables = list(range(n))
+    cands = [(1 << n) - 1] * n
+    for lam_s, per_var in dig["runs"].items():
+        ulg_ctx.load(X, float(lam_s))
+        offs, sets, scores = ulg_ctx.score_all(variables, cands, dig["max_parents"])
+        for v in variables:
+            d = per_var[v]
+            s = sets[offs[v]:offs[v + 1]]
+            sc = scores[offs[v]:offs[v + 1]]
+            assert len(s) == d["count"], f"lam={lam_s} variable {v}: {len(s)} stored vs oracle {d['count']}"
+            assert hashlib.sha256(np.ascontiguousarray(s, dtype=np.uint64).tobytes()).hexdigest() == d["sets_sha256"], \
+                f"lam={lam_s} variable {v}: stored sets differ from the oracle's"
+            tot = float(sc.astype(np.float64).sum())
+            assert abs(tot - d["score_sum"]) <= REL_TOL * max(abs(d["score_sum"]), 1.0), (v, tot, d["score_sum"])
+            for idx, (ps, pscore) in zip(np.unique(np.linspace(0, len(s) - 1, 64).astype(np.int64)), d["samples"]):
+                assert int(s[idx]) == ps
+                assert abs(float(sc[idx]) - pscore) <= REL_TOL * max(abs(pscore), 1.0), (v, ps, float(sc[idx]), pscore)

@@ -1081,6 +1081,292 @@ __global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, 
     }
 }
 
+// ---- wide layers (kMaxL < L <= kWideMax) ------------------------------------
+// The reference's default parent limit is n - 1 (score_main.cpp:296-298), so on
+// small n (data/hepatitis.clean.csv: n = 20) the layers run to 19 parents.
+// Those layers use runtime-L kernels: the same Cholesky-of-the-Gram score per
+// lane (the triangle in private memory), the direct-children decision in the
+// scoring kernel (a present child P\{a} >= -ts is always visited at the top
+// level: present keys never enter `checked`), and, for the rest, an explicit
+// stack replay of find_best_subset_score (BIC_OLS.cpp:125-172)
+// whose `checked` set is a 2^q-bit bitset per walking set in HBM (q local
+// bits: P, plus variable 0 when P lacks it).
+constexpr uint64_t kWideStepCap = 1ull << 30;  // per-set walk steps before the call fails loudly
+constexpr uint64_t kWideBitsWords = 1ull << 27;  // checked bitsets, all stream groups together (1 GiB)
+
+__device__ __forceinline__ uint64_t B64(const uint64_t *b, int a, int k) { return b[a * 64 + k]; }
+
+__device__ __forceinline__ uint64_t unrank_colex64(uint64_t r, int l, int U, const uint64_t *b) {
+    uint64_t mask = 0;
+    int c = U - 1;
+    for (int i = l; i >= 1; --i) {
+        while (c >= 0 && B64(b, c, i) > r) --c;
+        mask |= 1ull << c;
+        r -= B64(b, c, i);
+        --c;
+    }
+    return mask;
+}
+
+__device__ __forceinline__ uint64_t rank_colex64(uint64_t mask, const uint64_t *b) {
+    uint64_t r = 0;
+    int j = 0;
+    while (mask) {
+        const int x = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        ++j;
+        r += B64(b, x, j);
+    }
+    return r;
+}
+
+struct WideArgs {
+    const double *gram;       // n x n row-major
+    const uint64_t *binom;    // [64][64]
+    const uint8_t *cand;      // [nv][64]
+    const int *meta;          // [nv][4]
+    const uint64_t *tbl_off;  // [nv*S + 1]
+    const uint64_t *work;     // [nv + 1] prefix of this launch's sets
+    float *table;
+    uint64_t *queue;          // 3 words per undecided set: slot, compact mask, vi | ts bits << 32
+    unsigned long long *qcount;
+    double N;
+    double lambda;
+    int n, nv, S, L;
+};
+
+template <int LMAX, int PHASE>
+__global__ void __launch_bounds__(kBlock) score_wide_kernel(WideArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double *g = reinterpret_cast<double *>(smem);
+    for (int i = threadIdx.x; i < a.n * a.n; i += kBlock) g[i] = a.gram[i];
+    __syncthreads();
+    const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (gid >= a.work[a.nv]) return;
+    int lo = 0, hi = a.nv;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (a.work[mid] <= gid) lo = mid; else hi = mid;
+    }
+    const int vi = lo;
+    const int v = a.meta[vi * 4 + 0];
+    const int m = a.meta[vi * 4 + 1];
+    const bool z = a.meta[vi * 4 + 2] != 0;
+    const int L = a.L;
+    const uint64_t r = gid - a.work[vi];
+    uint64_t cm;
+    if (PHASE == 0) cm = (unrank_colex64(r, L - 1, m - 1, a.binom) << 1) | 1ull;
+    else if (z) cm = unrank_colex64(r, L, m - 1, a.binom) << 1;
+    else cm = unrank_colex64(r, L, m, a.binom);
+    const uint64_t slot = a.tbl_off[(uint64_t)vi * a.S + L] + rank_colex64(cm, a.binom);
+
+    int gv[LMAX];
+    {
+        uint64_t rem = cm;
+        for (int i = 0; i < L; ++i) {
+            gv[i] = a.cand[vi * 64 + __builtin_ctzll(rem)];
+            rem &= rem - 1;
+        }
+    }
+    // Cholesky of G[P,P] (packed rows, row i at i(i+1)/2), y = L^-1 G[P,v]:
+    // the unrolled kernels' operation order
+    double Lm[LMAX * (LMAX + 1) / 2];
+    double y[LMAX];
+    const int n = a.n;
+    for (int i = 0; i < L; ++i) {
+        for (int j = 0; j <= i; ++j) Lm[i * (i + 1) / 2 + j] = g[gv[i] * n + gv[j]];
+        y[i] = g[gv[i] * n + v];
+    }
+    const double cvv = g[v * n + v];
+    for (int j = 0; j < L; ++j) {
+        const int rj = j * (j + 1) / 2;
+        double s = Lm[rj + j];
+        for (int k = 0; k < j; ++k) s -= Lm[rj + k] * Lm[rj + k];
+        const double d = sqrt(s);
+        Lm[rj + j] = d;
+        const double inv = 1.0 / d;
+        for (int i = j + 1; i < L; ++i) {
+            const int ri = i * (i + 1) / 2;
+            double t = Lm[ri + j];
+            for (int k = 0; k < j; ++k) t -= Lm[ri + k] * Lm[rj + k];
+            Lm[ri + j] = t * inv;
+        }
+    }
+    double yy = 0.0;
+    for (int i = 0; i < L; ++i) {
+        const int ri = i * (i + 1) / 2;
+        double t = y[i];
+        for (int k = 0; k < i; ++k) t -= Lm[ri + k] * y[k];
+        t = t / Lm[ri + i];
+        y[i] = t;
+        yy += t * t;
+    }
+    const double rss = cvv - yy;
+    // BIC_OLS.cpp:366
+    const double the_score = a.N * log(rss / a.N) + a.lambda * log(a.N) * (double)L - 0.0;
+    const float ts = (float)the_score;
+    if (ts >= 0.0f) {
+        const float s = -ts;  // stored by the caller iff < 0 (score_calculator.cpp:111)
+        a.table[slot] = (s < 0.0f) ? s : absent_f();
+        return;
+    }
+    const float thr = -ts;
+    const uint64_t coff = a.tbl_off[(uint64_t)vi * a.S + L - 1];
+    bool dom = false;
+    {
+        uint64_t rem = cm;
+        while (rem) {
+            const uint64_t bit = rem & (0 - rem);
+            rem ^= bit;
+            dom |= a.table[coff + rank_colex64(cm ^ bit, a.binom)] >= thr;  // absent (NaN) never >= thr
+        }
+    }
+    if (dom) {
+        a.table[slot] = absent_f();
+        return;
+    }
+    const unsigned long long act = __ballot(1);
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)act) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(a.qcount, (unsigned long long)__popcll(act));
+    base = __shfl(base, leader);
+    const uint64_t pos = base + (uint64_t)__popcll(act & ((1ull << lane) - 1ull));
+    uint64_t *e = a.queue + 3 * pos;
+    e[0] = slot;
+    e[1] = cm;
+    e[2] = (uint64_t)(uint32_t)vi | ((uint64_t)fbits(ts) << 32);
+}
+
+// One lane per queued set: find_best_subset_score replayed step by step.  A
+// frame at depth d holds T, the parent vector (L - d entries; entries past the
+// filled ones are 0 = variable 0), the outer index idx, and while a
+// child list is being built the inner position i, the fill j and u.  The walk
+// stops at the first visited key >= -ts: that alone decides the store rule
+// (BIC_OLS.cpp:234 with best starting at 0 < -ts).
+template <int LMAX, int PHASE>
+__global__ void __launch_bounds__(64) walk_wide_kernel(WideArgs a, uint64_t qbase, uint64_t qn, uint64_t *bits,
+                                                       uint64_t wpl, unsigned long long *err) {
+    const uint64_t lid = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    const uint64_t qi = qbase + lid;
+    if (qi >= qn) return;
+    const uint64_t *e = a.queue + 3 * qi;
+    const uint64_t slot = e[0], cm = e[1];
+    const int vi = (int)(uint32_t)e[2];
+    const float ts = __uint_as_float((uint32_t)(e[2] >> 32));
+    const int L = a.L;
+    const bool z = a.meta[vi * 4 + 2] != 0;
+    uint8_t lc[LMAX + 1];  // local bit -> compact index
+    uint64_t Plocal;
+    {
+        uint64_t rem = cm;
+        const int first = PHASE == 0 ? 0 : 1;
+        lc[0] = 0;
+        for (int i = first; i < L + first; ++i) {
+            lc[i] = (uint8_t)__builtin_ctzll(rem);
+            rem &= rem - 1;
+        }
+        Plocal = PHASE == 0 ? ((1ull << L) - 1ull) : (((1ull << L) - 1ull) << 1);
+    }
+    const uint64_t *toffv = a.tbl_off + (uint64_t)vi * a.S;
+    uint64_t *chk = bits + lid * wpl;
+    chk[0] |= 1ull;  // checked.insert(empty_set)
+    const float thr = -ts;
+
+    uint64_t Ts[LMAX + 1];
+    uint8_t idxs[LMAX + 1], is[LMAX + 1], js[LMAX + 1], us[LMAX + 1], inner[LMAX + 1];
+    uint8_t pvs[LMAX * (LMAX + 1) / 2 + 1];
+    for (int i = 0; i < L; ++i) pvs[i] = (uint8_t)(i + (PHASE == 0 ? 0 : 1));
+    int d = 0;
+    Ts[0] = Plocal;
+    idxs[0] = 0;
+    inner[0] = 0;
+    bool dom = false;
+    uint64_t steps = 0;
+    while (true) {
+        if (++steps > kWideStepCap) {
+            atomicOr(err, 1ull);
+            break;
+        }
+        const int mm = L - d;
+        const int po = d * L - d * (d - 1) / 2;  // pvs offset of depth d
+        if (!inner[d]) {
+            if (idxs[d] == mm) {  // fb returns
+                if (d == 0) break;
+                --d;
+                const uint64_t c = Ts[d + 1];
+                chk[c >> 6] |= 1ull << (c & 63);  // checked.insert(thin_parents) after the call
+                continue;
+            }
+            const uint8_t u = pvs[po + idxs[d]];
+            const uint64_t T2 = Ts[d] ^ (1ull << u);
+            if ((chk[T2 >> 6] >> (T2 & 63)) & 1ull) {
+                ++idxs[d];
+                continue;
+            }
+            // is T2 in the cache as it stood when P was scored?
+            bool present = false;
+            const int pc = __popcll(T2);
+            if (pc < L || (PHASE == 1 && pc == L && (T2 & 1ull))) {
+                if (!(PHASE == 1 && (T2 & 1ull) && !z)) {
+                    uint64_t rk = 0, rem = T2;
+                    int j = 0;
+                    while (rem) {
+                        const int lb = __builtin_ctzll(rem);
+                        rem &= rem - 1;
+                        ++j;
+                        rk += B64(a.binom, lc[lb], j);
+                    }
+                    const float val = a.table[toffv[pc] + rk];
+                    if (fbits(val) != kAbsentBits) {
+                        present = true;
+                        if (val >= thr) {
+                            dom = true;
+                            break;
+                        }
+                    }
+                }
+            }
+            if (present) {
+                ++idxs[d];
+                continue;
+            }
+            inner[d] = 1;
+            is[d] = 0;
+            js[d] = 0;
+            us[d] = u;
+            for (int k = 0; k < mm - 1; ++k) pvs[po + mm + k] = 0;
+            continue;
+        }
+        if (is[d] == mm) {
+            inner[d] = 0;
+            ++idxs[d];
+            continue;
+        }
+        const uint8_t pi = pvs[po + is[d]];
+        ++is[d];
+        if (pi == us[d]) continue;
+        pvs[po + mm + js[d]] = pi;
+        ++js[d];
+        Ts[d + 1] = Ts[d] ^ (1ull << us[d]);
+        idxs[d + 1] = 0;
+        inner[d + 1] = 0;
+        ++d;
+    }
+    a.table[slot] = dom ? absent_f() : -ts;
+}
+
+using WideFn = void (*)(WideArgs);
+using WideWalkFn = void (*)(WideArgs, uint64_t, uint64_t, uint64_t *, uint64_t, unsigned long long *);
+WideFn wide_fn(int L, int phase) {
+    if (L <= 16) return phase == 0 ? score_wide_kernel<16, 0> : score_wide_kernel<16, 1>;
+    return phase == 0 ? score_wide_kernel<kWideMax, 0> : score_wide_kernel<kWideMax, 1>;
+}
+WideWalkFn wide_walk_fn(int L, int phase) {
+    if (L <= 16) return phase == 0 ? walk_wide_kernel<16, 0> : walk_wide_kernel<16, 1>;
+    return phase == 0 ? walk_wide_kernel<kWideMax, 0> : walk_wide_kernel<kWideMax, 1>;
+}
+
 __global__ void empty_set_kernel(const uint64_t *tbl_off, int nv, int S, float *table) {
     const int vi = blockIdx.x * blockDim.x + threadIdx.x;
     if (vi < nv) table[tbl_off[(uint64_t)vi * S]] = -0.0f;  // cache[empty] = -0.0f (BIC_OLS.cpp:249)
@@ -1142,6 +1428,7 @@ struct WriteArgs {
     const int *meta;
     const uint8_t *cand;
     const uint32_t *binom;
+    const uint64_t *binom64;  // wide layers (L > kMaxL)
     uint64_t total;
     int nv, S;
     uint64_t *sets;
@@ -1184,7 +1471,8 @@ __global__ void __launch_bounds__(kBlock) write_kernel(WriteArgs a) {
         }
         const int vi = lo / a.S, L = lo % a.S;
         const int m = a.meta[vi * 4 + 1];
-        const uint64_t cm = unrank_colex(s - a.tbl_off[lo], L, m, binom);
+        const uint64_t cm = L <= kMaxL ? unrank_colex(s - a.tbl_off[lo], L, m, binom)
+                                       : unrank_colex64(s - a.tbl_off[lo], L, m, a.binom64);
         uint64_t gs = 0;
         uint64_t rem = cm;
         while (rem) {
@@ -1310,6 +1598,57 @@ const char *kLayerNames[2][kMaxL + 1] = {
     {"", "score_layer_1_rest", "score_layer_2_rest", "score_layer_3_rest", "score_layer_4_rest",
      "score_layer_5_rest", "score_layer_6_rest", "score_layer_7_rest", "score_layer_8_rest"}};
 
+// One wide layer phase on stream st: the scoring launch, then (one sync for
+// the queue length) the walks, in chunks whose checked bitsets fit the budget.
+// `bits` is this stream group's own slice of c->d_wbits (`slice` words): the
+// groups' walks run concurrently on their own streams.
+int score_wide_layer(ulg_ctx *c, int L, int ph, hipStream_t st, const uint64_t *d_work, uint64_t cnt, int nv, int S,
+                     uint64_t *queue, unsigned long long *qc, unsigned long long *errf, uint64_t *bits,
+                     uint64_t slice) {
+    WideArgs wa;
+    wa.gram = c->gram.p;
+    wa.binom = c->d_binom64.p;
+    wa.cand = c->d_cand.p;
+    wa.meta = c->d_meta.p;
+    wa.tbl_off = c->d_tbl_off.p;
+    wa.work = d_work;
+    wa.table = c->table.p;
+    wa.queue = queue;
+    wa.qcount = qc;
+    wa.N = (double)c->N;
+    wa.lambda = c->lambda;
+    wa.n = c->n;
+    wa.nv = nv;
+    wa.S = S;
+    wa.L = L;
+    const uint64_t blocks = (cnt + kBlock - 1) / kBlock;
+    const WideFn sf = wide_fn(L, ph);
+    const int lds = c->n * c->n * 8;
+    if (lds > 64 * 1024) ULG_HIP(c, hipFuncSetAttribute((const void *)sf, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    prof_begin_s(c, ph == 0 ? "score_wide_var0" : "score_wide_rest", st);
+    hipLaunchKernelGGL(sf, dim3((unsigned)blocks), dim3(kBlock), (size_t)lds, st, wa);
+    prof_end_s(c, st);
+    ULG_HIP(c, hipGetLastError());
+    unsigned long long qn = 0;
+    ULG_HIP(c, hipMemcpyAsync(&qn, qc, 8, hipMemcpyDeviceToHost, st));
+    ULG_HIP(c, hipStreamSynchronize(st));
+    if (qn == 0) return ULG_OK;
+    // checked bitset: 2^q bits per walking set, q = L (P holds variable 0) or L + 1
+    const int q = ph == 0 ? L : L + 1;
+    const uint64_t wpl = q <= 6 ? 1ull : (1ull << (q - 6));
+    const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(qn, slice / wpl));  // slice >= wpl
+    const WideWalkFn wf = wide_walk_fn(L, ph);
+    for (uint64_t base = 0; base < qn; base += per) {
+        const uint64_t k = std::min<uint64_t>(per, qn - base);
+        ULG_HIP(c, hipMemsetAsync(bits, 0, (size_t)(k * wpl * 8), st));
+        prof_begin_s(c, ph == 0 ? "walk_wide_var0" : "walk_wide_rest", st);
+        hipLaunchKernelGGL(wf, dim3((unsigned)((k + 63) / 64)), dim3(64), 0, st, wa, base, base + k, bits, wpl, errf);
+        prof_end_s(c, st);
+        ULG_HIP(c, hipGetLastError());
+    }
+    return ULG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1393,9 +1732,9 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
         meta[i * 4 + 2] = (C & 1ull) ? 1 : 0;  // variable 0 is a candidate (compact index 0)
         kmax = std::max(kmax, std::min(m, max_parents));
     }
-    if (kmax > kMaxL)
+    if (kmax > kWideMax)
         return set_err(c, ULG_ERR_UNSUPPORTED,
-                       "ulg_cbic_score: parent sets larger than ULG_MAX_PARENTS_GPU (8) are not supported");
+                       "ulg_cbic_score: parent sets larger than ULG_MAX_PARENTS_GPU (31) are not supported");
     const int S = kmax + 1;
     // slab offsets: (vi, L) -> start, final sentinel = total slots
     std::vector<uint64_t> toff((size_t)nv * S + 1);
@@ -1497,16 +1836,30 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     }
     const uint64_t *d_wk = G > 1 ? c->d_workg.p : c->d_work.p;
     const std::vector<uint64_t> &h_wk = G > 1 ? workg : work;
-    uint64_t qwords = 0;  // per group: every lane of its largest launch may be queued
-    if (variant & 16) {
-        for (int g = 0; g < G; ++g)
-            for (int L = 1; L <= kmax; ++L)
-                for (int ph = 0; ph < 2; ++ph)
-                    qwords = std::max<uint64_t>(qwords, h_wk[(size_t)g * wstride + ((size_t)L * 2 + ph) * (nv + 1) + nv] *
-                                                            (uint64_t)(1 + 2 * bits_words(L)));
-        if ((rc = ensure(c, c->d_queue, (size_t)G * qwords)) || (rc = ensure(c, c->d_qcount, (size_t)G * 2 * (kmax + 1))))
+    uint64_t qwords = 0;   // per group: every lane of its largest launch may be queued
+    uint64_t wqwords = 0;  // the same for the wide layers' queue (3 words per set)
+    for (int g = 0; g < G; ++g)
+        for (int L = 1; L <= kmax; ++L)
+            for (int ph = 0; ph < 2; ++ph) {
+                const uint64_t cnt = h_wk[(size_t)g * (G > 1 ? wstride : 0) + ((size_t)L * 2 + ph) * (nv + 1) + nv];
+                if (L > kMaxL) wqwords = std::max<uint64_t>(wqwords, 3 * cnt);
+                else if (variant & 16) qwords = std::max<uint64_t>(qwords, cnt * (uint64_t)(1 + 2 * bits_words(L)));
+            }
+    // queue counters per (group, layer, phase), then the wide walks' error flag
+    const size_t nqc = (size_t)G * 2 * (kmax + 1) + 1;
+    if ((variant & 16) || kmax > kMaxL) {
+        if ((rc = ensure(c, c->d_queue, (size_t)G * qwords)) || (rc = ensure(c, c->d_qcount, nqc)) ||
+            (rc = ensure(c, c->d_wqueue, (size_t)G * wqwords)))
             return rc;
-        ULG_HIP(c, hipMemsetAsync(c->d_qcount.p, 0, sizeof(unsigned long long) * G * 2 * (kmax + 1), c->stream));
+        ULG_HIP(c, hipMemsetAsync(c->d_qcount.p, 0, sizeof(unsigned long long) * nqc, c->stream));
+    }
+    // wide-layer walks: one checked-bitset slice per stream group, allocated
+    // before any launch (2^q bits per walking set, q <= kmax + 1)
+    uint64_t wslice = 0;
+    if (kmax > kMaxL) {
+        const uint64_t wpl_max = kmax + 1 <= 6 ? 1ull : (1ull << (kmax + 1 - 6));
+        wslice = std::max<uint64_t>(kWideBitsWords / (uint64_t)G, wpl_max);
+        if ((rc = ensure(c, c->d_wbits, (size_t)(G * wslice)))) return rc;
     }
     // fork: the side streams start after the uploads / empty-set kernel
     if (G > 1) {
@@ -1526,6 +1879,14 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
                 sa.qcount = qc;
                 const uint64_t blocks = (cnt + kBlock - 1) / kBlock;
                 if (blocks > 0x7fffffffull) return set_err(c, ULG_ERR_UNSUPPORTED, "ulg_cbic_score: layer too large");
+                if (L > kMaxL) {
+                    if ((rc = score_wide_layer(c, L, ph, st, d_wk + wo, cnt, nv, S, c->d_wqueue.p + g * wqwords,
+                                               c->d_qcount.p + (size_t)g * 2 * (kmax + 1) + (L * 2 + ph),
+                                               c->d_qcount.p + nqc - 1, c->d_wbits.p + (size_t)g * wslice,
+                                               wslice)))
+                        return rc;
+                    continue;
+                }
                 const LdsLayout lay = lds_layout(n, nv, S, L, variant);
                 const KernelFn kfn = layer_kernel(L, ph, variant);
                 if (lay.total > 64 * 1024)
@@ -1639,6 +2000,7 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     wa.meta = c->d_meta.p;
     wa.cand = c->d_cand.p;
     wa.binom = c->d_binom.p;
+    wa.binom64 = c->d_binom64.p;
     wa.total = total_slots;
     wa.nv = nv;
     wa.S = S;
@@ -1651,9 +2013,14 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     set_total_kernel<<<1, 1, 0, c->stream>>>(c->d_blk.p, nb, nv, c->out_offsets.p);
     ULG_HIP(c, hipGetLastError());
     uint64_t stored = 0;
+    unsigned long long wide_err = 0;
     ULG_HIP(c, hipMemcpyAsync(&stored, c->d_blk.p + nb, 8, hipMemcpyDeviceToHost, c->stream));
+    if (kmax > kMaxL) ULG_HIP(c, hipMemcpyAsync(&wide_err, c->d_qcount.p + nqc - 1, 8, hipMemcpyDeviceToHost, c->stream));
     ULG_HIP(c, hipStreamSynchronize(c->stream));
     prof_collect(c);
+    if (wide_err)
+        return set_err(c, ULG_ERR_UNSUPPORTED,
+                       "ulg_cbic_score: a find_best_subset_score walk exceeded 2^30 steps in a wide layer");
 
     c->nv = nv;
     c->kmax = kmax;

@@ -24,6 +24,16 @@ const std::vector<uint32_t> &host_binom() {
     return t;
 }
 
+const std::vector<uint64_t> &host_binom64() {
+    static std::vector<uint64_t> t = [] {
+        std::vector<uint64_t> b(64 * 64, 0);
+        for (int a = 0; a < 64; ++a)
+            for (int k = 0; k < 64; ++k) b[a * 64 + k] = binom64(a, k);
+        return b;
+    }();
+    return t;
+}
+
 uint64_t binom64(int a, int b) {
     if (b < 0 || b > a) return 0;
     if (b > a - b) b = a - b;
@@ -97,7 +107,10 @@ int ulg_create(const int *device_ids, int ndev, ulg_ctx **out) {
     }
     const auto &b = host_binom();
     if (ensure(c, c->d_binom, b.size()) != ULG_OK ||
-        hipMemcpy(c->d_binom.p, b.data(), b.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(c->d_binom.p, b.data(), b.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess ||
+        ensure(c, c->d_binom64, host_binom64().size()) != ULG_OK ||
+        hipMemcpy(c->d_binom64.p, host_binom64().data(), host_binom64().size() * sizeof(uint64_t),
+                  hipMemcpyHostToDevice) != hipSuccess) {
         delete c;
         return ULG_ERR_HIP;
     }
@@ -118,7 +131,7 @@ void ulg_destroy(ulg_ctx *c) {
     c->sync_events.clear();
     release(c->raw); release(c->z); release(c->gram); release(c->partials); release(c->colstat);
     release(c->table); release(c->d_tbl_off); release(c->d_work); release(c->d_blk);
-    release(c->d_cand); release(c->d_meta); release(c->d_binom); release(c->d_stats); release(c->d_dump); release(c->d_queue); release(c->d_qcount); release(c->d_workg);
+    release(c->d_cand); release(c->d_meta); release(c->d_binom); release(c->d_binom64); release(c->d_wqueue); release(c->d_wbits); release(c->d_stats); release(c->d_dump); release(c->d_queue); release(c->d_qcount); release(c->d_workg);
     release(c->out_sets); release(c->out_scores); release(c->out_offsets);
     release(c->qbuf_in); release(c->qbuf_out);
     pss_release(c);

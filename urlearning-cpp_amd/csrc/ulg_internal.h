@@ -15,7 +15,8 @@
 namespace ulg {
 
 constexpr int kMaxVars = 63;               // varset = uint64, bit 63 kept free
-constexpr int kMaxL = ULG_MAX_PARENTS_GPU;  // unrolled layers on the device
+constexpr int kMaxL = ULG_UNROLLED_PARENTS_GPU;  // unrolled layers on the device
+constexpr int kWideMax = ULG_MAX_PARENTS_GPU;   // wide layers kMaxL+1 .. kWideMax (cbic.hip)
 constexpr int kBinomK = kMaxL + 2;          // binomial table columns C(a, 0..kBinomK-1)
 constexpr uint32_t kAbsentBits = 0xFFFFFFFFu;  // "not in the FloatMap" sentinel (a NaN payload)
 
@@ -76,6 +77,9 @@ struct ulg_ctx {
     ulg::DevBuf<uint8_t> d_cand;  // [nv][64] compact index -> variable
     ulg::DevBuf<int> d_meta;      // [nv][4]: var, m, var0in, pad
     ulg::DevBuf<uint32_t> d_binom;
+    ulg::DevBuf<uint64_t> d_binom64;              // [64][64] unclamped C(a, b) for the wide layers
+    ulg::DevBuf<uint64_t> d_wqueue;               // wide layers: sets left for the walk
+    ulg::DevBuf<uint64_t> d_wbits;                // wide layers: per-walk checked bitsets
     ulg::DevBuf<unsigned long long> d_stats;  // score_variant 13 statistics
     ulg::DevBuf<uint64_t> d_dump;
     ulg::DevBuf<uint64_t> d_queue;                // score_variant bit 4: undecided lanes
@@ -160,6 +164,8 @@ void pss_release(ulg_ctx *c);    // pss.hip
 
 // binomial table C(a, b), a < 64, b < kBinomK, clamped to uint32
 const std::vector<uint32_t> &host_binom();
+// C(a, b) for a, b < 64 (saturating at 2^64 - 1), [a * 64 + b]
+const std::vector<uint64_t> &host_binom64();
 uint64_t binom64(int a, int b);
 
 }  // namespace ulg
