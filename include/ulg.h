@@ -198,6 +198,28 @@ int ulg_astar_scc(ulg_ctx *ctx, const uint64_t *edges, int pd_count, int mode,
 int ulg_triplet_astar(ulg_ctx *ctx, const uint64_t *edges, int pd_count,
                       int *directed_graph, int64_t *stats);
 
+/* Multi-GPU triplet_astar (distinct clusters are independent A*
+ * problems).  The per-cluster results live in a memo on the context, valid
+ * for the loaded lists and one pd_count; ulg_triplet_astar reads and fills
+ * it, so its stats count only the searches that call made.
+ *   ulg_triplet_clusters: the distinct clusters (<= 26 variables) of the
+ *     driver's first sweep on the initial skeleton (triplet_astar.cpp:
+ *     1148-1204), in first-request order, no searching; *count = how many
+ *     (fails with ULG_ERR_ARG if cap is too small and nonzero).
+ *   ulg_triplet_solve: the re-opening exact-order A* (:285-674) of each
+ *     cluster into the memo; parents (optional, nc*n) receives each cluster
+ *     DAG's parent sets.  stats as ulg_triplet_astar.
+ *   ulg_triplet_memo_put: seed the memo with other ranks' results.
+ * Sharded over ranks, the clusters are solved once each and gathered; every
+ * rank then runs ulg_triplet_astar with a full memo and gets the same MEC a
+ * single GPU would (a result depends on its cluster only). */
+int ulg_triplet_clusters(ulg_ctx *ctx, const uint64_t *edges, uint64_t *clusters,
+                         int64_t cap, int64_t *count);
+int ulg_triplet_solve(ulg_ctx *ctx, const uint64_t *clusters, int64_t nc,
+                      int pd_count, uint64_t *parents, int64_t *stats);
+int ulg_triplet_memo_put(ulg_ctx *ctx, const uint64_t *clusters, int64_t nc,
+                         int pd_count, const uint64_t *parents);
+
 /* ---- tuning knobs -------------------------------------------------------
  * "score_variant" (0..7, 13, 16, 17; default 17): bit 0 = fully unrolled
  * presence gather in the scorer (layers <= 6), bit 1 = stack-machine

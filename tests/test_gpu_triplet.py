@@ -103,3 +103,98 @@ def test_cluster_pattern_databases_match_oracle(ulg_ctx, oracle_built):
             eh, ec = srch.pdb_h(S)
             assert np.float32(hv).tobytes() == np.float32(eh).tobytes(), (scc, S)
             assert int(cv) == ec
+
+
+def _sharded_worker(rank, world, port, result_dir, seed, n, extra):
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "urlearning-cpp_amd"))
+    import torch.distributed as dist
+    import shard
+    import synth as sy
+    import ulg as u
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    X, W = sy.gaussian_sem(n, 3000, seed)
+    rows = [r & ~(1 << i) for i, r in enumerate(sy.true_skeleton_edges(W, extra, seed))]
+    ctx = u.Context(0)
+    ctx.load(X, 2.0)
+    ctx.score(list(range(n)), u.candidates_from_edges(rows, n), 4)
+    ctx.search_from_scores()
+    res = shard.triplet_sharded(ctx, rows, world, rank)
+    np.savez(os.path.join(result_dir, f"t{rank}.npz"), mec=res["mec"],
+             st=np.array([res["runs"], res["distinct"], res["solved_here"], res["clusters"]]))
+    ctx.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("seed,n,extra", [(9410, 16, 0.1), (9411, 20, 0.15)])
+def test_triplet_sharded_over_two_ranks_equals_one_gpu(ulg_ctx, tmp_path, seed, n, extra):
+    """the first sweep's clusters solved once each over 2 ranks
+    (one libulg context per rank, gloo exchange), then the driver on every
+    rank: the MEC equals the single-GPU driver's, and the driver searches
+    only what the exchange did not cover."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    world = 2
+    mp.start_processes(_sharded_worker, args=(world, port, str(tmp_path), seed, n, extra), nprocs=world,
+                       join=True, start_method="spawn")
+    X, W = synth.gaussian_sem(n, 3000, seed)
+    rows = [r & ~(1 << i) for i, r in enumerate(synth.true_skeleton_edges(W, extra, seed))]
+    ulg_ctx.load(X, 2.0)
+    ulg_ctx.score(list(range(n)), ulg.candidates_from_edges(rows, n), 4)
+    ulg_ctx.search_from_scores()
+    one = ulg_ctx.triplet(edges=rows)
+    clusters = ulg_ctx.triplet_clusters(rows)
+    assert len(clusters) > world
+    solved = 0
+    for r in range(world):
+        d = np.load(tmp_path / f"t{r}.npz")
+        assert d["mec"].tolist() == one["mec"].tolist()
+        runs, distinct, here, ncl = (int(x) for x in d["st"])
+        assert runs == one["runs"] and ncl == len(clusters)
+        assert distinct <= one["distinct"]
+        solved += here
+    assert solved == len(clusters)
+
+
+def test_triplet_memo_reuse_and_put(ulg_ctx):
+    """A memo seeded by ulg_triplet_memo_put (here: from a second context)
+    leaves the driver nothing to search for those clusters, same MEC."""
+    n = 14
+    X, W = synth.gaussian_sem(n, 3000, 9412)
+    rows = [r & ~(1 << i) for i, r in enumerate(synth.true_skeleton_edges(W, 0.1, 9412))]
+    ulg_ctx.load(X, 2.0)
+    ulg_ctx.score(list(range(n)), ulg.candidates_from_edges(rows, n), 4)
+    ulg_ctx.search_from_scores()
+    one = ulg_ctx.triplet(edges=rows)
+    again = ulg_ctx.triplet(edges=rows)  # same lists: the context's memo answers every run
+    assert again["mec"].tolist() == one["mec"].tolist() and again["distinct"] == 0 and again["expanded"] == 0
+    clusters = ulg_ctx.triplet_clusters(rows)
+    par, st = ulg_ctx.triplet_solve(clusters)
+    # the driver asked for some of them (orientations grow clusters mid-sweep,
+    # so not necessarily all): only the rest are searched, and only once
+    assert st["distinct"] < len(clusters)
+    par2, st2 = ulg_ctx.triplet_solve(clusters)
+    assert st2["distinct"] == 0 and np.array_equal(par2, par)
+    other = ulg.Context(0)
+    try:
+        other.load(X, 2.0)
+        other.score(list(range(n)), ulg.candidates_from_edges(rows, n), 4)
+        other.search_from_scores()
+        p2, st2 = other.triplet_solve(clusters)
+        assert np.array_equal(p2, par) and st2["distinct"] == len(set(int(c) for c in clusters))
+        other.search_from_scores()  # new lists: memo cleared
+        other.triplet_memo_put(clusters, par)
+        res = other.triplet(edges=rows)
+        assert res["mec"].tolist() == one["mec"].tolist()
+        assert res["distinct"] == one["distinct"] - (len(clusters) - st["distinct"])
+    finally:
+        other.close()

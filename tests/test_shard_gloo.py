@@ -71,3 +71,53 @@ def test_stripe_is_a_partition():
         for ws in (1, 2, 4, 8):
             parts = [shard.stripe(n, ws, r) for r in range(ws)]
             assert sorted(v for p in parts for v in p) == list(range(n))
+
+
+def test_assign_clusters_is_a_balanced_deterministic_partition():
+    sys.path.insert(0, os.path.join(ROOT, "urlearning-cpp_amd"))
+    import shard
+    rng = np.random.default_rng(9600)
+    clusters = np.array([int(x) for x in rng.integers(1, 1 << 20, size=57)], dtype=np.uint64)
+    for ws in (1, 2, 3, 8):
+        own = shard.assign_clusters(clusters, ws)
+        assert np.array_equal(own, shard.assign_clusters(clusters, ws))
+        assert set(own.tolist()) <= set(range(ws))
+        loads = [sum(1 << bin(int(c)).count("1") for c, o in zip(clusters, own) if o == r) for r in range(ws)]
+        biggest = max(1 << bin(int(c)).count("1") for c in clusters)
+        assert max(loads) - min(loads) <= biggest  # LPT: within one job of each other
+
+
+def _memo_worker(rank, world, port, result_dir):
+    """Each rank contributes the memo rows of the clusters it owns; after the
+    one all-gather every rank holds every row (the exchange of
+    shard.triplet_sharded, with a stand-in per-cluster result)."""
+    sys.path.insert(0, os.path.join(ROOT, "urlearning-cpp_amd"))
+    import torch.distributed as dist
+    import shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 13
+    rng = np.random.default_rng(9601)
+    clusters = np.unique(rng.integers(1, 1 << n, size=40).astype(np.uint64))
+    own = shard.assign_clusters(clusters, world)
+    mine = clusters[own == rank]
+    parents = np.array([[(int(c) * 2654435761 + v) & ((1 << n) - 1) for v in range(n)] for c in mine],
+                       dtype=np.uint64).reshape(len(mine), n)
+    cl, pa = shard.unpack_memo(shard.allgather_rows(shard.pack_memo(mine, parents, n), world))
+    np.savez(os.path.join(result_dir, f"m{rank}.npz"), cl=cl, pa=pa, all=clusters)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_triplet_memo_exchange_complete_on_every_rank(tmp_path, world):
+    mp.start_processes(_memo_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    n = 13
+    for r in range(world):
+        d = np.load(tmp_path / f"m{r}.npz")
+        order = np.argsort(d["cl"])
+        assert np.array_equal(d["cl"][order], np.sort(d["all"]))
+        for c, row in zip(d["cl"], d["pa"]):
+            assert [int(x) for x in row] == [(int(c) * 2654435761 + v) & ((1 << n) - 1) for v in range(n)]

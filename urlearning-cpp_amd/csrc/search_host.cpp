@@ -165,6 +165,7 @@ int lists_loaded(ulg_ctx *c) {
     s.tables_ready = false;
     s.pdb_ready = false;
     s.host_costs_ready = false;
+    s.triplet_memo.clear();
     const int rc = search_build_tables(c, all_vars(s.n));
     if (rc == ULG_ERR_UNSUPPORTED) {
         c->err.clear();

@@ -4,6 +4,7 @@
 
 #include <cfloat>
 #include <cstdint>
+#include <unordered_map>
 #include <vector>
 
 #include "ulg_internal.h"
@@ -179,6 +180,11 @@ struct SearchState {
     DevBuf<int> d_bitpos;
     DevBuf<uint64_t> d_groups;
     bool pdb_ready = false;
+    // triplet_astar's per-cluster A* results (cluster -> optimal parent set
+    // per variable), valid for these lists and triplet_pd; filled by the
+    // driver, by ulg_triplet_solve and by ulg_triplet_memo_put (other ranks)
+    std::unordered_map<uint64_t, std::vector<uint64_t>> triplet_memo;
+    int triplet_pd = 0;
     // query scratch
     DevBuf<int> q_vars;
     DevBuf<uint64_t> q_sets, q_par;

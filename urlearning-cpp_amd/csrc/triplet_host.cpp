@@ -14,6 +14,9 @@
 // The orientation state is held as bit rows: out[i] bit j == directed_graph
 // [i][j].  Both directions set = undirected edge.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <unordered_map>
 #include <unordered_set>
@@ -35,7 +38,7 @@ struct Triplet {
     int n = 0, pd_count = 2;
     uint64_t nb[64] = {}, clusters[64] = {}, vstr[64] = {}, out[64] = {};
     std::unordered_set<uint64_t> checked;
-    std::unordered_map<uint64_t, std::vector<uint64_t>> memo;  // cluster -> optimal parents
+    std::unordered_map<uint64_t, std::vector<uint64_t>> *memo = nullptr;  // SearchState::triplet_memo
     int64_t runs = 0, distinct = 0, expanded = 0;
     int num_v_structures = 0;
     bool hang = false;
@@ -151,12 +154,40 @@ int cluster_astar(Triplet &t, uint64_t cluster, std::vector<uint64_t> &op) {
 
 const std::vector<uint64_t> *cluster_parents(Triplet &t, uint64_t cluster) {
     ++t.runs;
-    auto it = t.memo.find(cluster);
-    if (it != t.memo.end()) return &it->second;
+    auto it = t.memo->find(cluster);
+    if (it != t.memo->end()) return &it->second;
     std::vector<uint64_t> op;
+    static const bool trace = std::getenv("ULG_TRIPLET_TRACE") != nullptr;  // per-search progress on stderr
+    const int64_t e0 = t.expanded;
+    const auto c0 = std::chrono::steady_clock::now();
     if ((t.rc = cluster_astar(t, cluster, op))) return nullptr;
+    if (trace)
+        std::fprintf(stderr, "triplet: cluster %016llx (%d variables): %lld expansions in %.3f s\n",
+                     (unsigned long long)cluster, __builtin_popcountll(cluster), (long long)(t.expanded - e0),
+                     std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count());
     ++t.distinct;
-    return &t.memo.emplace(cluster, std::move(op)).first->second;
+    return &t.memo->emplace(cluster, std::move(op)).first->second;
+}
+
+// The context's memo for pd_count (a different pattern-database split gives
+// the same optimal cost but possibly another tied DAG: start over).
+std::unordered_map<uint64_t, std::vector<uint64_t>> *memo_for(SearchState &s, int pd_count) {
+    if (s.triplet_pd != pd_count) {
+        s.triplet_memo.clear();
+        s.triplet_pd = pd_count;
+    }
+    return &s.triplet_memo;
+}
+
+void init_skeleton(Triplet &t, const uint64_t *edges) {
+    const int n = t.n;
+    const uint64_t all = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+    // Skeleton::get_neighbors: the file's rows, or every variable (self
+    // included) without a skeleton; clusters add the variable itself (:1061-1072)
+    for (int v = 0; v < n; ++v) {
+        t.nb[v] = edges ? edges[v] : all;
+        t.clusters[v] = t.nb[v] | (1ull << v);
+    }
 }
 
 // process_triple (triplet_astar.cpp:811-989)
@@ -277,13 +308,8 @@ extern "C" int ulg_triplet_astar(ulg_ctx *c, const uint64_t *edges, int pd_count
     t.s = &s;
     t.n = n;
     t.pd_count = pd_count;
-    const uint64_t all = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
-    // Skeleton::get_neighbors: the file's rows, or every variable (self
-    // included) without a skeleton; clusters add the variable itself (:1061-1072)
-    for (int v = 0; v < n; ++v) {
-        t.nb[v] = edges ? edges[v] : all;
-        t.clusters[v] = t.nb[v] | (1ull << v);
-    }
+    t.memo = memo_for(s, pd_count);
+    init_skeleton(t, edges);
     for (int i = 0; i < n && !t.rc; ++i) {
         const uint64_t pin = t.nb[i];
         std::vector<int> unc;
@@ -333,5 +359,83 @@ extern "C" int ulg_triplet_astar(ulg_ctx *c, const uint64_t *edges, int pd_count
         stats[2] = t.expanded;
     }
     if (t.hang) return set_err(c, ULG_ERR_STATE, "ulg_triplet_astar: the reference heap's __down_heap would not terminate here");
+    return ULG_OK;
+}
+
+// The distinct clusters the driver's first sweep (triplet_astar.cpp:1148-1204)
+// asks A* for on the initial skeleton, in first-request order, without the
+// searches themselves: triples of a variable and two of its neighbours whose
+// cluster union has at most 26 variables.  Orientations found during the
+// sweep can add skeleton edges (and so clusters) that this list lacks; the
+// driver searches those itself.  Used to shard the searches over ranks.
+extern "C" int ulg_triplet_clusters(ulg_ctx *c, const uint64_t *edges, uint64_t *clusters, int64_t cap,
+                                    int64_t *count) {
+    if (!c || !count || (cap > 0 && !clusters)) return ULG_ERR_ARG;
+    if (!c->search || !c->search->lists_ready)
+        return set_err(c, ULG_ERR_STATE, "ulg_triplet_clusters: no parent-set lists");
+    Triplet t;
+    t.n = c->search->n;
+    init_skeleton(t, edges);
+    std::unordered_set<uint64_t> seen;
+    int64_t k = 0;
+    for (int i = 0; i < t.n; ++i) {
+        std::vector<int> unc;
+        for (int j = 0; j < t.n; ++j)
+            if (bit(t.nb[i], j)) unc.push_back(j);
+        for (size_t j = 0; j < unc.size(); ++j)
+            for (size_t q = 0; q < j; ++q) {
+                const uint64_t big = t.clusters[i] | t.clusters[unc[j]] | t.clusters[unc[q]];
+                if (__builtin_popcountll(big) > kMaxCluster || !seen.insert(big).second) continue;
+                if (k < cap) clusters[k] = big;
+                ++k;
+            }
+    }
+    *count = k;
+    return k > cap && cap > 0 ? set_err(c, ULG_ERR_ARG, "ulg_triplet_clusters: cap too small") : ULG_OK;
+}
+
+// One re-opening exact-order A* per cluster (clusters already in the memo
+// are not searched again); parents[i * n + v] = v's optimal parent set in
+// cluster i's DAG.  Results enter the memo ulg_triplet_astar reads.
+extern "C" int ulg_triplet_solve(ulg_ctx *c, const uint64_t *clusters, int64_t nc, int pd_count, uint64_t *parents,
+                                 int64_t *stats) {
+    if (!c || nc < 0 || (nc > 0 && !clusters) || pd_count < 1) return ULG_ERR_ARG;
+    if (!c->search || !c->search->lists_ready)
+        return set_err(c, ULG_ERR_STATE, "ulg_triplet_solve: no parent-set lists");
+    ULG_HIP(c, hipSetDevice(c->device));
+    SearchState &s = *c->search;
+    Triplet t;
+    t.c = c;
+    t.s = &s;
+    t.n = s.n;
+    t.pd_count = pd_count;
+    t.memo = memo_for(s, pd_count);
+    const uint64_t all = (t.n >= 64) ? ~0ull : ((1ull << t.n) - 1ull);
+    for (int64_t i = 0; i < nc; ++i) {
+        if ((clusters[i] & ~all) || __builtin_popcountll(clusters[i]) > kMaxCluster)
+            return set_err(c, ULG_ERR_ARG, "ulg_triplet_solve: cluster outside the variables or above 26 variables");
+        const std::vector<uint64_t> *op = cluster_parents(t, clusters[i]);
+        if (!op) return t.rc;
+        if (parents) std::memcpy(parents + i * t.n, op->data(), sizeof(uint64_t) * t.n);
+    }
+    if (stats) {
+        stats[0] = t.runs;
+        stats[1] = t.distinct;
+        stats[2] = t.expanded;
+    }
+    if (t.hang) return set_err(c, ULG_ERR_STATE, "ulg_triplet_solve: the reference heap's __down_heap would not terminate here");
+    return ULG_OK;
+}
+
+// Seed the memo with other ranks' results (same lists, same pd_count).
+extern "C" int ulg_triplet_memo_put(ulg_ctx *c, const uint64_t *clusters, int64_t nc, int pd_count,
+                                    const uint64_t *parents) {
+    if (!c || nc < 0 || (nc > 0 && (!clusters || !parents)) || pd_count < 1) return ULG_ERR_ARG;
+    if (!c->search || !c->search->lists_ready)
+        return set_err(c, ULG_ERR_STATE, "ulg_triplet_memo_put: no parent-set lists");
+    SearchState &s = *c->search;
+    auto *memo = memo_for(s, pd_count);
+    for (int64_t i = 0; i < nc; ++i)
+        (*memo)[clusters[i]] = std::vector<uint64_t>(parents + i * s.n, parents + (i + 1) * s.n);
     return ULG_OK;
 }

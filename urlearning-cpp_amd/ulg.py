@@ -49,6 +49,9 @@ def lib():
         L.ulg_pdb_query.argtypes = [P, I64, P, P, P]
         L.ulg_astar.argtypes = [P, P, I, I, P, P, C.POINTER(F), C.POINTER(I64), C.c_char_p, I64]
         L.ulg_triplet_astar.argtypes = [P, P, I, P, P]
+        L.ulg_triplet_clusters.argtypes = [P, P, P, I64, C.POINTER(I64)]
+        L.ulg_triplet_solve.argtypes = [P, P, I64, I, P, P]
+        L.ulg_triplet_memo_put.argtypes = [P, P, I64, I, P]
         L.ulg_mmpc.argtypes = [P, D, I, P]
         L.ulg_pss_format.argtypes = [P, C.c_char_p, P, P, C.POINTER(C.c_void_p), C.POINTER(I64)]
         L.ulg_pss_format_lists.argtypes = [P, I, P, P, P, C.c_char_p, P, P, C.POINTER(C.c_void_p), C.POINTER(I64)]
@@ -254,6 +257,33 @@ class Context:
         self._check(lib().ulg_triplet_astar(self._h, _ptr(e) if e is not None else None, int(pd_count), _ptr(dg),
                                             _ptr(stats)), "ulg_triplet_astar")
         return {"mec": dg.reshape(n, n), "runs": int(stats[0]), "distinct": int(stats[1]), "expanded": int(stats[2])}
+
+    def triplet_clusters(self, edges=None):
+        """ulg_triplet_clusters -> uint64 array of the first sweep's distinct clusters."""
+        e = None if edges is None else np.ascontiguousarray([int(x) for x in edges], dtype=np.uint64)
+        cnt = C.c_int64()
+        self._check(lib().ulg_triplet_clusters(self._h, _ptr(e) if e is not None else None, None, 0,
+                                               C.byref(cnt)), "ulg_triplet_clusters")
+        out = np.zeros(max(cnt.value, 1), dtype=np.uint64)
+        self._check(lib().ulg_triplet_clusters(self._h, _ptr(e) if e is not None else None, _ptr(out), len(out),
+                                               C.byref(cnt)), "ulg_triplet_clusters")
+        return out[:cnt.value]
+
+    def triplet_solve(self, clusters, pd_count=2):
+        """ulg_triplet_solve -> (parents [nc, n] uint64, {"runs", "distinct", "expanded"})."""
+        cl = np.ascontiguousarray(clusters, dtype=np.uint64)
+        par = np.zeros((max(len(cl), 1), self.search_n), dtype=np.uint64)
+        stats = np.zeros(3, dtype=np.int64)
+        self._check(lib().ulg_triplet_solve(self._h, _ptr(cl), len(cl), int(pd_count), _ptr(par), _ptr(stats)),
+                    "ulg_triplet_solve")
+        return par[:len(cl)], {"runs": int(stats[0]), "distinct": int(stats[1]), "expanded": int(stats[2])}
+
+    def triplet_memo_put(self, clusters, parents, pd_count=2):
+        cl = np.ascontiguousarray(clusters, dtype=np.uint64)
+        par = np.ascontiguousarray(parents, dtype=np.uint64).reshape(len(cl), self.search_n) if len(cl) else \
+            np.zeros((1, self.search_n), dtype=np.uint64)
+        self._check(lib().ulg_triplet_memo_put(self._h, _ptr(cl), len(cl), int(pd_count), _ptr(par)),
+                    "ulg_triplet_memo_put")
 
     def set_option(self, name: str, value: int):
         self._check(lib().ulg_set_option(self._h, name.encode(), int(value)), "ulg_set_option")
