@@ -235,6 +235,10 @@ int ulg_triplet_memo_put(ulg_ctx *ctx, const uint64_t *clusters, int64_t nc,
  * searched with tables built per skeleton component / triplet cluster, and
  * lookups outside the current tables scan the lists on the device -- same
  * answers, less memory.
+ * "score_streams" (1..4, default 3): variable groups scored on concurrent
+ * streams; "score_small_layers" (0..8, default 4): layers up to this size run
+ * one one-pass launch per phase over all variables on one stream (they are
+ * latency-bound), larger ones the two-pass form per group.
  * All variants compute identical results; the knob exists for A/B timing. */
 int ulg_set_option(ulg_ctx *ctx, const char *name, int64_t value);
 

@@ -1373,25 +1373,44 @@ __global__ void empty_set_kernel(const uint64_t *tbl_off, int nv, int S, float *
 }
 
 // ---- compaction of the slabs into (set, score) lists ------------------------
-constexpr int kSlotsPerThread = 4;
+constexpr int kSlotsPerThread = 16;  // contiguous slots per thread (four 16-B loads)
 constexpr int kSlotsPerBlock = kBlock * kSlotsPerThread;
 
+// the thread's kSlotsPerThread slots from `base` (absent past the end)
+__device__ __forceinline__ void load_slots(const float *table, uint64_t total, uint64_t base,
+                                           float (&v)[kSlotsPerThread]) {
+    if (base + kSlotsPerThread <= total) {
+        const float4 *p = reinterpret_cast<const float4 *>(table + base);
+#pragma unroll
+        for (int q = 0; q < kSlotsPerThread / 4; ++q) {
+            const float4 f = p[q];
+            v[4 * q] = f.x;
+            v[4 * q + 1] = f.y;
+            v[4 * q + 2] = f.z;
+            v[4 * q + 3] = f.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kSlotsPerThread; ++j) v[j] = base + j < total ? table[base + j] : absent_f();
+    }
+}
+
 __global__ void __launch_bounds__(kBlock) count_kernel(const float *table, uint64_t total, uint64_t *blk) {
-    __shared__ uint32_t red[kBlock];
+    __shared__ uint32_t red[kBlock / 64];
     const uint64_t base = (uint64_t)blockIdx.x * kSlotsPerBlock + threadIdx.x * kSlotsPerThread;
+    float v[kSlotsPerThread];
+    load_slots(table, total, base, v);
     uint32_t c = 0;
 #pragma unroll
-    for (int j = 0; j < kSlotsPerThread; ++j) {
-        const uint64_t s = base + j;
-        if (s < total && fbits(table[s]) != kAbsentBits) ++c;
-    }
-    red[threadIdx.x] = c;
+    for (int j = 0; j < kSlotsPerThread; ++j) c += fbits(v[j]) != kAbsentBits;
+    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
     __syncthreads();
-    for (int s = kBlock / 2; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-        __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < kBlock / 64; ++w) t += red[w];
+        blk[blockIdx.x] = t;
     }
-    if (threadIdx.x == 0) blk[blockIdx.x] = red[0];
 }
 
 // exclusive scan of nb block counts in place, total in blk[nb]; one block.
@@ -1401,19 +1420,17 @@ __global__ void __launch_bounds__(1024) scan_kernel(uint64_t *blk, int64_t nb) {
     const int64_t b0 = threadIdx.x * per, b1 = b0 + per < nb ? b0 + per : nb;
     uint64_t s = 0;
     for (int64_t i = b0; i < b1; ++i) s += blk[i];
+    // inclusive Hillis-Steele scan of the 1024 partial sums
     part[threadIdx.x] = s;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t acc = 0;
-        for (int i = 0; i < 1024; ++i) {
-            const uint64_t t = part[i];
-            part[i] = acc;
-            acc += t;
-        }
-        blk[nb] = acc;
+    for (int off = 1; off < 1024; off <<= 1) {
+        const uint64_t t = (int)threadIdx.x >= off ? part[threadIdx.x - off] : 0ull;
+        __syncthreads();
+        part[threadIdx.x] += t;
+        __syncthreads();
     }
-    __syncthreads();
-    uint64_t acc = part[threadIdx.x];
+    if (threadIdx.x == 1023) blk[nb] = part[1023];
+    uint64_t acc = part[threadIdx.x] - s;
     for (int64_t i = b0; i < b1; ++i) {
         const uint64_t t = blk[i];
         blk[i] = acc;
@@ -1436,43 +1453,69 @@ struct WriteArgs {
     int64_t *offsets;
 };
 
+constexpr int kWriteLdsSegs = 2048;  // slab offsets staged in LDS up to this many (vi, L) segments
+
+// Stored slots -> (set, score) lists.  A thread's slots are contiguous, so it
+// locates its first slot's (variable, layer) segment and unranks it once;
+// every later slot is the colex successor (Gosper's hack, typedefs.h:692-697)
+// inside the segment, or the first set (1 << L) - 1 of the next one.
 __global__ void __launch_bounds__(kBlock) write_kernel(WriteArgs a) {
-    __shared__ uint32_t pre[kBlock];
+    __shared__ uint32_t pre[kBlock / 64];
     __shared__ uint32_t binom[64 * kBinomK];
-    for (int i = threadIdx.x; i < 64 * kBinomK; i += kBlock) binom[i] = a.binom[i];
-    const uint64_t base = (uint64_t)blockIdx.x * kSlotsPerBlock + threadIdx.x * kSlotsPerThread;
-    uint32_t c = 0;
-    float vals[kSlotsPerThread];
-#pragma unroll
-    for (int j = 0; j < kSlotsPerThread; ++j) {
-        const uint64_t s = base + j;
-        vals[j] = s < a.total ? a.table[s] : absent_f();
-        if (fbits(vals[j]) != kAbsentBits) ++c;
-    }
-    pre[threadIdx.x] = c;
-    __syncthreads();
-    // Hillis-Steele inclusive scan over 256 counts
-    for (int off = 1; off < kBlock; off <<= 1) {
-        const uint32_t t = (int)threadIdx.x >= off ? pre[threadIdx.x - off] : 0u;
-        __syncthreads();
-        pre[threadIdx.x] += t;
-        __syncthreads();
-    }
-    uint64_t pos = a.blk[blockIdx.x] + pre[threadIdx.x] - c;
+    __shared__ uint64_t toff_s[kWriteLdsSegs + 1];
     const int nseg = a.nv * a.S;
+    const bool lds_off = nseg <= kWriteLdsSegs;
+    for (int i = threadIdx.x; i < 64 * kBinomK; i += kBlock) binom[i] = a.binom[i];
+    if (lds_off)
+        for (int i = threadIdx.x; i <= nseg; i += kBlock) toff_s[i] = a.tbl_off[i];
+    const uint64_t *toff = lds_off ? toff_s : a.tbl_off;
+    const uint64_t base = (uint64_t)blockIdx.x * kSlotsPerBlock + threadIdx.x * kSlotsPerThread;
+    float vals[kSlotsPerThread];
+    load_slots(a.table, a.total, base, vals);
+    uint32_t c = 0;
 #pragma unroll
-    for (int j = 0; j < kSlotsPerThread; ++j) {
-        if (fbits(vals[j]) == kAbsentBits) continue;
+    for (int j = 0; j < kSlotsPerThread; ++j) c += fbits(vals[j]) != kAbsentBits;
+    // block-wide exclusive prefix of the per-thread counts: wave scan + wave totals
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t incl = c;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)incl, o);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) pre[wv] = incl;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (int w = 0; w < wv; ++w) wbase += pre[w];
+    if (c == 0) return;
+    uint64_t pos = a.blk[blockIdx.x] + wbase + incl - c;
+    int first = 0;
+    while (fbits(vals[first]) == kAbsentBits) ++first;
+    uint64_t s0 = base + first;
+    int lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (toff[mid] <= s0) lo = mid; else hi = mid;
+    }
+    int seg = lo;
+    int vi = seg / a.S, L = seg % a.S;
+    int m = a.meta[vi * 4 + 1];
+    uint64_t cm = L <= kMaxL ? unrank_colex(s0 - toff[seg], L, m, binom)
+                             : unrank_colex64(s0 - toff[seg], L, m, a.binom64);
+    for (int j = first; j < kSlotsPerThread; ++j) {
         const uint64_t s = base + j;
-        int lo = 0, hi = nseg;
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (a.tbl_off[mid] <= s) lo = mid; else hi = mid;
+        if (j > first) {
+            if (s >= toff[seg + 1]) {
+                while (s >= toff[seg + 1]) ++seg;
+                vi = seg / a.S;
+                L = seg % a.S;
+                m = a.meta[vi * 4 + 1];
+                cm = L ? (~0ull >> (64 - L)) : 0ull;
+            } else {
+                const uint64_t r = cm + (cm & (0 - cm));
+                cm = r | (((r ^ cm) >> 2) >> __builtin_ctzll(cm));
+            }
         }
-        const int vi = lo / a.S, L = lo % a.S;
-        const int m = a.meta[vi * 4 + 1];
-        const uint64_t cm = L <= kMaxL ? unrank_colex(s - a.tbl_off[lo], L, m, binom)
-                                       : unrank_colex64(s - a.tbl_off[lo], L, m, a.binom64);
+        if (fbits(vals[j]) == kAbsentBits) continue;
         uint64_t gs = 0;
         uint64_t rem = cm;
         while (rem) {
@@ -1861,13 +1904,39 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
         wslice = std::max<uint64_t>(kWideBitsWords / (uint64_t)G, wpl_max);
         if ((rc = ensure(c, c->d_wbits, (size_t)(G * wslice)))) return rc;
     }
-    // fork: the side streams start after the uploads / empty-set kernel
-    if (G > 1) {
-        ULG_HIP(c, hipEventRecord(c->sync_events[0], c->stream));
-        for (int g = 1; g < G; ++g) ULG_HIP(c, hipStreamWaitEvent(gst[g], c->sync_events[0], 0));
-    }
+    // Small layers (L <= Ls, little work, latency-bound): one one-pass launch
+    // per phase over all variables on the context stream -- no queue, no walk
+    // launch, no stream groups.  The rest: per group, score + queued walk.
+    const int Ls = (variant & 16) && !(variant & 8) && !wck ? std::min(kmax, std::min(kMaxL, c->score_small_layers)) : 0;
+    const int vsmall = variant & 1;
+    bool forked = false;
     for (int L = 1; L <= kmax; ++L)
-        for (int ph = 0; ph < 2; ++ph)
+        for (int ph = 0; ph < 2; ++ph) {
+            if (L <= Ls) {
+                const size_t wo = ((size_t)L * 2 + ph) * (nv + 1);
+                const uint64_t cnt = work[wo + nv];
+                if (cnt == 0) continue;
+                ScoreArgs ss = sa;
+                ss.work = c->d_work.p + wo;
+                ss.queue = nullptr;
+                ss.qcount = nullptr;
+                const LdsLayout lay = lds_layout(n, nv, S, L, vsmall);
+                const KernelFn kfn = layer_kernel(L, ph, vsmall);
+                if (lay.total > 64 * 1024)
+                    ULG_HIP(c, hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, lay.total));
+                prof_begin_s(c, kLayerNames[ph][L], c->stream);
+                hipLaunchKernelGGL(kfn, dim3((unsigned)((cnt + kBlock - 1) / kBlock)), dim3(kBlock), (size_t)lay.total,
+                                   c->stream, ss);
+                prof_end_s(c, c->stream);
+                continue;
+            }
+            // fork: the side streams start after the uploads / empty-set
+            // kernel / small layers
+            if (G > 1 && !forked) {
+                ULG_HIP(c, hipEventRecord(c->sync_events[0], c->stream));
+                for (int g = 1; g < G; ++g) ULG_HIP(c, hipStreamWaitEvent(gst[g], c->sync_events[0], 0));
+                forked = true;
+            }
             for (int g = 0; g < G; ++g) {
                 const size_t wo = (size_t)g * (G > 1 ? wstride : 0) + ((size_t)L * 2 + ph) * (nv + 1);
                 const uint64_t cnt = h_wk[wo + nv];
@@ -1977,8 +2046,9 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
                     }
                 }
             }
+        }
     // join: the compaction on the context stream waits for every group
-    for (int g = 1; g < G; ++g) {
+    for (int g = 1; g < G && forked; ++g) {
         ULG_HIP(c, hipEventRecord(c->sync_events[g], gst[g]));
         ULG_HIP(c, hipStreamWaitEvent(c->stream, c->sync_events[g], 0));
     }

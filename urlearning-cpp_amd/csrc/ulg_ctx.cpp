@@ -153,6 +153,12 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         c->score_streams = (int)value;
         return ULG_OK;
     }
+    if (std::strcmp(name, "score_small_layers") == 0) {
+        if (value < 0 || value > ULG_UNROLLED_PARENTS_GPU)
+            return set_err(c, ULG_ERR_ARG, "score_small_layers must be 0..8");
+        c->score_small_layers = (int)value;
+        return ULG_OK;
+    }
     if (std::strcmp(name, "score_variant") == 0) {
         if (value < 0 || (value > 7 && value != 13 && value != 16 && value != 17 && value != 48 && value != 49))
             return set_err(c, ULG_ERR_ARG, "score_variant must be 0..7, 13, 16, 17, 48 or 49");

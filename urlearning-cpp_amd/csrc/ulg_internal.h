@@ -69,6 +69,7 @@ struct ulg_ctx {
     bool scored = false;
     int score_variant = 49;
     int score_streams = 3;                  // scorer variable groups on concurrent streams
+    int score_small_layers = 4;             // layers <= this run one-pass on one stream (two-pass variants)
     std::vector<hipStream_t> aux_streams;   // created on first use
     std::vector<hipEvent_t> sync_events;
     uint64_t table_budget_kb = 0;  // best-score table budget in KiB (0 = half the free HBM)  // see ScoreArgs::variant (ulg_set_option "score_variant")
