@@ -45,13 +45,17 @@ def digest(offs, sets, scores, n):
 def main(lams):
     ds = oracle.Dataset(csv_path=CSV)
     n = ds.n
+    out = os.path.join(ROOT, "tests", "golden", "c1_hepatitis_digest.json")
     res = {"csv": "hepatitis.clean.csv", "n": n, "N": int(ds.N), "max_parents": n - 1, "runs": {}}
+    if os.path.exists(out):  # add to the lambdas already there
+        with open(out) as f:
+            res["runs"].update(json.load(f)["runs"])
     for lam in lams:
         offs, sets, scores = ds.score_all(lam, [(1 << n) - 1] * n, n - 1, threads=os.cpu_count() or 8)
         res["runs"][repr(float(lam))] = digest(offs, sets, scores, n)
         print(f"lambda={lam}: {int(offs[n])} stored sets", flush=True)
-    with open(os.path.join(ROOT, "tests", "golden", "c1_hepatitis_digest.json"), "w") as f:
-        json.dump(res, f, indent=0)
+        with open(out, "w") as f:  # after every lambda: a long run keeps what it finished
+            json.dump(res, f, indent=0)
 
 
 if __name__ == "__main__":
