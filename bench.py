@@ -194,6 +194,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-search", action="store_true")
     ap.add_argument("--score-variant", type=int, default=None, help="A/B knob (ulg_set_option score_variant)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo + --device: rehearse the N>1 code path with several ranks on one GPU")
+    ap.add_argument("--device", type=int, default=None, help="GPU for every rank (default LOCAL_RANK)")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -202,10 +205,13 @@ def main():
 
     import torch
     dist = None
+    if args.device is not None:
+        local = args.device
+    cdev = "cuda" if args.dist_backend == "nccl" else "cpu"  # where collective tensors live
     if ws > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=ws)
+        dist.init_process_group(args.dist_backend, rank=rank, world_size=ws)
 
     seed = 9200 + (rank if args.mode == "weak" else 0)
     X, _ = synth.gaussian_sem(n, N, seed)
@@ -236,7 +242,7 @@ def main():
             sc_t = torch.empty(max(stored, 1), dtype=torch.float32, device="cuda")
             off_t = torch.empty(len(variables) + 1, dtype=torch.int64, device="cuda")
             ctx.fetch_device(sets_t.data_ptr(), sc_t.data_ptr(), off_t.data_ptr())
-            shard.allgather_lists(shard.pack_device(variables, off_t, sets_t, sc_t), ws)
+            shard.allgather_lists(shard.pack_device(variables, off_t, sets_t, sc_t).to(cdev), ws)
         return scored
 
     for _ in range(args.warmup):
@@ -262,10 +268,10 @@ def main():
     ctx.profile(False)
     elapsed = t1 - t0
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        u = torch.tensor([scored_total], dtype=torch.float64, device="cuda")
+        u = torch.tensor([scored_total], dtype=torch.float64, device=cdev)
         dist.all_reduce(u, op=dist.ReduceOp.SUM)
         scored_all = float(u.item())
     else:
@@ -299,7 +305,8 @@ def main():
             "scaling": "weak" if args.mode == "weak" else "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": f"synthetic: seeded linear-Gaussian SEM (synth.gaussian_sem, seed {9200}+rank), {skel_note}",
+            "data": f"synthetic: seeded linear-Gaussian SEM (synth.gaussian_sem, seed "
+                    f"{'9200+rank' if args.mode == 'weak' else '9200, one dataset'}), {skel_note}",
             "config": {"workload": f"{args.config.upper()} cBIC scoring: n={n}, N={N}, max-parents k={k}, "
                                    f"lambda={lam}, {skel_note}, all {n} variables per "
                                    f"{'GPU' if args.mode == 'weak' else 'job'}",
