@@ -9,7 +9,9 @@ import synth  # noqa: E402
 import ulg  # noqa: E402
 
 ctx = ulg.Context(0)
-for name, n, N, k in (("c2", 20, 10000, 4), ("c3", 25, 10000, 6)):
+CFG = {"c2": (20, 10000, 4), "c3": (25, 10000, 6)}
+for name in (sys.argv[1:] or ["c2", "c3"]):
+    n, N, k = CFG[name]
     X, _ = synth.gaussian_sem(n, N, 9200)
     full = [(1 << n) - 1] * n
     ctx.load(X, 2.0)

@@ -13,7 +13,7 @@ import re
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libulg.so")
+LIB_PATH = os.environ.get("ULG_LIB", os.path.join(HERE, "libulg.so"))  # ULG_LIB: A/B builds
 HEADER = os.path.join(os.path.dirname(HERE), "include", "ulg.h")
 
 _lib = None
