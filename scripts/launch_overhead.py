@@ -9,10 +9,10 @@ X, _ = synth.gaussian_sem(n, N, 9200)
 ctx = ulg.Context(0)
 ctx.load(X, 2.0)
 full = [(1 << n) - 1] * n
-for streams, small in ((3, 4), (3, 5), (3, 6), (1, 4), (2, 4), (4, 4)):
+for streams, small in [tuple(int(x) for x in a.split(",")) for a in (sys.argv[1:] or ["3,4"])]:
     ctx.set_option("score_streams", streams)
     ctx.set_option("score_small_layers", small)
-    for k in range(4, 7):
+    for k in range(5, 7):
         for _ in range(3):
             ctx.score(list(range(n)), full, k)
         reps = 20

@@ -1600,10 +1600,12 @@ SlicedFn sliced_fn_k(int L, int phase) {
 }
 // sets per lane: more sets share one walk of the union tree, fewer give more
 // waves to hide the walk's latency
+// sets per lane of the bit-sliced walk: 2 up to layer 5 (more, smaller
+// unions), 4 above (C3: layer 5 0.58 -> 0.54 ms, layer 6 best at 4 or 8);
+// ULG_SLICED_K=2|4|8 overrides for A/B
 int sliced_k(int L) {
-    (void)L;
     const char *e = std::getenv("ULG_SLICED_K");
-    const int k = e ? std::atoi(e) : 4;
+    const int k = e ? std::atoi(e) : (L <= 5 ? 2 : 4);
     return (k == 2 || k == 8) ? k : 4;
 }
 SlicedFn sliced_fn(int L, int phase) {
