@@ -9,8 +9,15 @@ X, _ = synth.gaussian_sem(n, N, 9200)
 ctx = ulg.Context(0)
 ctx.load(X, 2.0)
 full = [(1 << n) - 1] * n
+if len(sys.argv) > 1:
+    ctx.set_option("score_variant", int(sys.argv[1]))
 for _ in range(3):
     ctx.score(list(range(n)), full, k)
+import time
+t0 = time.perf_counter()
+for _ in range(20):
+    ctx.score(list(range(n)), full, k)
+print(f"variant {sys.argv[1] if len(sys.argv) > 1 else 'default'}: {1e3 * (time.perf_counter() - t0) / 20:.3f} ms per call")
 ctx.profile(True)
 ctx.profile_reset()
 for _ in range(10):
