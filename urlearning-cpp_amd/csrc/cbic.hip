@@ -1039,8 +1039,9 @@ __global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, 
 #pragma unroll
         for (int r = 0; r < S::NV0; ++r) {
             const int t0 = r * S::E;
-            const uint32_t hb = (uint32_t)(hw[t0 >> 6] >> (t0 & 63)) & ((1u << S::E) - 1u);
-            const uint32_t ob = (uint32_t)(ow[t0 >> 6] >> (t0 & 63)) & ((1u << S::E) - 1u);
+            constexpr uint32_t EM = S::E == 32 ? ~0u : ((1u << S::E) - 1u);
+            const uint32_t hb = (uint32_t)(hw[t0 >> 6] >> (t0 & 63)) & EM;
+            const uint32_t ob = (uint32_t)(ow[t0 >> 6] >> (t0 & 63)) & EM;
             uint32_t hs, os;
             if constexpr (S::K == 8) {
                 // 4 bits -> bytes 0..3 (non-overlapping partial products)
@@ -1595,7 +1596,17 @@ SlicedFn sliced_fn_k(int L, int phase) {
         case 4: return sliced_pick<4, K>(phase);
         case 5: return sliced_pick<5, K>(phase);
         case 6: return sliced_pick<6, K>(phase);
-        default: return nullptr;  // L = 7, 8: the vectors no longer fit in registers
+        default: return nullptr;
+    }
+}
+// L = 7, 8 (256 / 512 local subsets): 2 and 1 sets per lane keep each of the
+// two vectors at 16 registers (C4: 3.95 -> 2.75 ms per step against the
+// per-lane walk_kernel)
+SlicedFn sliced_fn_wide(int L, int phase) {
+    switch (L) {
+        case 7: return sliced_pick<7, 2>(phase);
+        case 8: return sliced_pick<8, 1>(phase);
+        default: return nullptr;
     }
 }
 // sets per lane: more sets share one walk of the union tree, fewer give more
@@ -1604,11 +1615,13 @@ SlicedFn sliced_fn_k(int L, int phase) {
 // unions), 4 above (C3: layer 5 0.58 -> 0.54 ms, layer 6 best at 4 or 8);
 // ULG_SLICED_K=2|4|8 overrides for A/B
 int sliced_k(int L) {
+    if (L >= 7) return L == 7 ? 2 : 1;
     const char *e = std::getenv("ULG_SLICED_K");
     const int k = e ? std::atoi(e) : (L <= 5 ? 2 : 4);
     return (k == 2 || k == 8) ? k : 4;
 }
 SlicedFn sliced_fn(int L, int phase) {
+    if (L >= 7) return sliced_fn_wide(L, phase);
     switch (sliced_k(L)) {
         case 2: return sliced_fn_k<2>(L, phase);
         case 4: return sliced_fn_k<4>(L, phase);
