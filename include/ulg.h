@@ -91,7 +91,8 @@ int ulg_mmpc(ulg_ctx *ctx, double alpha, int max_cond, uint64_t *rows);
 
 /* Score all parent sets of size <= max_parents within each variable's
  * candidate set (candidates[i] for variable vars[i]; the variable's own bit
- * is ignored).  Runs the layer-synchronous HIP scorer; results stay on the
+ * is ignored).  max_parents < 1 or > n - 1 means n - 1, the reference's
+ * "a value less than 1 means no limit" (score_main.cpp:228,296-298).  Runs the layer-synchronous HIP scorer; results stay on the
  * device until ulg_cbic_fetch.  *total_stored = number of stored sets,
  * *total_scored = number of parent sets evaluated (incl. empty sets). */
 int ulg_cbic_score(ulg_ctx *ctx, const int *vars, int nv,

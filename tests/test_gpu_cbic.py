@@ -95,6 +95,36 @@ def test_sparse_skeleton_and_variable_subset(ulg_ctx, oracle_built):
     _compare_lists(*o, *g, variables, ctx="sparse")
 
 
+@pytest.mark.parametrize("k", [0, 1, 9, 12])
+def test_edge_parent_limits_and_isolated_variables(ulg_ctx, oracle_built, k):
+    """Edge cases of calculateScores_internal (score_calculator.cpp:54-135):
+    -p 0 (no limit: n - 1, score_main.cpp:296-298), a limit above the
+    candidate count (layers stop at m), a variable whose candidate set is
+    itself only (m = 0), one whose only candidate is variable 0, and a
+    skeleton row without variable 0."""
+    n = 12
+    X, _ = synth.gaussian_sem(n, 900, 9220)
+    full = (1 << n) - 1
+    variables = [0, 3, 5, 7, 11, 1]
+    cands = [full, 1 << 3, (1 << 5) | 1, full & ~1, (1 << 11) | (1 << 4) | (1 << 9), full]
+    ulg_ctx.load(X, 2.0)
+    g = ulg_ctx.score_all(variables, cands, k)
+    o = _oracle_lists(oracle_built, X, 2.0, variables, cands, k if k >= 1 else n - 1)
+    _compare_lists(*o, *g, variables, ctx=f"edge k={k}")
+    assert g[0][variables.index(3) + 1] - g[0][variables.index(3)] == 1  # m = 0: the empty set alone
+
+
+def test_parent_limit_above_gpu_maximum_fails_loudly(ulg_ctx):
+    """More than ULG_MAX_PARENTS_GPU (31) parents: a status code and a
+    message, not a silent truncation."""
+    import ulg
+    n = 40
+    X, _ = synth.gaussian_sem(n, 200, 9221)
+    ulg_ctx.load(X, 2.0)
+    with pytest.raises(ulg.ULGError, match="ULG_MAX_PARENTS_GPU"):
+        ulg_ctx.score([0], [(1 << n) - 1], 32)
+
+
 def test_quantize_matches_oracle(ulg_ctx, oracle_built):
     rng = np.random.default_rng(7)
     vals = np.concatenate([rng.normal(0, 3e4, 20000), rng.normal(0, 1, 20000), rng.normal(0, 1e-5, 5000),
