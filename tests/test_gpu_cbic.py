@@ -114,6 +114,27 @@ def test_edge_parent_limits_and_isolated_variables(ulg_ctx, oracle_built, k):
     assert g[0][variables.index(3) + 1] - g[0][variables.index(3)] == 1  # m = 0: the empty set alone
 
 
+def test_constant_column_nan_scores_match_oracle(ulg_ctx, oracle_built):
+    """A constant column normalises to NaN (x - mean = 0, sd = 0, as
+    BIC_OLS.cpp:66-97 divides): every set containing it, and the variable's
+    own sets, score NaN.  NaN is never >= -ts and never pruned, so such sets
+    are stored and stop the subset recursion like any stored key; the absent
+    sentinel (a NaN of its own payload) must not swallow them."""
+    n = 7
+    X, _ = synth.gaussian_sem(n, 600, 9230)
+    X[:, 2] = 3.0
+    variables = list(range(n))
+    cands = [(1 << n) - 1] * n
+    ulg_ctx.load(X, 2.0)
+    g_offs, g_sets, g_sc = ulg_ctx.score_all(variables, cands, 4)
+    o_offs, o_sets, o_sc = _oracle_lists(oracle_built, X, 2.0, variables, cands, 4)
+    assert np.array_equal(o_offs, g_offs) and np.array_equal(o_sets, g_sets)
+    assert np.array_equal(np.isnan(o_sc), np.isnan(g_sc)) and np.isnan(g_sc).any()
+    ok = ~np.isnan(o_sc)
+    err = np.abs(o_sc[ok].astype(np.float64) - g_sc[ok]) / np.maximum(np.abs(o_sc[ok]), 1.0)
+    assert err.max(initial=0.0) <= REL_TOL
+
+
 def test_parent_limit_above_gpu_maximum_fails_loudly(ulg_ctx):
     """More than ULG_MAX_PARENTS_GPU (31) parents: a status code and a
     message, not a silent truncation."""
