@@ -252,3 +252,29 @@ def test_gpu_mode_rejects_ancestors(ulg_ctx, oracle_built):
     ulg_ctx.search_load(offs, sets, costs)
     with pytest.raises(RuntimeError):
         ulg_ctx.astar(edges=[(1 << n) - 1] * n, mode=1, ancestors=0b1, scc=0b110)
+
+
+@pytest.mark.parametrize("symmetric", [True, False])
+def test_gpu_search_sparse_skeleton_optimal_cost(ulg_ctx, oracle_built, symmetric):
+    """GPU layer search under the neighbour filter (astar_main.cpp:305-313):
+    with symmetric rows it settles disconnected subsets without reading their
+    predecessors; with asymmetric rows (a hand-edited skeleton file) it reads
+    them all.  Either way the optimal cost equals the oracle's A*."""
+    import ulg
+    o = oracle_built
+    n = 16
+    X, W = synth.gaussian_sem(n, 3000, 9330)
+    rows = synth.true_skeleton_edges(W, extra_frac=0.2, seed=5)
+    if not symmetric:  # drop one direction of a few edges
+        for i in range(n):
+            nb = [j for j in range(n) if (rows[i] >> j) & 1 and j > i]
+            if nb and i % 3 == 0:
+                rows[i] &= ~(1 << nb[0])
+    cands = ulg.candidates_from_edges(rows, n)
+    offs, sets, scores, costs = _oracle_pipeline(o, X, 2.0, 4, cands)
+    ulg_ctx.search_load(offs, sets, costs)
+    ulg_ctx.pdb_build(2)
+    res = ulg_ctx.astar(edges=rows, mode=1, net_text=False)
+    ref = o.Search(n, offs, sets, costs).astar(edges=rows)
+    assert ref["rc"] == 0
+    assert abs(res["cost"] - ref["cost"]) <= 1e-6 * abs(ref["cost"]), (res["cost"], ref["cost"])

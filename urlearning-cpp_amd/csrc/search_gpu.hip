@@ -33,6 +33,7 @@ struct LayerArgs {
     const int *comp_vars;    // compact bit -> variable
     const uint64_t *edges;   // skeleton rows (may be null)
     int skeleton;            // apply the neighbour filter
+    int symmetric;           // skeleton rows symmetric: reachable == connected (see layer_pull_kernel)
     int m;                   // component size
     int layer;               // layer of the nodes computed by this launch (>= 1)
     uint64_t count;          // C(m, layer)
@@ -49,8 +50,11 @@ __device__ __forceinline__ uint64_t Bn(const uint64_t *b, int a, int k) { return
 __global__ void __launch_bounds__(kB) layer_pull_kernel(LayerArgs a) {
     __shared__ uint64_t binom[33 * 33];
     __shared__ int cv[kMaxM];
+    __shared__ uint64_t edg[64];
     for (int i = threadIdx.x; i < 33 * 33; i += kB) binom[i] = a.binom[i];
     for (int i = threadIdx.x; i < a.m; i += kB) cv[i] = a.comp_vars[i];
+    if (a.symmetric)
+        for (int i = threadIdx.x; i < 64; i += kB) edg[i] = a.edges[i];
     __syncthreads();
     const uint64_t r = (uint64_t)blockIdx.x * kB + threadIdx.x;
     const int L = a.layer;
@@ -69,9 +73,26 @@ __global__ void __launch_bounds__(kB) layer_pull_kernel(LayerArgs a) {
     }
     uint64_t Tg = 0;
     for (uint64_t x = Tc; x; x &= x - 1) Tg |= 1ull << cv[__builtin_ctzll(x)];
+    // With symmetric rows a node is reachable iff T induces a connected
+    // subgraph: the filter lets a leaf follow P only if one of its neighbours
+    // is in P, so every reachable T grows connected, and a connected T can be
+    // grown from any of its vertices.  A disconnected T has no reached
+    // predecessor it may follow, so it is settled here without the L
+    // predecessor reads (most of the lattice on a sparse skeleton).
+    bool connected = true;
+    if (a.symmetric && L > 1) {
+        uint64_t seen = Tg & (0 - Tg), fr = seen;
+        while (fr) {
+            uint64_t nb = 0;
+            for (uint64_t y = fr; y; y &= y - 1) nb |= edg[__builtin_ctzll(y)];
+            fr = nb & Tg & ~seen;
+            seen |= fr;
+        }
+        connected = seen == Tg;
+    }
     // rank(T \ a_j) = sum_{i<j} C(a_i, i+1) + sum_{i>j} C(a_i, i)   (a_0 < a_1 < ...)
     uint64_t suffix = 0;
-    {
+    if (connected) {
         int i = 0;
         for (uint64_t x = Tc; x; x &= x - 1, ++i)
             if (i >= 1) suffix += Bn(binom, __builtin_ctzll(x), i);
@@ -81,7 +102,7 @@ __global__ void __launch_bounds__(kB) layer_pull_kernel(LayerArgs a) {
     int bestj = 255;
     bool reached = false;
     uint64_t x = Tc;
-    for (int j = 0; j < L; ++j) {
+    for (int j = 0; j < (connected ? L : 0); ++j) {
         const int aj = __builtin_ctzll(x);
         x &= x - 1;  // x now holds a_{j+1}, ...
         const int leaf = cv[aj];
@@ -197,6 +218,13 @@ int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, flo
     if (e == hipSuccess) e = hipMemsetAsync(d_acc.p, 0, kCounters * 8, c->stream);
     if (e != hipSuccess) { cleanup(); return set_err(c, ULG_ERR_HIP, hipGetErrorString(e)); }
     const SearchDev dv = s.dev();
+    bool symmetric = edges != nullptr;  // off-diagonal rows mirror each other
+    for (int i = 0; i < n && symmetric; ++i)
+        for (int j = 0; j < n; ++j)
+            if (i != j && (((edges[i] >> j) ^ (edges[j] >> i)) & 1ull)) {
+                symmetric = false;
+                break;
+            }
     bool fail = false;
     for (uint64_t comp : comps) {
         const int m = __builtin_popcountll(comp);
@@ -224,8 +252,8 @@ int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, flo
         float *gprev = d_g0.p, *gcur = d_g1.p;
         for (int d = 1; d <= m; ++d) {
             const uint64_t cnt = binom64(m, d);
-            LayerArgs a{dv, d_bn.p, d_cv.p, d_edges.p, edges ? 1 : 0, m, d, cnt, gprev, gcur, d_leaf.p + loff[d],
-                        d < m ? d_acc.p : nullptr};
+            LayerArgs a{dv, d_bn.p, d_cv.p, d_edges.p, edges ? 1 : 0, symmetric ? 1 : 0, m, d, cnt, gprev, gcur,
+                        d_leaf.p + loff[d], d < m ? d_acc.p : nullptr};
             prof_begin(c, "search_layer_pull");
             layer_pull_kernel<<<(unsigned)((cnt + kB - 1) / kB), kB, 0, c->stream>>>(a);
             prof_end(c);
