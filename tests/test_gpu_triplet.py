@@ -198,3 +198,23 @@ def test_triplet_memo_reuse_and_put(ulg_ctx):
         assert res["distinct"] == one["distinct"] - (len(clusters) - st["distinct"])
     finally:
         other.close()
+
+
+def test_triplet_look_ahead_threads_equal_sequential(ulg_ctx, oracle_built, monkeypatch):
+    """The first sweep's look-ahead searches on host threads (host-built
+    pattern databases, results held until the driver asks) give the
+    sequential driver's MEC and statistics, and both equal the oracle's."""
+    o = oracle_built
+    n = 18
+    X, W = synth.gaussian_sem(n, 3000, 9413)
+    rows = [r & ~(1 << i) for i, r in enumerate(synth.true_skeleton_edges(W, 0.15, 9413))]
+    offs, sets, costs = _oracle_costs(o, X, 2.0, 3, ulg.candidates_from_edges(rows, n))
+    res = {}
+    for threads in ("1", "8"):
+        monkeypatch.setenv("ULG_TRIPLET_THREADS", threads)
+        ulg_ctx.search_load(offs, sets, costs)
+        res[threads] = ulg_ctx.triplet(edges=rows)
+    ref = o.triplet(o.Search(n, offs, sets, costs), edges=rows)
+    for r in res.values():
+        assert r["mec"].tolist() == ref["mec"].tolist()
+        assert (r["runs"], r["distinct"], r["expanded"]) == (ref["runs"], ref["distinct"], ref["expanded"])

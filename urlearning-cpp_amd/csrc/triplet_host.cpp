@@ -14,7 +14,10 @@
 // The orientation state is held as bit rows: out[i] bit j == directed_graph
 // [i][j].  Both directions set = undirected edge.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <cmath>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -39,6 +42,15 @@ struct Triplet {
     uint64_t nb[64] = {}, clusters[64] = {}, vstr[64] = {}, out[64] = {};
     std::unordered_set<uint64_t> checked;
     std::unordered_map<uint64_t, std::vector<uint64_t>> *memo = nullptr;  // SearchState::triplet_memo
+    struct SpecResult {
+        std::vector<uint64_t> op;
+        int64_t nexp = 0;
+        bool hang = false;
+    };
+    std::unordered_map<uint64_t, SpecResult> spec;  // searched ahead, not yet asked for
+    int threads = 1;           // host threads for searches ahead (ULG_TRIPLET_THREADS)
+    bool parallel_ok = false;  // device tables cover every variable; host costs ready
+    int ci = -1, cj = 0, ck = 0;  // the first sweep's current triple (speculate); -1: off
     int64_t runs = 0, distinct = 0, expanded = 0;
     int num_v_structures = 0;
     bool hang = false;
@@ -64,19 +76,19 @@ struct Triplet {
     }
 };
 
+// One cluster's search, host side only: the goal's leaf chain (for the
+// parent queries), expansions, and whether the reference heap would spin.
+struct ClusterRun {
+    int64_t nexp = 0;
+    bool hang = false;
+    std::vector<int> qv;        // leaves from the goal back to the root
+    std::vector<uint64_t> qs;   // the set each leaf was added to (incl. itself)
+};
+
 // run_astar_on_one_scc of triplet_astar.cpp:285-674 with ancestors = {} and
 // the_scc = cluster: no skeleton filter, and a closed node whose g strictly
-// improves is pushed back onto the open list (:556-576).
-int cluster_astar(Triplet &t, uint64_t cluster, std::vector<uint64_t> &op) {
-    ulg_ctx *c = t.c;
-    int rc;
-    // every lookup of this search and of its PDB lies inside the cluster
-    if ((rc = search_ensure_scope(c, cluster)) || (rc = search_cost_table_host(c))) return rc;
-    if ((rc = search_build_pdb(c, t.pd_count, 0, cluster))) return rc;
-    HostTables T;
-    host_tables(*t.s, T);
-    const int n = t.n;
-    op.assign(n, 0);
+// improves is pushed back onto the open list (:556-576).  Reads only T.
+void astar_cluster(const HostTables &T, uint64_t cluster, ClusterRun &R) {
     std::vector<Node> nodes;
     nodes.reserve(1024);
     SubsetIndex generated;
@@ -126,44 +138,205 @@ int cluster_astar(Triplet &t, uint64_t cluster, std::vector<uint64_t> &op) {
             }
         }
     }
-    t.expanded += nexp;
-    if (open.hang) t.hang = true;
-    if (goal < 0) return ULG_OK;  // no goal: every parent set stays empty
-    // reconstructSolution (:172-224): walk the leaves back from the goal and
-    // ask the device for each leaf's best parent set among its predecessors
+    R.nexp = nexp;
+    R.hang = open.hang;
+    if (goal < 0) return;  // no goal: every parent set stays empty
+    // reconstructSolution (:172-224): walk the leaves back from the goal
     const int count = __builtin_popcountll(cluster);
-    std::vector<int> qv;
-    std::vector<uint64_t> qs;
     uint64_t remaining = nodes[goal].sub;
     int64_t cur = goal;
     for (int i = 0; i < count && cur >= 0; ++i) {
         const int leaf = nodes[cur].leaf;
-        qv.push_back(leaf);
-        qs.push_back(remaining);
+        R.qv.push_back(leaf);
+        R.qs.push_back(remaining);
         remaining ^= 1ull << leaf;
         cur = generated.find(remaining);
     }
-    if (!qv.empty()) {
-        std::vector<float> qc(qv.size());
-        std::vector<uint64_t> qp(qv.size());
-        if ((rc = search_query(c, (int64_t)qv.size(), qv.data(), qs.data(), qc.data(), qp.data()))) return rc;
-        for (size_t i = 0; i < qv.size(); ++i) op[qv[i]] = qp[i];
+}
+
+// each leaf's best parent set among its predecessors, from the device tables
+int cluster_parents_of(Triplet &t, const ClusterRun &R, std::vector<uint64_t> &op) {
+    op.assign(t.n, 0);
+    if (R.qv.empty()) return ULG_OK;
+    std::vector<float> qc(R.qv.size());
+    std::vector<uint64_t> qp(R.qv.size());
+    if (int rc = search_query(t.c, (int64_t)R.qv.size(), R.qv.data(), R.qs.data(), qc.data(), qp.data())) return rc;
+    for (size_t i = 0; i < R.qv.size(); ++i) op[R.qv[i]] = qp[i];
+    return ULG_OK;
+}
+
+int cluster_astar(Triplet &t, uint64_t cluster, std::vector<uint64_t> &op) {
+    ulg_ctx *c = t.c;
+    int rc;
+    // every lookup of this search and of its PDB lies inside the cluster
+    if ((rc = search_ensure_scope(c, cluster)) || (rc = search_cost_table_host(c))) return rc;
+    if ((rc = search_build_pdb(c, t.pd_count, 0, cluster))) return rc;
+    HostTables T;
+    host_tables(*t.s, T);
+    ClusterRun R;
+    astar_cluster(T, cluster, R);
+    t.expanded += R.nexp;
+    if (R.hang) t.hang = true;
+    return cluster_parents_of(t, R, op);
+}
+
+// StaticPatternDatabase over `scc` (static_pattern_database.cpp:95-120 groups,
+// :176-219 reverse DP) on the host, with search_build_pdb's exact float
+// operations and order (pdb_bs_kernel + pdb_layer_kernel), for the parallel
+// cluster searches: each needs its own database while the device holds one.
+struct HostPdb {
+    std::vector<uint64_t> groups, pd_off;
+    std::vector<float> pd;
+};
+bool pdb_host(const HostTables &T, uint64_t scc, int pd_count, HostPdb &P) {
+    const int remaining = __builtin_popcountll(scc);
+    const int pds = (int)std::ceil((float)remaining / pd_count);
+    int var = scc ? __builtin_ctzll(scc) : -1;
+    int x = 0;
+    P.groups.clear();
+    for (int g = 0; g < pd_count; ++g) {
+        uint64_t grp = 0;
+        for (int sz = 0; sz < pds && x < remaining; ++sz) {
+            grp |= 1ull << var;
+            const uint64_t rest = (var + 1 < 64) ? (scc >> (var + 1)) : 0;
+            var = var + (rest ? (__builtin_ctzll(rest) + 1) : 0);
+            ++x;
+        }
+        P.groups.push_back(grp);
+    }
+    P.pd_off.assign(pd_count + 1, 0);
+    for (int g = 0; g < pd_count; ++g) {
+        const int sz = __builtin_popcountll(P.groups[g]);
+        if (sz > 24) return false;
+        P.pd_off[g + 1] = P.pd_off[g] + (1ull << sz);
+    }
+    P.pd.assign(P.pd_off[pd_count], 0.0f);
+    std::vector<float> bsv;
+    for (int g = 0; g < pd_count; ++g) {
+        const uint64_t grp = P.groups[g];
+        const int s = __builtin_popcountll(grp);
+        if (s == 0) continue;
+        int bitpos[64];
+        int q = 0;
+        for (int b = 0; b < 64; ++b)
+            if ((grp >> b) & 1ull) bitpos[q++] = b;
+        bsv.assign((size_t)s << s, 0.0f);
+        for (uint64_t R = 1; R < (1ull << s); ++R) {
+            uint64_t Rg = 0;
+            for (int b = 0; b < s; ++b)
+                if ((R >> b) & 1ull) Rg |= 1ull << bitpos[b];
+            for (int j = 0; j < s; ++j) {
+                if (!((R >> j) & 1ull)) continue;
+                const int leaf = bitpos[j];
+                bsv[R * s + j] = T.bs(leaf, scc & ~(Rg & ~(1ull << leaf)));
+            }
+        }
+        float *pd = P.pd.data() + P.pd_off[g];
+        for (int layer = 1; layer <= s; ++layer)
+            for (uint64_t R = 1; R < (1ull << s); ++R) {
+                if (__builtin_popcountll(R) != layer) continue;
+                float cur = 0.0f;
+                for (int j = s - 1; j >= 0; --j) {
+                    if (!((R >> j) & 1ull)) continue;
+                    const float newG = bsv[R * s + j] + pd[R ^ (1ull << j)];
+                    if (cur == 0 || newG < cur) cur = newG;
+                }
+                pd[R] = cur;
+            }
+    }
+    return true;
+}
+
+// Searches of several clusters on host threads (each with its own host PDB,
+// all reading the shared host cost table), then their parent queries on the
+// device in order.  Results go to t.spec; cluster_parents counts a search
+// (distinct, expansions) only when the driver asks for its cluster, so the
+// statistics are the sequential driver's.
+int solve_parallel(Triplet &t, const std::vector<uint64_t> &batch) {
+    HostTables base;
+    host_tables(*t.s, base);
+    std::vector<ClusterRun> runs(batch.size());
+    std::vector<char> ok(batch.size(), 1);
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+        HostPdb P;
+        for (size_t i; (i = next.fetch_add(1)) < batch.size();) {
+            if (!pdb_host(base, batch[i], t.pd_count, P)) { ok[i] = 0; continue; }
+            HostTables T = base;
+            T.pd = P.pd.data();
+            T.groups = P.groups;
+            T.pd_off = P.pd_off;
+            astar_cluster(T, batch[i], runs[i]);
+        }
+    };
+    std::vector<std::thread> pool;
+    const int nt = std::min<int>(t.threads, (int)batch.size());
+    for (int k = 1; k < nt; ++k) pool.emplace_back(work);
+    work();
+    for (auto &th : pool) th.join();
+    for (size_t i = 0; i < batch.size(); ++i) {
+        if (!ok[i]) return set_err(t.c, ULG_ERR_UNSUPPORTED, "pattern-database group larger than 24 variables");
+        Triplet::SpecResult sp;
+        sp.nexp = runs[i].nexp;
+        sp.hang = runs[i].hang;
+        if (int rc = cluster_parents_of(t, runs[i], sp.op)) return rc;
+        t.spec.emplace(batch[i], std::move(sp));
     }
     return ULG_OK;
+}
+
+// Up to `want` distinct clusters, not yet searched, of the triples the first
+// sweep reaches after (ci, cj, ck) on the current skeleton -- orientations may
+// still change some of them, which only leaves a result unused.
+void speculate(Triplet &t, std::vector<uint64_t> &batch, size_t want) {
+    std::unordered_set<uint64_t> seen(batch.begin(), batch.end());
+    for (int i = t.ci; i < t.n && batch.size() < want; ++i) {
+        std::vector<int> unc;
+        for (int j = 0; j < t.n; ++j)
+            if (bit(t.nb[i], j)) unc.push_back(j);
+        for (int j = (i == t.ci ? t.cj : 0); j < (int)unc.size() && batch.size() < want; ++j)
+            for (int k = (i == t.ci && j == t.cj ? t.ck + 1 : 0); k < j && batch.size() < want; ++k) {
+                int a[3] = {i, unc[j], unc[k]};
+                std::sort(a, a + 3);
+                const uint64_t key = ((uint64_t)a[0] << 40) + ((uint64_t)a[1] << 20) + (uint64_t)a[2];
+                if (t.checked.count(key)) continue;
+                const uint64_t big = t.clusters[i] | t.clusters[unc[j]] | t.clusters[unc[k]];
+                if (__builtin_popcountll(big) > kMaxCluster || t.memo->count(big) || t.spec.count(big) ||
+                    !seen.insert(big).second)
+                    continue;
+                batch.push_back(big);
+            }
+    }
 }
 
 const std::vector<uint64_t> *cluster_parents(Triplet &t, uint64_t cluster) {
     ++t.runs;
     auto it = t.memo->find(cluster);
     if (it != t.memo->end()) return &it->second;
-    std::vector<uint64_t> op;
     static const bool trace = std::getenv("ULG_TRIPLET_TRACE") != nullptr;  // per-search progress on stderr
-    const int64_t e0 = t.expanded;
     const auto c0 = std::chrono::steady_clock::now();
-    if ((t.rc = cluster_astar(t, cluster, op))) return nullptr;
+    if (!t.spec.count(cluster) && t.threads > 1 && t.ci >= 0 && t.parallel_ok) {
+        std::vector<uint64_t> batch{cluster};
+        speculate(t, batch, (size_t)t.threads);
+        if ((t.rc = solve_parallel(t, batch))) return nullptr;
+    }
+    auto sp = t.spec.find(cluster);
+    std::vector<uint64_t> op;
+    int64_t nexp;
+    if (sp != t.spec.end()) {
+        nexp = sp->second.nexp;
+        if (sp->second.hang) t.hang = true;
+        t.expanded += nexp;
+        op = std::move(sp->second.op);
+        t.spec.erase(sp);
+    } else {
+        const int64_t e0 = t.expanded;
+        if ((t.rc = cluster_astar(t, cluster, op))) return nullptr;
+        nexp = t.expanded - e0;
+    }
     if (trace)
         std::fprintf(stderr, "triplet: cluster %016llx (%d variables): %lld expansions in %.3f s\n",
-                     (unsigned long long)cluster, __builtin_popcountll(cluster), (long long)(t.expanded - e0),
+                     (unsigned long long)cluster, __builtin_popcountll(cluster), (long long)nexp,
                      std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count());
     ++t.distinct;
     return &t.memo->emplace(cluster, std::move(op)).first->second;
@@ -177,6 +350,17 @@ std::unordered_map<uint64_t, std::vector<uint64_t>> *memo_for(SearchState &s, in
         s.triplet_pd = pd_count;
     }
     return &s.triplet_memo;
+}
+
+// Look-ahead searches on host threads need the lattice tables over every
+// variable (then no cluster rebuilds them) and their host copy.
+void set_parallel(Triplet &t) {
+    const char *e = std::getenv("ULG_TRIPLET_THREADS");
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    t.threads = e ? std::max(1, std::atoi(e)) : std::min(8, hw);
+    const uint64_t all = (t.n >= 64) ? ~0ull : ((1ull << t.n) - 1ull);
+    t.parallel_ok = t.threads > 1 && t.s->tables_ready && (t.s->scope & all) == all &&
+                    search_cost_table_host(t.c) == ULG_OK;
 }
 
 void init_skeleton(Triplet &t, const uint64_t *edges) {
@@ -310,6 +494,7 @@ extern "C" int ulg_triplet_astar(ulg_ctx *c, const uint64_t *edges, int pd_count
     t.pd_count = pd_count;
     t.memo = memo_for(s, pd_count);
     init_skeleton(t, edges);
+    set_parallel(t);
     for (int i = 0; i < n && !t.rc; ++i) {
         const uint64_t pin = t.nb[i];
         std::vector<int> unc;
@@ -331,11 +516,15 @@ extern "C" int ulg_triplet_astar(ulg_ctx *c, const uint64_t *edges, int pd_count
             const int vj = unc[j];
             for (size_t k = 0; k < j && !t.rc; ++k) {
                 const int vk = unc[k];
+                t.ci = i;
+                t.cj = (int)j;
+                t.ck = (int)k;
                 process_triple(t, i, vj, vk);
                 if (!bit(t.nb[vj], vk) && (t.dg(vj, vk) || t.dg(vk, vj))) t.add_edge(vj, vk);
             }
         }
     }
+    t.ci = -1;  // no look-ahead past the first sweep
     // unfaithful edges: oriented pairs the skeleton lacks (:1256-1290)
     int delta = 1;
     while (delta > 0 && !t.rc) {
@@ -411,9 +600,18 @@ extern "C" int ulg_triplet_solve(ulg_ctx *c, const uint64_t *clusters, int64_t n
     t.pd_count = pd_count;
     t.memo = memo_for(s, pd_count);
     const uint64_t all = (t.n >= 64) ? ~0ull : ((1ull << t.n) - 1ull);
-    for (int64_t i = 0; i < nc; ++i) {
+    for (int64_t i = 0; i < nc; ++i)
         if ((clusters[i] & ~all) || __builtin_popcountll(clusters[i]) > kMaxCluster)
             return set_err(c, ULG_ERR_ARG, "ulg_triplet_solve: cluster outside the variables or above 26 variables");
+    set_parallel(t);
+    if (t.parallel_ok) {  // every cluster not searched yet, on host threads
+        std::vector<uint64_t> batch;
+        std::unordered_set<uint64_t> seen;
+        for (int64_t i = 0; i < nc; ++i)
+            if (!t.memo->count(clusters[i]) && seen.insert(clusters[i]).second) batch.push_back(clusters[i]);
+        if (!batch.empty() && (t.rc = solve_parallel(t, batch))) return t.rc;
+    }
+    for (int64_t i = 0; i < nc; ++i) {
         const std::vector<uint64_t> *op = cluster_parents(t, clusters[i]);
         if (!op) return t.rc;
         if (parents) std::memcpy(parents + i * t.n, op->data(), sizeof(uint64_t) * t.n);
