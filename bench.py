@@ -128,6 +128,33 @@ def roofline(ctx, cfg, per_layer_sets, steps):
              "fp64_tflops": sets * flops_per_set / (p["avg_ms"] * 1e-3) / 1e12}, p)
 
 
+PMC_SEARCH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1", "pmc_search_traffic.json")
+
+
+def search_roofline(cfg, n, pull, reps):
+    """Roofline of the GPU order-graph sweep (layer_pull_kernel, one launch
+    per layer) on a full skeleton: a layer-L node reads L predecessors' g
+    (4 B) and best-score keys (8 B) and writes its g (4 B) and leaf (1 B), so
+    one sweep's algorithmic bytes are sum_L C(n, L) (12 L + 5).  The achieved
+    rate divides them by the sweep's summed kernel time (HIP events on the
+    launch stream); traffic is the PMC-measured bytes of one sweep."""
+    cnt, sweep_ms = pull["count"], pull["total_ms"] / reps
+    algo = sum(math.comb(n, L) * (12 * L + 5) for L in range(1, n + 1))
+    achieved = algo / (sweep_ms * 1e-3) / 1e9
+    traffic, src = None, None
+    try:
+        t = json.load(open(PMC_SEARCH))
+        if t.get("config_id") == cfg["id"] and t.get("n") == n:
+            traffic, src = t["traffic_bytes_per_sweep"], "profiles/r1/pmc_search_traffic.json"
+    except (OSError, ValueError):
+        pass
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per sweep",
+            "traffic_source": src, "kernel": "layer_pull_kernel", "launches_per_sweep": cnt // reps,
+            "sweep_kernel_ms": sweep_ms, "algorithmic_bytes_per_sweep": algo,
+            "bytes_per_node": "12 L + 5 (L predecessors x (4 B g + 8 B key) + 4 B g + 1 B leaf written)"}
+
+
 def search_metrics(ctx, cfg, variables, cands, rank, ws, reps=3, edges=None, skel_note="full skeleton"):
     """Order-graph search side on this rank's scored lists: GPU best-score
     tables + pattern database + GPU layer-synchronous search at the bench
@@ -145,16 +172,24 @@ def search_metrics(ctx, cfg, variables, cands, rank, ws, reps=3, edges=None, ske
     ctx.pdb_build(2)
     t2 = _t.perf_counter()
     best = None
+    # HIP events around every layer_pull_kernel launch of the sweeps
+    ctx.profile(True)
+    ctx.profile_select(["search_layer_pull"])
+    ctx.profile_reset()
     for _ in range(reps):
         ts = _t.perf_counter()
         g = ctx.astar(edges=skel, mode=1, net_text=False)
         dt = _t.perf_counter() - ts
         best = dt if best is None else min(best, dt)
+    pull = ctx.profile_get("search_layer_pull")
+    ctx.profile(False)
     out["gpu_search"] = {"config": f"{cfg['id'].upper()} lists (n={n}, k={k}), {skel_note}, static PDB(2)",
                          "expansions": g["expanded"], "ms": 1e3 * best,
                          "expansions_per_s": g["expanded"] / best, "goal_cost": g["cost"],
                          "tables_ms": 1e3 * (t1 - t0), "pdb_ms": 1e3 * (t2 - t1),
                          "note": "layer-synchronous pull over the whole order lattice; best of %d" % reps}
+    if edges is None and pull is not None:
+        out["gpu_search"]["roofline"] = search_roofline(cfg, n, pull, reps)
     if rank == 0 and ws == 1:
         c2 = CONFIGS["c2"]
         n2, N2, k2 = c2["n"], c2["N"], c2["k"]

@@ -208,3 +208,38 @@ def test_scorer_variants_identical(ulg_ctx, oracle_built, variant):
             _compare_lists(*o, *g, variables, ctx=f"variant {variant} k={k}")
     finally:
         ulg_ctx.set_option("score_variant", 17)
+
+
+@pytest.mark.parametrize("sets_per_lane", ["1", "1w2", "2", "4", "8"])
+def test_walk_forms_identical(ulg_ctx, oracle_built, monkeypatch, sets_per_lane):
+    """The walk forms (ULG_SLICED_K: 1 = lane-transposed scalar walk, 64 sets
+    per wave, or 128 at layer 6 with ULG_LANE_NW=2; 2/4/8 = bit-sliced walk)
+    store exactly the oracle's sets, with and without variable 0 among the
+    candidates (both N4 phases)."""
+    monkeypatch.setenv("ULG_SLICED_K", sets_per_lane[0])
+    monkeypatch.setenv("ULG_LANE_NW", "2" if sets_per_lane.endswith("w2") else "1")
+    n = 12
+    X, _ = synth.gaussian_sem(n, 3000, 9250)
+    ulg_ctx.load(X, 2.0)
+    for cands in ([(1 << n) - 1] * n, [((1 << n) - 1) & ~1] * n):
+        variables = list(range(1, n)) if cands[0] & 1 == 0 else list(range(n))
+        cands = cands[:len(variables)]
+        g = ulg_ctx.score_all(variables, cands, 6)
+        o = _oracle_lists(oracle_built, X, 2.0, variables, cands, 6)
+        _compare_lists(*o, *g, variables, ctx=f"ULG_SLICED_K={sets_per_lane}")
+
+
+def test_walk_forms_identical_c3(ulg_ctx, monkeypatch):
+    """At C3 (n=25, N=10k, k=6, full skeleton: 4,751,275 sets) the
+    lane-transposed walk stores the bit-sliced walk's lists bit for bit."""
+    n = 25
+    X, _ = synth.gaussian_sem(n, 10000, 9200)
+    ulg_ctx.load(X, 2.0)
+    res = {}
+    for k in ("4", "1", "1w2"):
+        monkeypatch.setenv("ULG_SLICED_K", k[0])
+        monkeypatch.setenv("ULG_LANE_NW", "2" if k.endswith("w2") else "1")
+        res[k] = ulg_ctx.score_all(list(range(n)), [(1 << n) - 1] * n, 6)
+    for k in ("1", "1w2"):
+        for a, b in zip(res["4"], res[k]):
+            assert a.tobytes() == b.tobytes(), k
