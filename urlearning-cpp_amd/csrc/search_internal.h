@@ -122,10 +122,22 @@ __device__ inline uint64_t bs_key_scan(const SearchDev &d, int v, uint64_t S) {
 
 // One read of the lattice when S lies inside the tables' scope (every stored
 // set that can be a subset of S is in the table), else the list scan.
+// pext over the set bits of x (x a subset of m): |x| steps instead of |m|
+__device__ inline uint64_t pext_sparse(uint64_t x, uint64_t m) {
+    uint64_t r = 0;
+    for (uint64_t y = x; y; y &= y - 1) r |= 1ull << __popcll(m & ((y & (0 - y)) - 1));
+    return r;
+}
+
 __device__ inline uint64_t bs_key(const SearchDev &d, int v, uint64_t S) {
     if (d.tables && (S & ~d.scope) == 0) {
         const uint64_t D = d.support[v];
-        return d.table[d.tb_off[v] + pext64(S & D, D)];
+        const uint64_t x = S & D;
+        const uint64_t all = (d.n >= 64) ? ~0ull : ((1ull << d.n) - 1ull);
+        const uint64_t lo = (1ull << v) - 1ull;
+        // D_v = every variable but v (a full skeleton): pext closes the hole at v
+        const uint64_t idx = D == (all & ~(1ull << v)) ? (((v < 63 ? (x >> (v + 1)) : 0ull) << v) | (x & lo)) : pext_sparse(x, D);
+        return d.table[d.tb_off[v] + idx];
     }
     return bs_key_scan(d, v, S);
 }
