@@ -250,9 +250,18 @@ int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, flo
         if (e == hipSuccess) e = hipMemcpyAsync(d_g0.p, &zero, 4, hipMemcpyHostToDevice, c->stream);
         if (e != hipSuccess) { cleanup(); return set_err(c, ULG_ERR_HIP, hipGetErrorString(e)); }
         float *gprev = d_g0.p, *gcur = d_g1.p;
+        // a skeleton complete on the component filters nothing (a non-empty
+        // P always meets the leaf's row) and leaves every subset connected:
+        // the launches skip the filter and the connectivity test
+        bool complete = true;
+        for (uint64_t x = edges ? comp : 0ull; x; x &= x - 1) {
+            const int b = __builtin_ctzll(x);
+            if (comp & ~(edges[b] | (1ull << b))) complete = false;
+        }
+        const int filt = edges && !complete ? 1 : 0;
         for (int d = 1; d <= m; ++d) {
             const uint64_t cnt = binom64(m, d);
-            LayerArgs a{dv, d_bn.p, d_cv.p, d_edges.p, edges ? 1 : 0, symmetric ? 1 : 0, m, d, cnt, gprev, gcur,
+            LayerArgs a{dv, d_bn.p, d_cv.p, d_edges.p, filt, symmetric && filt ? 1 : 0, m, d, cnt, gprev, gcur,
                         d_leaf.p + loff[d], d < m ? d_acc.p : nullptr};
             prof_begin(c, "search_layer_pull");
             layer_pull_kernel<<<(unsigned)((cnt + kB - 1) / kB), kB, 0, c->stream>>>(a);
