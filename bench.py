@@ -169,6 +169,10 @@ def search_metrics(ctx, cfg, variables, cands, rank, ws, reps=3, edges=None, ske
     t0 = _t.perf_counter()
     ctx.search_from_scores()
     t1 = _t.perf_counter()
+    tables_ms = 1e3 * (t1 - t0)
+    ctx.search_from_scores()  # again, with the 3.4 GB of C3 tables already allocated
+    tables_again_ms = 1e3 * (_t.perf_counter() - t1)
+    t1 = _t.perf_counter()
     ctx.pdb_build(2)
     t2 = _t.perf_counter()
     best = None
@@ -186,7 +190,8 @@ def search_metrics(ctx, cfg, variables, cands, rank, ws, reps=3, edges=None, ske
     out["gpu_search"] = {"config": f"{cfg['id'].upper()} lists (n={n}, k={k}), {skel_note}, static PDB(2)",
                          "expansions": g["expanded"], "ms": 1e3 * best,
                          "expansions_per_s": g["expanded"] / best, "goal_cost": g["cost"],
-                         "tables_ms": 1e3 * (t1 - t0), "pdb_ms": 1e3 * (t2 - t1),
+                         "tables_ms": tables_ms, "tables_rebuild_ms": tables_again_ms,
+                         "pdb_ms": 1e3 * (t2 - t1),
                          "note": "layer-synchronous pull over the whole order lattice; best of %d" % reps}
     if edges is None and pull is not None:
         out["gpu_search"]["roofline"] = search_roofline(cfg, n, pull, reps)
