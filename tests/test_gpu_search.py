@@ -70,14 +70,14 @@ def test_bestscore_tables_heterogeneous_supports(ulg_ctx, oracle_built):
         assert int(p) == ep, (v, S, p, ep)
 
 
-@pytest.mark.parametrize("n", [16, 25])
-def test_bestscore_big_tables_register_zeta(ulg_ctx, oracle_built, n):
+@pytest.mark.parametrize("n,k", [(16, 2), (25, 2), (20, 4)])
+def test_bestscore_big_tables_register_zeta(ulg_ctx, oracle_built, n, k):
     """Tables of >= 2^14 entries per variable take the sorted-entries tile
     build and the register-blocked subset-min (pass A for every m >= 14, pass
     B when a variable has 10 bits above bit 14: n = 25 gives m = 24)."""
     o = oracle_built
     X, _ = synth.gaussian_sem(n, 2000, 9303 + n)
-    offs, sets, scores, costs = _oracle_pipeline(o, X, 0.5, 2)
+    offs, sets, scores, costs = _oracle_pipeline(o, X, 0.5, k)
     ulg_ctx.search_load(offs, sets, costs)
     srch = o.Search(n, offs, sets, costs)
     rng = np.random.default_rng(n)
