@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/c3_oracle.json: the CPU oracle's command-line path
+at BASELINE config C3 (n=25, N=10k, k=6, lambda=2, full skeleton, seeded
+synthetic data synth.gaussian_sem(25, 10000, 9200)).
+
+  ref_score c3.csv c3.pss -f cBIC --lambda 2 -p 6 -t T   (score_main.cpp)
+  ref_astar c3.pss -n c3_net                             (astar_main.cpp)
+
+The fixture holds, per variable, the count and a SHA-256 of the stored
+parent sets (sorted uint64 masks), the sum of the printed scores, and the
+oracle's netFile / netFile.csv text with the goal cost and the expansion
+count.  tests/test_gpu_c3_dag.py checks the GPU pipeline against it.
+Runs in this container only (it needs oracle/build/ and a few minutes of
+CPU): python tests/golden/make_c3_fixture.py [workdir] [threads]
+"""
+import hashlib
+import json
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "urlearning-cpp_amd"))
+import numpy as np  # noqa: E402
+import synth  # noqa: E402
+
+N_VARS, N_ROWS, K, LAM, SEED = 25, 10000, 6, 2.0, 9200
+
+
+def pss_sets(path):
+    """Per variable: sorted stored parent masks and the sum of the printed
+    scores (score_main.cpp:173-203 layout; names are the CSV column indices
+    as the reference names header-less columns)."""
+    names, blocks, cur = [], [], None
+    with open(path) as f:
+        for line in f:
+            t = line.split()
+            if not t:
+                continue
+            if t[0] == "VAR":
+                names.append(t[1])
+                cur = []
+                blocks.append(cur)
+            elif t[0] == "META" or cur is None:
+                continue
+            else:
+                cur.append(t)
+    idx = {nm: i for i, nm in enumerate(names)}
+    out = []
+    for b in blocks:
+        masks = sorted(sum(1 << idx[p] for p in row[1:]) for row in b)
+        # each printed score read back as the float32 the GPU's quantize gives
+        out.append((masks, float(np.sum(np.array([row[0] for row in b], dtype=np.float32).astype(np.float64)))))
+    return out
+
+
+def sets_digest(masks):
+    return hashlib.sha256(np.asarray(masks, dtype=np.uint64).tobytes()).hexdigest()
+
+
+def main():
+    work = sys.argv[1] if len(sys.argv) > 1 else "/tmp/c3ref"
+    threads = sys.argv[2] if len(sys.argv) > 2 else str(os.cpu_count() or 8)
+    os.makedirs(work, exist_ok=True)
+    csv = os.path.join(work, "c3.csv")
+    pss = os.path.join(work, "c3_ref.pss")
+    net = os.path.join(work, "c3_ref_net")
+    if not os.path.exists(net):
+        X, _ = synth.gaussian_sem(N_VARS, N_ROWS, SEED)
+        synth.write_csv(csv, X)
+        b = os.path.join(ROOT, "oracle", "build")
+        subprocess.run([os.path.join(b, "ref_score"), csv, pss, "-f", "cBIC", "--lambda", str(LAM), "-p", str(K),
+                        "-t", threads], check=True)
+        subprocess.run([os.path.join(b, "ref_astar"), pss, "-n", net], check=True,
+                       stdout=open(os.path.join(work, "astar.log"), "w"))
+    log = open(os.path.join(work, "astar.log")).read()
+    cost = float(re.search(r"Found solution: (\S+)", log).group(1))
+    expanded = int(re.search(r"Nodes expanded: (\d+)", log).group(1))
+    ref_time = float(re.search(r"ref_astar: time=(\S+)s", log).group(1))
+    per_var = pss_sets(pss)
+    res = {"config": "C3: n=25, N=10000, k=6, lambda=2, full skeleton, synth.gaussian_sem(25, 10000, 9200)",
+           "generator": "tests/golden/make_c3_fixture.py (oracle/build/ref_score -t T, ref_astar)",
+           "stored_per_variable": [len(m) for m, _ in per_var],
+           "sets_sha256_per_variable": [sets_digest(m) for m, _ in per_var],
+           "printed_score_sum_per_variable": [s for _, s in per_var],
+           "goal_cost": cost, "expanded": expanded, "oracle_astar_seconds": ref_time,
+           "net_file": open(net).read(), "net_csv": open(net + ".csv").read()}
+    out = os.path.join(ROOT, "tests", "golden", "c3_oracle.json")
+    json.dump(res, open(out, "w"), indent=1)
+    print(f"wrote {out}: {sum(res['stored_per_variable'])} stored sets, cost {cost}, {expanded} expansions")
+
+
+if __name__ == "__main__":
+    main()

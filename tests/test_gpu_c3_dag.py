@@ -1,0 +1,46 @@
+"""BASELINE config C3 end to end against the CPU oracle's command-line path
+(north_star: "the optimal DAG identical to the CPU reference" at n=25,
+k<=6, N=10k).  tests/golden/c3_oracle.json holds what oracle/build/ref_score
+and ref_astar produced on the same seeded data (make_c3_fixture.py).  The
+GPU scorer must store the same parent sets for every variable (bit-exact
+index work, compared through per-variable SHA-256 digests of the sorted
+masks) with the same printed (%f) scores, and the exact-order A* over the
+GPU-built tables must write the oracle's netFile with the same goal cost and
+expansion count."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import synth
+
+pytestmark = pytest.mark.gpu
+
+FIXTURE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c3_oracle.json")
+
+
+@pytest.mark.timeout(600)
+def test_c3_pipeline_equals_oracle(ulg_ctx):
+    ref = json.load(open(FIXTURE))
+    n, N, k = 25, 10000, 6
+    X, _ = synth.gaussian_sem(n, N, 9200)
+    full = [(1 << n) - 1] * n
+    ulg_ctx.load(X, 2.0)
+    offs, sets, scores = ulg_ctx.score_all(list(range(n)), full, k)
+    printed = ulg_ctx.quantize(scores)
+    for v in range(n):
+        s = np.sort(sets[offs[v]:offs[v + 1]].astype(np.uint64))
+        assert len(s) == ref["stored_per_variable"][v], v
+        assert hashlib.sha256(s.tobytes()).hexdigest() == ref["sets_sha256_per_variable"][v], v
+        # a .pss line holds the cost, the negated stored score (the reader
+        # takes cost = -1 * atof, score_cache.cpp:135-159)
+        tot = -float(np.sum(printed[offs[v]:offs[v + 1]].astype(np.float64)))
+        want = ref["printed_score_sum_per_variable"][v]
+        assert abs(tot - want) <= 1e-12 * max(abs(want), 1.0), (v, tot, want)
+    ulg_ctx.search_from_scores()
+    res = ulg_ctx.astar(edges=full, mode=0, net_text=True)
+    assert np.float32(res["cost"]).tobytes() == np.float32(ref["goal_cost"]).tobytes()
+    assert res["expanded"] == ref["expanded"]
+    assert res["net_text"] == ref["net_file"]
