@@ -191,19 +191,35 @@ struct Heap {
     void adjust(int64_t hole, int64_t len, HeapEnt value) {
         const int64_t top = hole;
         int64_t second = hole;
+        // the moved nodes' pq writes are deferred (in order) behind write
+        // prefetches: nothing reads pq during the sift
+        uint32_t mv_idx[64];
+        int64_t mv_pos[64];
+        int nm = 0;
         while (second < (len - 1) / 2) {
+            // the grandchildren (4 contiguous entries): the heap outgrows the
+            // caches, and this descent is a chain of dependent loads
+            const int64_t gc = 4 * second + 3;
+            if (gc + 3 < len) {
+                __builtin_prefetch(&a[gc]);
+                __builtin_prefetch(&a[gc + 3]);
+            }
             second = 2 * (second + 1);
             if (cns(a[second], a[second - 1])) second--;
             a[hole] = a[second];
-            setpos(a[hole], hole);
+            __builtin_prefetch(&(*nodes)[a[hole].idx], 1);
+            mv_idx[nm] = a[hole].idx;
+            mv_pos[nm++] = hole;
             hole = second;
         }
         if ((len & 1) == 0 && second == (len - 2) / 2) {
             second = 2 * (second + 1);
             a[hole] = a[second - 1];
-            setpos(a[hole], hole);
+            mv_idx[nm] = a[hole].idx;
+            mv_pos[nm++] = hole;
             hole = second - 1;
         }
+        for (int i = 0; i < nm; ++i) (*nodes)[mv_idx[i]].pq = (int32_t)mv_pos[i];
         push_hole(hole, top, value);
     }
     uint32_t pop() {
