@@ -51,7 +51,14 @@ __global__ void __launch_bounds__(kB) layer_pull_kernel(LayerArgs a) {
     __shared__ uint64_t binom[33 * 33];
     __shared__ int cv[kMaxM];
     __shared__ uint64_t edg[64];
-    for (int i = threadIdx.x; i < 33 * 33; i += kB) binom[i] = a.binom[i];
+    // only the rows and columns this layer reads: C(c, i) for c < m, i <= layer
+    {
+        const int cols = a.layer + 1;
+        for (int e = threadIdx.x; e < a.m * cols; e += kB) {
+            const int r = e / cols, i = e - r * cols;
+            binom[r * 33 + i] = a.binom[r * 33 + i];
+        }
+    }
     for (int i = threadIdx.x; i < a.m; i += kB) cv[i] = a.comp_vars[i];
     if (a.symmetric)
         for (int i = threadIdx.x; i < 64; i += kB) edg[i] = a.edges[i];
