@@ -1,28 +1,42 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X cBIC-score hot path (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2] [--mode weak|shard]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4] [--mode shard|weak]
 
-One step = one full cBIC scoring pass (every parent set of size <= k of every
-variable through the layer-synchronous HIP scorer, stored-set rule and
-dominance recursion included) over inputs already resident in HBM.
+One step = one full cBIC scoring pass over one dataset (every parent set of
+size <= k of every variable through the layer-synchronous HIP scorer,
+stored-set rule and dominance recursion included) over inputs already
+resident in HBM.
 
---mode weak (default): every rank scores the whole configuration on its own
-    synthetic dataset (seed 9200 + rank): a batch of independent structure-
-    learning problems, per-GPU work fixed as N grows, no collective in the
-    data path.
---mode shard: one dataset, variables striped over ranks (score_main.cpp:136-139)
-    and the per-variable (set, score) lists exchanged with one RCCL
-    all_gather inside the timed step; strong scaling.
+--mode shard (default): SURVEY 8e.  The variables are balanced over the
+    ranks by the parent sets each one scores (shard.assign), every rank
+    scores its share, and the per-variable (set, score) lists are exchanged
+    with ONE all-gather (RCCL over xGMI) inside the timed step
+    (shard.ListExchange).  After the timed region every rank builds its own
+    best-score tables and pattern database from the gathered lists and runs
+    the GPU order-graph search (A* is replicas-only); the exchange,
+    table build and search are reported separately.  Strong scaling: the
+    job's work is fixed as N grows.  At N = 1 there is no exchange.
+--mode weak: every rank scores the whole configuration on its own synthetic
+    dataset (seed 9200 + rank), no collective in the data path.
+
+--gpus N > 1 without WORLD_SIZE in the environment starts N worker processes
+(one per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR=127.0.0.1 set) before
+anything touches the GPU and exits with their status; under
+torch.distributed.run the ranks come from the environment and --gpus must
+agree with WORLD_SIZE.
 
 Rank 0 prints one JSON line.  cpu_baseline = the CPU oracle (a faithful C
 restatement that solves each OLS over all N rows like the reference) timed on
 a bounded sample on this host, rank 0 at N=1 only.
 """
 import argparse
+import hashlib
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -40,8 +54,9 @@ CONFIGS = {
     "c2": dict(n=20, N=10000, k=4, lam=2.0),
     "c3": dict(n=25, N=10000, k=6, lam=2.0),
     # BASELINE C4: n=30, N=100k, MMPC skeleton (built on the GPU from the same
-    # data, alpha 0.01), 2-hop candidate sets; k capped at the HIP scorer's 8
-    "c4": dict(n=30, N=100000, k=8, lam=2.0, skeleton="mmpc", alpha=0.01),
+    # data, alpha 0.01), 2-hop candidate sets, the reference's default parent
+    # limit -p = n - 1 (score_main.cpp:296-298): layers 9..18 run the wide kernels
+    "c4": dict(n=30, N=100000, k=29, lam=2.0, skeleton="mmpc", alpha=0.01),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
@@ -71,13 +86,14 @@ def cpu_baseline(cfg, X, target_s=15.0):
     t0 = time.perf_counter()
     c = oracle.score_sample(ds, lam, variables, cands, k, frac, threads)
     dt = time.perf_counter() - t0
-    return {"value": c / dt, "unit": "parent-set scores/s", "cores": threads, "kind": "port",
+    return {"value": c / dt, "unit": "parent-set scores/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
             "sample": f"CPU oracle (C restatement, per-set OLS over all N rows) on {nvars} of {n} variables, "
                       f"first {frac:.4f} of every layer 1..{k} in Gosper order: {c} parent sets in {dt:.2f} s "
                       f"on {threads} threads"}
 
 
-PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1", "pmc_traffic.json")
+PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r2")
+PMC_TRAFFIC = os.path.join(PROFILES, "pmc_traffic.json")
 
 
 def pmc_traffic(cfg, sets, label):
@@ -91,7 +107,7 @@ def pmc_traffic(cfg, sets, label):
     if (t.get("config_id") != cfg["id"] or round(t.get("sets_per_launch", -1)) != round(sets)
             or t.get("label") != label):
         return None, None
-    return t["traffic_bytes_per_launch"], "profiles/r1/pmc_traffic.json"
+    return t["traffic_bytes_per_launch"], "profiles/r2/pmc_traffic.json"
 
 
 def roofline(ctx, cfg, per_layer_sets, steps):
@@ -128,50 +144,57 @@ def roofline(ctx, cfg, per_layer_sets, steps):
              "fp64_tflops": sets * flops_per_set / (p["avg_ms"] * 1e-3) / 1e12}, p)
 
 
-PMC_SEARCH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1", "pmc_search_traffic.json")
+PMC_SEARCH = os.path.join(PROFILES, "pmc_search_traffic.json")
 
 
 def search_roofline(cfg, n, pull, reps):
     """Roofline of the GPU order-graph sweep (layer_pull_kernel, one launch
     per layer) on a full skeleton: a layer-L node reads L predecessors' g
-    (4 B) and best-score keys (8 B) and writes its g (4 B) and leaf (1 B), so
-    one sweep's algorithmic bytes are sum_L C(n, L) (12 L + 5).  The achieved
-    rate divides them by the sweep's summed kernel time (HIP events on the
-    launch stream); traffic is the PMC-measured bytes of one sweep."""
+    (4 B) and best-score costs (4 B, the 32-bit lattice) and writes its g
+    (4 B) and leaf (1 B), so one sweep's algorithmic bytes are
+    sum_L C(n, L) (8 L + 5).  The achieved rate divides them by the sweep's
+    summed kernel time (HIP events on the launch stream); traffic is the
+    PMC-measured bytes of one sweep."""
     cnt, sweep_ms = pull["count"], pull["total_ms"] / reps
-    algo = sum(math.comb(n, L) * (12 * L + 5) for L in range(1, n + 1))
+    algo = sum(math.comb(n, L) * (8 * L + 5) for L in range(1, n + 1))
     achieved = algo / (sweep_ms * 1e-3) / 1e9
     traffic, src = None, None
     try:
         t = json.load(open(PMC_SEARCH))
         if t.get("config_id") == cfg["id"] and t.get("n") == n:
-            traffic, src = t["traffic_bytes_per_sweep"], "profiles/r1/pmc_search_traffic.json"
+            traffic, src = t["traffic_bytes_per_sweep"], "profiles/r2/pmc_search_traffic.json"
     except (OSError, ValueError):
         pass
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per sweep",
             "traffic_source": src, "kernel": "layer_pull_kernel", "launches_per_sweep": cnt // reps,
             "sweep_kernel_ms": sweep_ms, "algorithmic_bytes_per_sweep": algo,
-            "bytes_per_node": "12 L + 5 (L predecessors x (4 B g + 8 B key) + 4 B g + 1 B leaf written)"}
+            "bytes_per_node": "8 L + 5 (L predecessors x (4 B g + 4 B best-score cost) + 4 B g + 1 B leaf written)"}
 
 
-def search_metrics(ctx, cfg, variables, cands, rank, ws, reps=3, edges=None, skel_note="full skeleton"):
-    """Order-graph search side on this rank's scored lists: GPU best-score
-    tables + pattern database + GPU layer-synchronous search at the bench
-    config (A* expansions/s), then the exact-order A* (reference pop order,
-    bit-exact DAG) and the CPU oracle's A* on config C2 (rank 0, N=1 only)."""
+def search_metrics(ctx, cfg, variables, cands, rank, ws, reps=3, edges=None, skel_note="full skeleton",
+                   loaded=False):
+    """Order-graph search side: GPU best-score tables + pattern database +
+    the GPU layer-synchronous search at the bench config (time to the optimal
+    order cost; it settles every lattice node, so its rate is lattice nodes/s,
+    not A* expansions), then the exact-order A* (the reference's pop order,
+    bit-exact DAG; true A* expansions/s) and the CPU oracle's A* on config C2
+    (rank 0, N=1 only).  loaded: the lists are already in the search state
+    (ulg_search_load_scores after the exchange)."""
     import time as _t
     n, k = cfg["n"], cfg["k"]
     full = [(1 << n) - 1] * n
     skel = full if edges is None else edges
     out = {}
-    ctx.score(list(range(n)), full if edges is None else ulg.candidates_from_edges(edges, n), k)
-    t0 = _t.perf_counter()
-    ctx.search_from_scores()
-    t1 = _t.perf_counter()
-    tables_ms = 1e3 * (t1 - t0)
-    ctx.search_from_scores()  # again, with the 3.4 GB of C3 tables already allocated
-    tables_again_ms = 1e3 * (_t.perf_counter() - t1)
+    tables_ms = tables_again_ms = None
+    if not loaded:
+        ctx.score(list(range(n)), full if edges is None else ulg.candidates_from_edges(edges, n), k)
+        t0 = _t.perf_counter()
+        ctx.search_from_scores()
+        tables_ms = 1e3 * (_t.perf_counter() - t0)
+        t1 = _t.perf_counter()
+        ctx.search_from_scores()  # again, with the tables already allocated (3.4 GB at C3)
+        tables_again_ms = 1e3 * (_t.perf_counter() - t1)
     t1 = _t.perf_counter()
     ctx.pdb_build(2)
     t2 = _t.perf_counter()
@@ -188,11 +211,12 @@ def search_metrics(ctx, cfg, variables, cands, rank, ws, reps=3, edges=None, ske
     pull = ctx.profile_get("search_layer_pull")
     ctx.profile(False)
     out["gpu_search"] = {"config": f"{cfg['id'].upper()} lists (n={n}, k={k}), {skel_note}, static PDB(2)",
-                         "expansions": g["expanded"], "ms": 1e3 * best,
-                         "expansions_per_s": g["expanded"] / best, "goal_cost": g["cost"],
+                         "lattice_nodes": g["expanded"], "time_to_optimal_cost_ms": 1e3 * best,
+                         "lattice_nodes_per_s": g["expanded"] / best, "goal_cost": g["cost"],
                          "tables_ms": tables_ms, "tables_rebuild_ms": tables_again_ms,
                          "pdb_ms": 1e3 * (t2 - t1),
-                         "note": "layer-synchronous pull over the whole order lattice; best of %d" % reps}
+                         "note": "layer-synchronous pull over the whole order lattice (every node settled, "
+                                 "so nodes/s is not an A* expansion rate); best of %d" % reps}
     if edges is None and pull is not None:
         out["gpu_search"]["roofline"] = search_roofline(cfg, n, pull, reps)
     if rank == 0 and ws == 1:
@@ -218,19 +242,60 @@ def search_metrics(ctx, cfg, variables, cands, rank, ws, reps=3, edges=None, ske
         r = srch.astar(edges=full2)
         dt = _t.perf_counter() - ts
         out["cpu_baseline"] = {"value": r["expanded"] / dt, "unit": "A* expansions/s", "cores": 1, "kind": "port",
+                               "cpu": cpu_model(),
                                "sample": f"CPU oracle A* (sorted-list scans, reference heap) on C2: "
                                          f"{r['expanded']} expansions in {dt:.2f} s",
                                "same_dag_as_exact": [int(x) for x in r["vpar"]] == [int(x) for x in e["vpar"]]}
     return out
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n):
+    """--gpus N without a launcher: one worker process per GPU, started before
+    this process touches the GPU; returns the worst exit status."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc != 0), 0)
+
+
+def lists_digest(offsets, sets, scores):
+    """SHA-256 over (offsets, sets, score bits) of the gathered lists."""
+    h = hashlib.sha256()
+    h.update(np.asarray(offsets, dtype=np.int64).tobytes())
+    h.update(np.asarray(sets).view(np.uint64).tobytes())
+    h.update(np.asarray(scores, dtype=np.float32).tobytes())
+    return h.hexdigest()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="GPUs (ranks); default 1, or WORLD_SIZE under a launcher")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--mode", default="weak", choices=["weak", "shard"])
+    ap.add_argument("--mode", default="shard", choices=["shard", "weak"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-search", action="store_true")
     ap.add_argument("--score-variant", type=int, default=None, help="A/B knob (ulg_set_option score_variant)")
@@ -239,7 +304,11 @@ def main():
     ap.add_argument("--device", type=int, default=None, help="GPU for every rank (default LOCAL_RANK)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(spawn_ranks(args.gpus))
     ws, rank, local = dist_env()
+    if args.gpus is not None and args.gpus != ws:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}")
     cfg = dict(CONFIGS[args.config], id=args.config)
     n, N, k, lam = cfg["n"], cfg["N"], cfg["k"], cfg["lam"]
 
@@ -252,6 +321,9 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group(args.dist_backend, rank=rank, world_size=ws)
+        ws = dist.get_world_size()
+    else:
+        torch.cuda.set_device(local)
 
     seed = 9200 + (rank if args.mode == "weak" else 0)
     X, _ = synth.gaussian_sem(n, N, seed)
@@ -261,38 +333,40 @@ def main():
     ctx.load(X, lam)
     cands_all = [(1 << n) - 1] * n
     skel_note = "full n x n skeleton"
+    rows = None
     if cfg.get("skeleton") == "mmpc":
         rows = ctx.mmpc(cfg["alpha"])
         cands_all = ulg.candidates_from_edges(rows, n)
         skel_note = (f"MMPC skeleton (ulg_mmpc, alpha {cfg['alpha']}: {sum(bin(r).count('1') for r in rows) // 2} "
                      f"edges), 2-hop candidate sets")
+    ex = None
     if args.mode == "shard":
-        variables = shard.stripe(n, ws, rank)
+        parts = shard.assign(n, ws, cands_all, k)
+        variables = parts[rank]
+        if ws > 1:
+            ex = shard.ListExchange(n, parts, cands_all, k, rank, device="cuda", comm_device=cdev)
     else:
         variables = list(range(n))
     cands = [cands_all[v] for v in variables]
+    units_rank = sum(shard.var_weight(n, v, cands_all[v], k) for v in variables)
     msz = [bin(cands_all[v] & ~(1 << v)).count("1") for v in range(n)]
-    units_rank = sum(sum(math.comb(msz[v], L) for L in range(k + 1)) for v in variables)
 
     def step():
         stored, scored = ctx.score(variables, cands, k)
-        if args.mode == "shard" and ws > 1:
-            # one RCCL all-gather of the per-variable (set, score) lists (shard.py)
-            sets_t = torch.empty(max(stored, 1), dtype=torch.int64, device="cuda")
-            sc_t = torch.empty(max(stored, 1), dtype=torch.float32, device="cuda")
-            off_t = torch.empty(len(variables) + 1, dtype=torch.int64, device="cuda")
-            ctx.fetch_device(sets_t.data_ptr(), sc_t.data_ptr(), off_t.data_ptr())
-            shard.allgather_lists(shard.pack_device(variables, off_t, sets_t, sc_t).to(cdev), ws)
+        if ex is not None:
+            ex.fill(ctx, stored)
+            ex.allgather()  # the one collective of the data path
         return scored
 
     for _ in range(args.warmup):
         step()
     # HIP events in the timed region only around the roofline unit's kernels
     # (two host-side event records per timed kernel would otherwise show up in
-    # a ~2 ms step of ~35 launches); the full per-kernel breakdown comes from
-    # one extra profiled step after the timed region
+    # a ~1.5 ms step of ~35 launches); the full per-kernel breakdown comes from
+    # one extra profiled step after it
+    kk = min(k, max(msz[v] for v in variables)) if variables else k
     ctx.profile(True)
-    ctx.profile_select([f"score_layer_{k}_rest", f"walk_{k}_rest"])
+    ctx.profile_select([f"score_layer_{kk}_rest", f"walk_{kk}_rest"])
     ctx.profile_reset()
     if dist:
         dist.barrier()
@@ -318,8 +392,8 @@ def main():
         scored_all = float(scored_total)
 
     # sets in one launch of the dominant kernel (layer k, sets without variable 0)
-    per_launch = sum(math.comb(msz[v] - (1 if (v != 0 and cands_all[v] & 1) else 0), k) for v in variables)
-    roof, _ = roofline(ctx, cfg, per_launch, args.steps)
+    per_launch = sum(math.comb(msz[v] - (1 if (v != 0 and cands_all[v] & 1) else 0), kk) for v in variables)
+    roof, _ = roofline(ctx, dict(cfg, k=kk), per_launch, args.steps)
     ctx.profile(True)
     ctx.profile_select(None)
     ctx.profile_reset()
@@ -327,10 +401,35 @@ def main():
     kernels = ctx.profile_dump()
     ctx.profile(False)
 
+    # split of the sharded step, measured after the timed region: scoring
+    # alone vs scoring + exchange (synchronised, so not part of `value`)
+    split = None
+    if ex is not None:
+        ts_score, ts_ex = [], []
+        for _ in range(max(3, min(args.steps, 10))):
+            if dist:
+                dist.barrier()
+            torch.cuda.synchronize()
+            a = time.perf_counter()
+            stored, _ = ctx.score(variables, cands, k)
+            ex.fill(ctx, stored)
+            torch.cuda.synchronize()
+            b = time.perf_counter()
+            ex.allgather()
+            torch.cuda.synchronize()
+            c = time.perf_counter()
+            ts_score.append(b - a)
+            ts_ex.append(c - b)
+        split = {"score_ms": 1e3 * float(np.median(ts_score)), "exchange_ms": 1e3 * float(np.median(ts_ex)),
+                 "exchange_bytes_per_rank": ex.block, "exchange_bytes_total": ex.block * ws,
+                 "block_capacity_sets": ex.cap,
+                 "note": "medians of synchronised steps after the timed region (rank-local clocks)"}
+
     search = None
-    if args.mode == "weak" and not args.no_search:
-        search = search_metrics(ctx, cfg, variables, cands, rank, ws,
-                                edges=rows if cfg.get("skeleton") == "mmpc" else None, skel_note=skel_note)
+    if args.mode == "shard" and not args.no_search:
+        search = sharded_search(ctx, cfg, ex, variables, cands, rows, skel_note, rank, ws, dist, cdev, torch)
+    elif args.mode == "weak" and not args.no_search:
+        search = search_metrics(ctx, cfg, variables, cands, rank, ws, edges=rows, skel_note=skel_note)
 
     if rank == 0:
         res = {
@@ -348,21 +447,70 @@ def main():
             "data": f"synthetic: seeded linear-Gaussian SEM (synth.gaussian_sem, seed "
                     f"{'9200+rank' if args.mode == 'weak' else '9200, one dataset'}), {skel_note}",
             "config": {"workload": f"{args.config.upper()} cBIC scoring: n={n}, N={N}, max-parents k={k}, "
-                                   f"lambda={lam}, {skel_note}, all {n} variables per "
-                                   f"{'GPU' if args.mode == 'weak' else 'job'}",
+                                   f"lambda={lam}, {skel_note}, "
+                                   + (f"all {n} variables per GPU" if args.mode == "weak" else
+                                      f"{n} variables balanced over {ws} GPU(s), one all-gather of the lists"),
                        "config_id": args.config, "mode": args.mode,
+                       "parallelism": f"variable shard x{ws}" if args.mode == "shard" else f"replicas x{ws}",
                        "parent_sets_per_step_per_rank": units_rank},
             "roofline": roof,
-            "kernel_ms_one_step": {kk: round(vv["total_ms"], 4) for kk, vv in kernels.items()},
+            "kernel_ms_one_step": {kk2: round(vv["total_ms"], 4) for kk2, vv in kernels.items()},
         }
+        if split is not None:
+            res["shard_step"] = split
         if search is not None:
             res["astar"] = search
         if ws == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(cfg, X)
-        print(json.dumps(res))
+        print(json.dumps(res), flush=True)
     ctx.close()
     if dist:
         dist.destroy_process_group()
+
+
+def sharded_search(ctx, cfg, ex, variables, cands, rows, skel_note, rank, ws, dist, cdev, torch):
+    """After the exchange: every rank holds every variable's list, builds its
+    own best-score tables and pattern database and runs the GPU order-graph
+    search (replicas).  Ranks must agree on the lists (digest) and
+    the goal cost."""
+    n = cfg["n"]
+    if ex is not None:
+        stored, _ = ctx.score(variables, cands, cfg["k"])
+        ex.fill(ctx, stored)
+        ex.allgather()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        offsets, sets_t, scores_t = ex.assemble(device="cuda")
+        t1 = time.perf_counter()
+
+        def load():
+            ctx.search_load_scores(offsets, sets_t.data_ptr(), scores_t.data_ptr(), device_ptrs=True)
+        digest = lists_digest(offsets, sets_t.cpu().numpy(), scores_t.cpu().numpy())
+    else:
+        stored, _ = ctx.score(variables, cands, cfg["k"])
+        offs, sets, scores = ctx.fetch(stored)
+        t0 = t1 = time.perf_counter()
+
+        def load():
+            ctx.search_load_scores(offs, sets, scores, device_ptrs=False)
+        digest = lists_digest(offs, sets, scores)
+    ta = time.perf_counter()
+    load()
+    tb = time.perf_counter()
+    load()  # again, with the tables already allocated (3.4 GB at C3)
+    tc = time.perf_counter()
+    out = search_metrics(ctx, cfg, variables, cands, rank, ws, edges=rows, skel_note=skel_note, loaded=True)
+    out["gpu_search"].update(assemble_ms=1e3 * (t1 - t0), tables_ms=1e3 * (tb - ta), tables_rebuild_ms=1e3 * (tc - tb))
+    out["lists_sha256"] = digest
+    if dist:
+        # every rank must hold the same lists and find the same goal cost
+        h = torch.tensor([int(digest[:15], 16), int(np.float32(out["gpu_search"]["goal_cost"]).view(np.int32))],
+                         dtype=torch.int64, device=cdev)
+        lo, hi = h.clone(), h.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        out["ranks_agree"] = bool(torch.equal(lo, hi))
+    return out
 
 
 if __name__ == "__main__":

@@ -147,6 +147,16 @@ int ulg_search_load(ulg_ctx *ctx, int n, const int64_t *offsets,
  * (every variable must have been scored); costs go through the device
  * "%f" round trip (ulg_quantize_costs), lists stay on the device. */
 int ulg_search_from_scores(ulg_ctx *ctx);
+/* Same from per-variable lists of .pss scores (not yet costs) in variable
+ * order -- what the multi-GPU exchange hands every rank (one
+ * all-gather of the per-variable lists, then local tables).  offsets[n+1] is
+ * a host array (variable v owns [offsets[v], offsets[v+1]) of sets/scores);
+ * device_ptrs = 1: sets and scores are device pointers on this context's GPU
+ * (e.g. the all-gather's output tensor), 0: host pointers.  Scores go
+ * through the device "%f" round trip like ulg_search_from_scores. */
+int ulg_search_load_scores(ulg_ctx *ctx, int n, const int64_t *offsets,
+                           const uint64_t *sets, const float *scores,
+                           int device_ptrs);
 /* SparseParentList::getScore / getParents for count (variable, S) pairs:
  * the cost of the first (cost, file-order) stored set that is a subset of
  * S, or FLT_MAX if none; parents[i] gets that set (0 if none). */
@@ -240,8 +250,21 @@ int ulg_triplet_memo_put(ulg_ctx *ctx, const uint64_t *clusters, int64_t nc,
  * streams; "score_small_layers" (0..8, default 4): layers up to this size run
  * one one-pass launch per phase over all variables on one stream (they are
  * latency-bound), larger ones the two-pass form per group.
+ * "time_limit_ms" (default 0 = none): the reference's -r running-time budget
+ * (score: per calculateScores call, score_calculator.cpp:33-52,78,91; astar:
+ * a watchdog over the search, astar_main.cpp:135-138,266,696-706).  The GPU
+ * scorer checks it after every complete layer (it synchronises the scoring
+ * streams there, so only set it when a budget is wanted) and keeps the layers
+ * finished so far -- the reference stops mid-layer, at a point that depends
+ * on its clock; the exact-order A* checks it every 4096 pops and stops
+ * without a goal for that component, as the reference's loop does.
  * All variants compute identical results; the knob exists for A/B timing. */
 int ulg_set_option(ulg_ctx *ctx, const char *name, int64_t value);
+/* Read-back of per-call state: "out_of_time" (1 if the last ulg_cbic_score or
+ * ulg_astar* ran out of time_limit_ms), "highest_completed_layer" (the
+ * reference's ScoreCalculator::highestCompletedLayer of the last scoring call,
+ * score_calculator.h:45). */
+int ulg_get_info(ulg_ctx *ctx, const char *name, int64_t *value);
 
 /* ---- profiling (per-kernel HIP-event timing on the context stream) ---- */
 int ulg_profile_enable(ulg_ctx *ctx, int on);

@@ -22,6 +22,7 @@
 //     enumeration index), holding the stored score or an absent sentinel.
 #include <cstdio>
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 
@@ -2140,7 +2141,11 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     const int Ls = (variant & 16) && !(variant & 8) && !wck ? std::min(kmax, std::min(kMaxL, c->score_small_layers)) : 0;
     const int vsmall = variant & 1;
     bool forked = false;
-    for (int L = 1; L <= kmax; ++L)
+    // -r (score_calculator.cpp:33-52,78): checked after every complete layer
+    const auto t_call = std::chrono::steady_clock::now();
+    c->out_of_time = 0;
+    int done_L = kmax;
+    for (int L = 1; L <= kmax; ++L) {
         for (int ph = 0; ph < 2; ++ph) {
             if (L <= Ls) {
                 const size_t wo = ((size_t)L * 2 + ph) * (nv + 1);
@@ -2277,6 +2282,17 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
                 }
             }
         }
+        if (c->time_limit_ms > 0 && L < kmax) {
+            for (int g = 0; g < (forked ? G : 1); ++g) ULG_HIP(c, hipStreamSynchronize(gst[g]));
+            const double ms =
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call).count();
+            if (ms > (double)c->time_limit_ms) {
+                done_L = L;
+                c->out_of_time = 1;
+                break;
+            }
+        }
+    }
     // join: the compaction on the context stream waits for every group
     for (int g = 1; g < G && forked; ++g) {
         ULG_HIP(c, hipEventRecord(c->sync_events[g], gst[g]));
@@ -2284,6 +2300,16 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     }
     ULG_HIP(c, hipGetLastError());
 
+    if (done_L < kmax) {
+        // out of time: the layers never launched hold no stored set
+        scored = 0;
+        for (int i = 0; i < nv; ++i) {
+            const uint64_t b = toff[(size_t)i * S + done_L + 1], e = toff[(size_t)i * S + S];
+            if (e > b) ULG_HIP(c, hipMemsetAsync(c->table.p + b, 0xff, (size_t)(e - b) * 4, c->stream));
+            for (int L = 0; L <= done_L; ++L) scored += (int64_t)(toff[(size_t)i * S + L + 1] - toff[(size_t)i * S + L]);
+        }
+    }
+    c->completed_layer = done_L;
     // compaction
     const int64_t nb = (int64_t)((total_slots + kSlotsPerBlock - 1) / kSlotsPerBlock);
     if ((rc = ensure(c, c->d_blk, (size_t)nb + 1))) return rc;

@@ -8,13 +8,17 @@
 // BestScore table (replaces the sorted-list linear scan): for variable v with
 // parent-set support D_v (union of its stored sets, m_v = |D_v|), a dense
 // table over all 2^m_v subsets S of D_v holds
-//     key(S) = min over stored sets P subset of S of (ordered(cost_P) << 32 | file_index_P)
-// i.e. exactly the first entry of the list sorted by (cost, file order) that
-// is a subset of S (SparseParentList with the pinned N7 tie-break).  It is
-// filled by a scatter of the stored sets and an in-place subset-min ("zeta")
-// transform: bits 0..13 inside 128 KiB LDS tiles, the remaining bits in a
-// second pass over strided tiles whose rows are 16 contiguous entries.  Both
-// passes stream the table once (HBM-bound).  Lookup: key = T_v[pext(S, D_v)].
+//     T_v(S) = min over stored sets P subset of S of ordkey(cost_P)
+// (4 B per entry), i.e. the cost of the first entry of the list sorted by
+// (cost, file order) that is a subset of S -- what SparseParentList::getScore
+// returns.  getParents (the file index behind the min) is needed only for
+// the few reconstruction queries; those scan the list with the pinned N7
+// (cost, file order) tie-break (bs_key_scan), which finds a set of exactly
+// this cost.  The table is filled by a scatter of the stored sets and an
+// in-place subset-min ("zeta") transform: bits 0..13 inside LDS tiles, the
+// remaining bits in a second pass over strided tiles whose rows are 16
+// contiguous entries.  Both passes stream the table once (HBM-bound).
+// Lookup: cost = ord_cost(T_v[pext(S, D_v)]).
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -29,9 +33,9 @@ using namespace ulg;
 namespace {
 
 constexpr int kB = 256;
-constexpr int kTileBits = 14;  // pass A: 2^14 u64 = 128 KiB LDS
-constexpr int kRowBits = 4;    // pass B rows: 16 contiguous u64 = 128 B
-constexpr int kColBits = 10;   // pass B: 2^10 rows x 16 = 2^14 u64
+constexpr int kTileBits = 14;  // pass A: 2^14 u32 = 64 KiB LDS
+constexpr int kRowBits = 4;    // pass B rows: 16 contiguous u32 = 64 B
+constexpr int kColBits = 10;   // pass B: 2^10 rows x 16 = 2^14 u32
 
 // D_v = union of v's stored sets inside scope (variables outside scope get
 // D_v = {} and a one-entry table)
@@ -50,22 +54,22 @@ __global__ void __launch_bounds__(kB) support_kernel(const uint64_t *sets, const
 
 __global__ void __launch_bounds__(kB) scatter_kernel(const uint64_t *sets, const float *costs, const int64_t *offsets,
                                                      int n, const uint64_t *support, const uint64_t *tb_off,
-                                                     uint64_t *table) {
+                                                     uint32_t *table) {
     const int v = blockIdx.y;
     const int64_t b = offsets[v], e = offsets[v + 1];
     const uint64_t D = support[v];
     for (int64_t i = b + (int64_t)blockIdx.x * kB + threadIdx.x; i < e; i += (int64_t)gridDim.x * kB) {
         if (sets[i] & ~D) continue;  // outside the scope
         const uint64_t idx = pext64(sets[i], D);
-        table[tb_off[v] + idx] = ((uint64_t)ordkey(costs[i]) << 32) | (uint64_t)(i - b);
+        table[tb_off[v] + idx] = ordkey(costs[i]);  // stored sets are distinct: one writer per slot
     }
 }
 
 // pass A: all subset bits inside a contiguous tile of 2^T entries.
-__global__ void __launch_bounds__(1024) zeta_tile_kernel(uint64_t *table, const uint64_t *tb_off, const int *tiles_prefix,
+__global__ void __launch_bounds__(1024) zeta_tile_kernel(uint32_t *table, const uint64_t *tb_off, const int *tiles_prefix,
                                                          const int *mbits, int nvar) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint64_t *t = reinterpret_cast<uint64_t *>(smem);
+    uint32_t *t = reinterpret_cast<uint32_t *>(smem);
     // which variable / tile
     int lo = 0, hi = nvar;
     while (hi - lo > 1) {
@@ -83,7 +87,7 @@ __global__ void __launch_bounds__(1024) zeta_tile_kernel(uint64_t *table, const 
         const uint64_t bit = 1ull << b;
         for (uint64_t p = threadIdx.x; p < (size >> 1); p += 1024) {
             const uint64_t i = ((p >> b) << (b + 1)) | (p & (bit - 1));
-            const uint64_t a = t[i], c = t[i | bit];
+            const uint32_t a = t[i], c = t[i | bit];
             if (a < c) t[i | bit] = a;
         }
         __syncthreads();
@@ -93,7 +97,7 @@ __global__ void __launch_bounds__(1024) zeta_tile_kernel(uint64_t *table, const 
 
 // pass B: bits [bit_lo, bit_lo + G) over tiles of 2^G rows x 16 contiguous entries.
 struct ZetaBArgs {
-    uint64_t *table;
+    uint32_t *table;
     const uint64_t *tb_off;
     const int *blocks_prefix;
     const int *mbits;
@@ -102,7 +106,7 @@ struct ZetaBArgs {
 };
 __global__ void __launch_bounds__(1024) zeta_strided_kernel(ZetaBArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint64_t *t = reinterpret_cast<uint64_t *>(smem);
+    uint32_t *t = reinterpret_cast<uint32_t *>(smem);
     int lo = 0, hi = a.nvar;
     while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
@@ -116,7 +120,7 @@ __global__ void __launch_bounds__(1024) zeta_strided_kernel(ZetaBArgs a) {
     const uint64_t bid = blockIdx.x - a.blocks_prefix[v];
     // tile origin inside v's table; v's table itself starts at tb_off[v], which
     // is not aligned to 2^m when the supports differ in size: add, never OR
-    uint64_t *tv = a.table + a.tb_off[v];
+    uint32_t *tv = a.table + a.tb_off[v];
     const uint64_t base = ((bid & ((1ull << nlow) - 1)) << kRowBits) | ((bid >> nlow) << (bit_lo + G));
     const int rows = 1 << G;
     const int size = rows << kRowBits;
@@ -130,7 +134,7 @@ __global__ void __launch_bounds__(1024) zeta_strided_kernel(ZetaBArgs a) {
             const int lw = p & 15, q = p >> 4;  // q indexes rows with bit j clear
             const int r0 = ((q >> j) << (j + 1)) | (q & ((1 << j) - 1));
             const int i0 = (r0 << kRowBits) | lw, i1 = ((r0 | (1 << j)) << kRowBits) | lw;
-            const uint64_t x = t[i0], y = t[i1];
+            const uint32_t x = t[i0], y = t[i1];
             if (x < y) t[i1] = x;
         }
         __syncthreads();
@@ -153,7 +157,7 @@ constexpr int kPadLds = (1 << kRegTileBits) + (1 << (kRegTileBits - 4));
 
 __device__ __forceinline__ int padx(int e) { return e + (e >> 4); }
 
-__device__ __forceinline__ void min4(uint64_t (&r)[16]) {
+__device__ __forceinline__ void min4(uint32_t (&r)[16]) {
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
@@ -164,18 +168,18 @@ __device__ __forceinline__ void min4(uint64_t (&r)[16]) {
 // one (global table index, packed key) per stored set inside the tables' scope
 __global__ void __launch_bounds__(kB) entries_kernel(const uint64_t *sets, const float *costs, const int64_t *offsets,
                                                      int n, const uint64_t *support, const uint64_t *tb_off,
-                                                     uint64_t *idx, uint64_t *key) {
+                                                     uint64_t *idx, uint32_t *key) {
     const int v = blockIdx.y;
     const int64_t b = offsets[v], e = offsets[v + 1];
     const uint64_t D = support[v];
     for (int64_t i = b + (int64_t)blockIdx.x * kB + threadIdx.x; i < e; i += (int64_t)gridDim.x * kB) {
         if (sets[i] & ~D) {
             idx[i] = ~0ull;  // outside the scope: sorts past every slot
-            key[i] = ~0ull;
+            key[i] = 0xFFFFFFFFu;
             continue;
         }
         idx[i] = tb_off[v] + pext64(sets[i], D);
-        key[i] = ((uint64_t)ordkey(costs[i]) << 32) | (uint64_t)(i - b);
+        key[i] = ordkey(costs[i]);
     }
 }
 
@@ -190,11 +194,11 @@ __device__ __forceinline__ int64_t lower_bound_u64(const uint64_t *a, int64_t n,
 
 // pass A for tables of >= 2^14 entries: builds each tile from its sorted
 // entries (no fill, no read of the table) and writes it once
-__global__ void __launch_bounds__(1024) zeta_tile_reg_kernel(uint64_t *table, uint64_t ntiles_total,
-                                                             const uint64_t *eidx, const uint64_t *ekey,
+__global__ void __launch_bounds__(1024) zeta_tile_reg_kernel(uint32_t *table, uint64_t ntiles_total,
+                                                             const uint64_t *eidx, const uint32_t *ekey,
                                                              int64_t nent) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint64_t *t = reinterpret_cast<uint64_t *>(smem);
+    uint32_t *t = reinterpret_cast<uint32_t *>(smem);
     __shared__ int64_t range[2];
     const int tid = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x << kRegTileBits;  // tiles are contiguous over all variables
@@ -202,11 +206,11 @@ __global__ void __launch_bounds__(1024) zeta_tile_reg_kernel(uint64_t *table, ui
         range[0] = lower_bound_u64(eidx, nent, base);
         range[1] = lower_bound_u64(eidx, nent, base + (1ull << kRegTileBits));
     }
-    for (int i = tid; i < (1 << kRegTileBits); i += 1024) t[padx(i)] = ~0ull;
+    for (int i = tid; i < (1 << kRegTileBits); i += 1024) t[padx(i)] = 0xFFFFFFFFu;
     __syncthreads();
     for (int64_t k = range[0] + tid; k < range[1]; k += 1024) t[padx((int)(eidx[k] - base))] = ekey[k];
     __syncthreads();
-    uint64_t r[16];
+    uint32_t r[16];
     // bits 0-3: entries tid*16 + i
 #pragma unroll
     for (int i = 0; i < 16; ++i) r[i] = t[padx(tid * 16 + i)];
@@ -241,7 +245,7 @@ __global__ void __launch_bounds__(1024) zeta_tile_reg_kernel(uint64_t *table, ui
 // a tile is 1024 rows (those bits) x 16 contiguous entries (bits 0-3)
 __global__ void __launch_bounds__(1024) zeta_strided_reg_kernel(ZetaBArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint64_t *t = reinterpret_cast<uint64_t *>(smem);
+    uint32_t *t = reinterpret_cast<uint32_t *>(smem);
     int lo = 0, hi = a.nvar;
     while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
@@ -251,10 +255,10 @@ __global__ void __launch_bounds__(1024) zeta_strided_reg_kernel(ZetaBArgs a) {
     const int bit_lo = a.bit_lo;
     const int nlow = bit_lo - kRowBits;
     const uint64_t bid = blockIdx.x - a.blocks_prefix[v];
-    uint64_t *tv = a.table + a.tb_off[v];
+    uint32_t *tv = a.table + a.tb_off[v];
     const uint64_t base = ((bid & ((1ull << nlow) - 1)) << kRowBits) | ((bid >> nlow) << (bit_lo + 10));
     const int tid = threadIdx.x, c = tid & 15, q = tid >> 4;
-    uint64_t r[16];
+    uint32_t r[16];
     // row bits 0-3: rows (q << 4) | i
 #pragma unroll
     for (int i = 0; i < 16; ++i) r[i] = tv[base | ((uint64_t)((q << 4) | i) << bit_lo) | c];
@@ -277,9 +281,9 @@ __global__ void __launch_bounds__(1024) zeta_strided_reg_kernel(ZetaBArgs a) {
     for (int i = 0; i < 16; ++i) tv[base | ((uint64_t)((i << 6) | q) << bit_lo) | c] = r[i];
 }
 
-__global__ void __launch_bounds__(kB) cost_table_kernel(const uint64_t *table, uint64_t total, float *costs) {
+__global__ void __launch_bounds__(kB) cost_table_kernel(const uint32_t *table, uint64_t total, float *costs) {
     const uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x;
-    if (i < total) costs[i] = key_cost(table[i]);
+    if (i < total) costs[i] = ord_cost(table[i]);
 }
 
 __global__ void __launch_bounds__(kB) query_kernel(SearchDev d, int64_t count, const int *vars, const uint64_t *S,
@@ -287,9 +291,12 @@ __global__ void __launch_bounds__(kB) query_kernel(SearchDev d, int64_t count, c
     const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
     if (i >= count) return;
     const int v = vars[i];
-    const uint64_t key = bs_key(d, v, S[i]);
-    costs[i] = key_cost(key);
-    parents[i] = (key == ~0ull) ? 0ull : d.sets[d.offsets[v] + (int64_t)(key & 0xffffffffull)];
+    costs[i] = bs_cost(d, v, S[i]);
+    if (parents) {
+        // getParents: the first (cost, file order) stored subset -- its cost is the table's
+        const uint64_t key = bs_key_scan(d, v, S[i]);
+        parents[i] = (key == ~0ull) ? 0ull : d.sets[d.offsets[v] + (int64_t)(key & 0xffffffffull)];
+    }
 }
 
 __global__ void quantize_lists_kernel(const float *scores, float *costs, int64_t count) {
@@ -320,7 +327,7 @@ __global__ void __launch_bounds__(kB) pdb_bs_kernel(PdbBsArgs a) {
     const int leaf = a.bitpos[j];
     const uint64_t removed = Rg & ~(1ull << leaf);
     const uint64_t choices = (a.scc & ~removed) | a.anc;
-    a.bsv[R * s + j] = key_cost(bs_key(a.d, leaf, choices));
+    a.bsv[R * s + j] = bs_cost(a.d, leaf, choices);
 }
 
 // one layer of the reverse BFS (static_pattern_database.cpp:184-207):
@@ -368,8 +375,8 @@ int search_build_tables(ulg_ctx *c, uint64_t scope) {
     std::vector<uint64_t> support(n, 0);
     ULG_HIP(c, hipMemcpyAsync(support.data(), s.d_support.p, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
     ULG_HIP(c, hipStreamSynchronize(c->stream));
-    // memory check before touching the current tables: 8 B packed key + 4 B
-    // device cost + 4 B pinned host cost per entry
+    // memory check before touching the current tables: 4 B ordered cost + 4 B
+    // device float cost + 4 B pinned host cost per entry
     uint64_t total = 0;
     for (int v = 0; v < n; ++v) {
         const int m = __builtin_popcountll(support[v]);
@@ -380,11 +387,11 @@ int search_build_tables(ulg_ctx *c, uint64_t scope) {
     if (budget == 0) {
         size_t free_b = 0, tot_b = 0;
         ULG_HIP(c, hipMemGetInfo(&free_b, &tot_b));
-        budget = (uint64_t)(free_b / 2) + (uint64_t)s.d_table.cap * 8 + (uint64_t)s.d_cost_table.cap * 4;
+        budget = (uint64_t)(free_b / 2) + (uint64_t)s.d_table.cap * 4 + (uint64_t)s.d_cost_table.cap * 4;
     }
-    if (total * 16 > budget)
+    if (total * 12 > budget)
         return set_err(c, ULG_ERR_UNSUPPORTED, "best-score tables for this scope need " +
-                                                   std::to_string((total * 16) >> 10) + " KiB (budget " +
+                                                   std::to_string((total * 12) >> 10) + " KiB (budget " +
                                                    std::to_string(budget >> 10) + " KiB)");
     s.tables_ready = false;
     s.pdb_ready = false;
@@ -427,15 +434,15 @@ int search_build_tables(ulg_ctx *c, uint64_t scope) {
                                                       (int)nsets, 0, end_bit, c->stream));
         prof_end(c);
         ULG_HIP(c, hipFuncSetAttribute((const void *)zeta_tile_reg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       kPadLds * 8));
+                                       kPadLds * 4));
         prof_begin(c, "bs_zeta_tile");
-        zeta_tile_reg_kernel<<<(unsigned)(total >> kRegTileBits), 1024, (size_t)kPadLds * 8, c->stream>>>(
+        zeta_tile_reg_kernel<<<(unsigned)(total >> kRegTileBits), 1024, (size_t)kPadLds * 4, c->stream>>>(
             s.d_table.p, total >> kRegTileBits, s.e_idx2.p, s.e_key2.p, nsets);
         prof_end(c);
         ULG_HIP(c, hipGetLastError());
     } else {
     prof_begin(c, "bs_fill");
-    ULG_HIP(c, hipMemsetAsync(s.d_table.p, 0xff, total * 8, c->stream));
+    ULG_HIP(c, hipMemsetAsync(s.d_table.p, 0xff, total * 4, c->stream));
     prof_end(c);
     prof_begin(c, "bs_scatter");
     scatter_kernel<<<dim3(gx, n), kB, 0, c->stream>>>(s.d_sets.p, s.d_costs.p, s.d_offsets.p, n, s.d_support.p,
@@ -448,8 +455,8 @@ int search_build_tables(ulg_ctx *c, uint64_t scope) {
     }
     ULG_HIP(c, hipMemcpyAsync(s.d_prefix.p, tiles_prefix.data(), (size_t)(n + 1) * 4, hipMemcpyHostToDevice, c->stream));
     const int maxm0 = *std::max_element(s.mbits.begin(), s.mbits.end());
-    const size_t ldsA = (size_t)8 << std::min(maxm0, kTileBits);
-    ULG_HIP(c, hipFuncSetAttribute((const void *)zeta_tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(8 << kTileBits)));
+    const size_t ldsA = (size_t)4 << std::min(maxm0, kTileBits);
+    ULG_HIP(c, hipFuncSetAttribute((const void *)zeta_tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 << kTileBits)));
     prof_begin(c, "bs_zeta_tile");
     zeta_tile_kernel<<<tiles_prefix[n], 1024, ldsA, c->stream>>>(s.d_table.p, s.d_tb_off.p, s.d_prefix.p, s.d_mbits.p, n);
     prof_end(c);
@@ -457,7 +464,7 @@ int search_build_tables(ulg_ctx *c, uint64_t scope) {
     }
     const int maxm = *std::max_element(s.mbits.begin(), s.mbits.end());
     // pass B over the remaining high bits, kColBits at a time
-    ULG_HIP(c, hipFuncSetAttribute((const void *)zeta_strided_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(8 << (kColBits + kRowBits))));
+    ULG_HIP(c, hipFuncSetAttribute((const void *)zeta_strided_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 << (kColBits + kRowBits))));
     for (int bit_lo = kTileBits; bit_lo < maxm; bit_lo += kColBits) {
         std::fill(blocks_prefix.begin(), blocks_prefix.end(), 0);
         for (int v = 0; v < n; ++v) {
@@ -476,10 +483,10 @@ int search_build_tables(ulg_ctx *c, uint64_t scope) {
         prof_begin(c, "bs_zeta_strided");
         if (full_window) {
             ULG_HIP(c, hipFuncSetAttribute((const void *)zeta_strided_reg_kernel,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, kPadLds * 8));
-            zeta_strided_reg_kernel<<<blocks_prefix[n], 1024, (size_t)kPadLds * 8, c->stream>>>(za);
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kPadLds * 4));
+            zeta_strided_reg_kernel<<<blocks_prefix[n], 1024, (size_t)kPadLds * 4, c->stream>>>(za);
         } else {
-            zeta_strided_kernel<<<blocks_prefix[n], 1024, (size_t)8 << (G + kRowBits), c->stream>>>(za);
+            zeta_strided_kernel<<<blocks_prefix[n], 1024, (size_t)4 << (G + kRowBits), c->stream>>>(za);
         }
         prof_end(c);
         ULG_HIP(c, hipGetLastError());

@@ -119,7 +119,7 @@ __global__ void __launch_bounds__(kB) layer_pull_kernel(LayerArgs a) {
             const float gp = a.gprev[prefix + suffix];
             if (gp < FLT_MAX) {
                 reached = true;
-                const float cand = gp + key_cost(bs_key(a.d, leaf, P));
+                const float cand = gp + bs_cost(a.d, leaf, P);
                 if (cand < best || bestj == 255) {
                     best = cand;
                     bestj = j;

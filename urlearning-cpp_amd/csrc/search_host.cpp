@@ -12,6 +12,7 @@
 // pattern databases.  Parent sets for the reconstruction come from the device
 // query kernel.
 #include <algorithm>
+#include <chrono>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -58,8 +59,10 @@ struct ExactResult {
 };
 
 // run_astar_on_one_scc (astar_main.cpp:216-546)
+using Clock = std::chrono::steady_clock;
+
 int astar_one(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool skeleton_good, uint64_t ancestors,
-              uint64_t the_scc, int64_t *expanded, bool *hang, ExactResult &res) {
+              uint64_t the_scc, int64_t *expanded, bool *hang, ExactResult &res, const Clock::time_point *deadline) {
     const int n = T.n;
     std::vector<Node> nodes;
     nodes.reserve(1 << 16);
@@ -75,6 +78,11 @@ int astar_one(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool skele
     const float upperBound = FLT_MAX;
     int64_t nexp = 0;
     while (!open.a.empty()) {
+        // the -r watchdog (astar_main.cpp:135-138,266): the loop ends without a goal
+        if (deadline && (nexp & 4095) == 0 && Clock::now() > *deadline) {
+            c->out_of_time = 1;
+            break;
+        }
         const uint32_t ui = open.pop();
         ++nexp;
         const uint64_t variables = nodes[ui].sub;
@@ -269,6 +277,34 @@ int ulg_search_from_scores(ulg_ctx *c) {
     return lists_loaded(c);
 }
 
+int ulg_search_load_scores(ulg_ctx *c, int n, const int64_t *offsets, const uint64_t *sets, const float *scores,
+                           int device_ptrs) {
+    if (!c || n < 1 || n > kMaxVars || !offsets || !sets || !scores)
+        return set_err(c, ULG_ERR_ARG, "ulg_search_load_scores: bad arguments");
+    for (int v = 0; v < n; ++v)
+        if (offsets[v + 1] < offsets[v] || offsets[v + 1] - offsets[v] > 0xffffffffll)
+            return set_err(c, ULG_ERR_ARG, "ulg_search_load_scores: bad offsets");
+    ULG_HIP(c, hipSetDevice(c->device));
+    SearchState &s = state(c);
+    const int64_t total = offsets[n] - offsets[0];
+    int rc;
+    if ((rc = ensure(c, s.d_sets, (size_t)std::max<int64_t>(total, 1))) || (rc = ensure(c, s.d_costs, (size_t)std::max<int64_t>(total, 1))) ||
+        (rc = ensure(c, s.d_offsets, (size_t)n + 1)) || (rc = ensure(c, s.d_scores_tmp, (size_t)std::max<int64_t>(total, 1))))
+        return rc;
+    s.n = n;
+    s.offsets.assign(n + 1, 0);
+    for (int v = 0; v <= n; ++v) s.offsets[v] = offsets[v] - offsets[0];
+    const hipMemcpyKind kind = device_ptrs ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    if (total) {
+        ULG_HIP(c, hipMemcpyAsync(s.d_sets.p, sets + offsets[0], (size_t)total * 8, kind, c->stream));
+        ULG_HIP(c, hipMemcpyAsync(s.d_scores_tmp.p, scores + offsets[0], (size_t)total * 4, kind, c->stream));
+    }
+    ULG_HIP(c, hipMemcpyAsync(s.d_offsets.p, s.offsets.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    if ((rc = search_quantize_device(c, s.d_scores_tmp.p, s.d_costs.p, total))) return rc;
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    return lists_loaded(c);
+}
+
 int ulg_bestscore_query(ulg_ctx *c, int64_t count, const int *vars, const uint64_t *S, float *costs, uint64_t *parents) {
     if (!c || count < 0 || (count && (!vars || !S))) return ULG_ERR_ARG;
     if (!c->search || !c->search->lists_ready) return set_err(c, ULG_ERR_STATE, "ulg_bestscore_query: no parent-set lists");
@@ -329,6 +365,8 @@ int ulg_astar_scc(ulg_ctx *c, const uint64_t *edges, int pd_count, int mode, uin
     }
     *expanded = 0;
     *goal_cost = 0.0f;
+    c->out_of_time = 0;
+    const Clock::time_point deadline = Clock::now() + std::chrono::milliseconds(c->time_limit_ms);
     for (int i = 0; i < n; ++i) { vpar[i] = 0; order[i] = 0; }
     if (net_text && net_cap > 0) net_text[0] = 0;
     if (mode == ULG_ASTAR_GPU) return astar_gpu(c, edges, vpar, order, goal_cost, expanded);
@@ -345,7 +383,9 @@ int ulg_astar_scc(ulg_ctx *c, const uint64_t *edges, int pd_count, int mode, uin
         HostTables T;
         host_tables(s, T);
         ExactResult r;
-        if ((rc = astar_one(c, T, edges, good, ancestors, comp, expanded, &hang, r))) return rc;
+        if ((rc = astar_one(c, T, edges, good, ancestors, comp, expanded, &hang, r,
+                            c->time_limit_ms > 0 ? &deadline : nullptr)))
+            return rc;
         if (!r.found) { fail = true; continue; }
         // each component rewrites netFile and netFile.csv (astar_main.cpp:470,519)
         for (int v = 0; v < n; ++v) vpar[v] = 0;
@@ -364,7 +404,7 @@ int ulg_astar_scc(ulg_ctx *c, const uint64_t *edges, int pd_count, int mode, uin
         }
     }
     if (hang) return set_err(c, ULG_ERR_STATE, "ulg_astar: the reference heap's __down_heap would not terminate here");
-    if (fail) return set_err(c, ULG_ERR_STATE, "ulg_astar: a component has no goal");
+    if (fail && !c->out_of_time) return set_err(c, ULG_ERR_STATE, "ulg_astar: a component has no goal");
     return ULG_OK;
 }
 

@@ -40,6 +40,20 @@ __host__ __device__ inline uint32_t ordkey(float f) {
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
+// inverse of ordkey; 0xFFFFFFFF (no stored subset) reads as FLT_MAX.  (Only
+// the NaN 0x7FFFFFFF maps there too.)
+__host__ __device__ inline float ord_cost(uint32_t k) {
+    if (k == 0xFFFFFFFFu) return FLT_MAX;
+    const uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+    float f;
+#ifdef __HIP_DEVICE_COMPILE__
+    f = __uint_as_float(u);
+#else
+    __builtin_memcpy(&f, &u, 4);
+#endif
+    return f;
+}
+
 __host__ __device__ inline float key_cost(uint64_t key) {
     if (key == ~0ull) return FLT_MAX;  // no stored subset: getScore returns FLT_MAX
     const uint32_t k = (uint32_t)(key >> 32);
@@ -93,7 +107,7 @@ __host__ __device__ inline float quantize_score(float x) {
 
 // device view of the search tables (passed by value to kernels)
 struct SearchDev {
-    const uint64_t *table;   // packed (ordered cost << 32 | file index) per subset of D_v
+    const uint32_t *table;   // ordered cost (ordkey) of the best stored subset, per subset of D_v
     const uint64_t *tb_off;  // [n+1]
     const uint64_t *support; // D_v
     const uint64_t *sets;    // per-variable lists, file order
@@ -120,8 +134,6 @@ __device__ inline uint64_t bs_key_scan(const SearchDev &d, int v, uint64_t S) {
     return best;
 }
 
-// One read of the lattice when S lies inside the tables' scope (every stored
-// set that can be a subset of S is in the table), else the list scan.
 // pext over the set bits of x (x a subset of m): |x| steps instead of |m|
 __device__ inline uint64_t pext_sparse(uint64_t x, uint64_t m) {
     uint64_t r = 0;
@@ -129,17 +141,22 @@ __device__ inline uint64_t pext_sparse(uint64_t x, uint64_t m) {
     return r;
 }
 
-__device__ inline uint64_t bs_key(const SearchDev &d, int v, uint64_t S) {
-    if (d.tables && (S & ~d.scope) == 0) {
-        const uint64_t D = d.support[v];
-        const uint64_t x = S & D;
-        const uint64_t all = (d.n >= 64) ? ~0ull : ((1ull << d.n) - 1ull);
-        const uint64_t lo = (1ull << v) - 1ull;
-        // D_v = every variable but v (a full skeleton): pext closes the hole at v
-        const uint64_t idx = D == (all & ~(1ull << v)) ? (((v < 63 ? (x >> (v + 1)) : 0ull) << v) | (x & lo)) : pext_sparse(x, D);
-        return d.table[d.tb_off[v] + idx];
-    }
-    return bs_key_scan(d, v, S);
+// index of S in v's table: pext(S & D_v, D_v); a full skeleton's
+// D_v = every variable but v closes the hole at v with two shifts
+__device__ inline uint64_t bs_index(const SearchDev &d, int v, uint64_t S) {
+    const uint64_t D = d.support[v];
+    const uint64_t x = S & D;
+    const uint64_t all = (d.n >= 64) ? ~0ull : ((1ull << d.n) - 1ull);
+    const uint64_t lo = (1ull << v) - 1ull;
+    return D == (all & ~(1ull << v)) ? (((v < 63 ? (x >> (v + 1)) : 0ull) << v) | (x & lo)) : pext_sparse(x, D);
+}
+
+// getScore(v, S): one 4-B read of the lattice when S lies inside the tables'
+// scope (every stored set that can be a subset of S is in the table), else
+// the list scan.
+__device__ inline float bs_cost(const SearchDev &d, int v, uint64_t S) {
+    if (d.tables && (S & ~d.scope) == 0) return ord_cost(d.table[d.tb_off[v] + bs_index(d, v, S)]);
+    return key_cost(bs_key_scan(d, v, S));
 }
 
 // StaticPatternDatabase::h (static_pattern_database.cpp:145-174)
@@ -171,8 +188,10 @@ struct SearchState {
     std::vector<uint64_t> support, tb_off;
     std::vector<int> mbits;
     uint64_t table_entries = 0;
-    DevBuf<uint64_t> d_table, d_tb_off, d_support;
-    DevBuf<uint64_t> e_idx, e_key, e_idx2, e_key2;  // sorted (table index, key) of the stored sets
+    DevBuf<uint32_t> d_table;      // ordkey(best cost) per subset of D_v
+    DevBuf<uint64_t> d_tb_off, d_support;
+    DevBuf<uint64_t> e_idx, e_idx2;  // sorted (table index, key) of the stored sets
+    DevBuf<uint32_t> e_key, e_key2;
     DevBuf<unsigned char> sort_tmp;
     DevBuf<int> d_mbits, d_prefix;
     bool lists_ready = false;   // the per-variable lists are on the device

@@ -165,12 +165,30 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         c->score_variant = (int)value;
         return ULG_OK;
     }
+    if (std::strcmp(name, "time_limit_ms") == 0) {
+        if (value < 0) return set_err(c, ULG_ERR_ARG, "time_limit_ms must be >= 0");
+        c->time_limit_ms = value;
+        return ULG_OK;
+    }
     if (std::strcmp(name, "table_budget_kb") == 0) {
         if (value < 0) return set_err(c, ULG_ERR_ARG, "table_budget_kb must be >= 0");
         c->table_budget_kb = (uint64_t)value;
         return ULG_OK;
     }
     return set_err(c, ULG_ERR_ARG, std::string("unknown option: ") + name);
+}
+
+int ulg_get_info(ulg_ctx *c, const char *name, int64_t *value) {
+    if (!c || !name || !value) return ULG_ERR_ARG;
+    if (std::strcmp(name, "out_of_time") == 0) {
+        *value = c->out_of_time;
+        return ULG_OK;
+    }
+    if (std::strcmp(name, "highest_completed_layer") == 0) {
+        *value = c->completed_layer;
+        return ULG_OK;
+    }
+    return set_err(c, ULG_ERR_ARG, std::string("unknown info: ") + name);
 }
 
 int ulg_profile_enable(ulg_ctx *c, int on) {

@@ -72,6 +72,9 @@ struct ulg_ctx {
     int score_small_layers = 4;             // layers <= this run one-pass on one stream (two-pass variants)
     std::vector<hipStream_t> aux_streams;   // created on first use
     std::vector<hipEvent_t> sync_events;
+    int64_t time_limit_ms = 0;     // -r: wall-clock budget per scoring call / search (0 = none)
+    int out_of_time = 0;           // the last scoring call or search ran out of its budget
+    int completed_layer = -1;      // highest fully scored layer of the last scoring call
     uint64_t table_budget_kb = 0;  // best-score table budget in KiB (0 = half the free HBM)  // see ScoreArgs::variant (ulg_set_option "score_variant")
     ulg::DevBuf<float> table;
     ulg::DevBuf<uint64_t> d_tbl_off, d_work, d_blk;

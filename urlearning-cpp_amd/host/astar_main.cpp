@@ -33,7 +33,7 @@ int main(int argc, char **argv) {
             {"a", "argument", true, "2", "Number of static pattern databases"},
             {"p", "pc_{i-1}", true, "", "Variables which can only be used as ancestors (CSV of indices; with -s)"},
             {"s", "scc_i", true, "", "Variables which will be added in the search (CSV of indices; blank: all)"},
-            {"r", "runningTime", true, "0", "Maximum running time (not applied)"},
+            {"r", "runningTime", true, "0", "The maximum running time (s) for the algorithm (exact mode).  0 means no running time."},
             {"n", "netFile", true, "", "The file to which the learned network is written."},
             {"", "mode", true, "exact", "exact (reference pop order) or gpu (GPU order-graph search)"},
             {"", "device", true, "0", "HIP device to use."},
@@ -108,6 +108,11 @@ int main(int argc, char **argv) {
     float cost = 0.0f;
     int64_t expanded = 0;
     std::vector<char> text(1 << 20);
+    const int running_time = std::atoi(args.get("runningTime").c_str());
+    if (running_time > 0) {
+        std::printf("Maximum running time: %d\n", running_time);  // astar_main.cpp:698
+        if (rc == ULG_OK) rc = ulg_set_option(ctx, "time_limit_ms", (int64_t)running_time * 1000);
+    }
     if (rc == ULG_OK)
         rc = ulg_astar_scc(ctx, good ? rows.data() : nullptr, pd, mode == "gpu" ? ULG_ASTAR_GPU : ULG_ASTAR_EXACT,
                            ancestors, scc, vpar.data(), order.data(), &cost, &expanded, text.data(),
@@ -118,7 +123,23 @@ int main(int argc, char **argv) {
         ulg_destroy(ctx);
         return 1;
     }
+    int64_t oot = 0;
+    ulg_get_info(ctx, "out_of_time", &oot);
     ulg_destroy(ctx);
+    if (oot) {
+        // astar_main.cpp:136,535-540: the loop ended without a goal
+        std::printf("Out of time\n");
+        std::printf("No solution found.\n");
+        std::printf("Nodes expanded: %lld\n", (long long)expanded);
+        // a component finished before the watchdog keeps its netFile
+        const std::string net = args.get("netFile");
+        if (!net.empty() && text[0] && (!ulgio::write_text(net, std::string(text.data())) ||
+                                        !ulgio::write_net_csv(net + ".csv", vpar, n))) {
+            std::fprintf(stderr, "astar: cannot write '%s'\n", net.c_str());
+            return 1;
+        }
+        return 0;
+    }
     std::printf("Found solution: %f\n", (double)cost);
     std::printf("Nodes expanded: %lld\n", (long long)expanded);
     std::printf("Timing: read .pss %.3f s, HIP init %.3f s, GPU best-score tables %.3f s, search (%s) %.3f s (%.3g expansions/s)\n",

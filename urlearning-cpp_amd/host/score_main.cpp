@@ -32,7 +32,7 @@ int main(int argc, char **argv) {
             {"e", "ess", true, "1", "The equivalent sample size (written to META ess)."},
             {"p", "maxParents", true, "0", "The maximum number of parents for any variable. A value less than 1 means no limit."},
             {"t", "threads", true, "1", "Host threads in the reference; the GPU scores every variable at once."},
-            {"r", "time", true, "-1", "Per-variable time limit in the reference (not applied)."},
+            {"r", "time", true, "-1", "The maximum amount of time (s) to use for each variable (every variable is scored at once: the budget of the whole call, checked after each layer). A value less than 1 means no limit."},
             {"s", "hasHeader", false, "", "Add this flag if the first line of the input file gives the variable names."},
             {"o", "doNotPrune", false, "", "No effect (the reference's pruning is disabled, score_main.cpp:167-171)."},
             {"", "enableDeCamposPruning", false, "", "No effect for cBIC."},
@@ -107,7 +107,18 @@ int main(int argc, char **argv) {
     std::vector<int> vars(n);
     for (int v = 0; v < n; ++v) vars[v] = v;
     int64_t stored = 0, scored = 0;
+    const int running_time = std::atoi(args.get("time").c_str());
+    if (running_time > 0) {
+        std::printf("I am using a timer in the calculation function.\n");  // score_calculator.cpp:40
+        if (rc == ULG_OK) rc = ulg_set_option(ctx, "time_limit_ms", (int64_t)running_time * 1000);
+    }
     if (rc == ULG_OK) rc = ulg_cbic_score(ctx, vars.data(), n, cands.data(), maxp, &stored, &scored);
+    int64_t oot = 0, done_layer = 0;
+    if (rc == ULG_OK && running_time > 0) {
+        ulg_get_info(ctx, "out_of_time", &oot);
+        ulg_get_info(ctx, "highest_completed_layer", &done_layer);
+        if (oot) std::printf("Out of time\n");  // score_calculator.cpp:28-31
+    }
     const double t1 = ulgcli::now_s();
     if (rc != ULG_OK) {
         std::fprintf(stderr, "score: %s\n", ulg_last_error(ctx));
@@ -145,6 +156,7 @@ int main(int argc, char **argv) {
     ulg_destroy(ctx);
     const double t3 = ulgcli::now_s();
     std::printf("URLearning (MI355X), Score Calculator: n=%d N=%lld k=%d lambda=%g\n", n, (long long)N, maxp, lambda);
+    if (oot) std::printf("Scoring stopped after layer %lld of %d (-r %d s)\n", (long long)done_layer, maxp, running_time);
     std::printf("Parent sets scored: %lld, stored: %lld, GPU scoring %.3f s (%.3g sets/s), GPU .pss format %.3f s, "
                 "file write %.3f s (%lld bytes)\n",
                 (long long)scored, (long long)stored, t1 - t0, (double)scored / (t1 - t0), t2 - t1, t3 - t2,

@@ -1,11 +1,20 @@
 """Variable-sharded scoring across ranks (one process per GPU) and the single
-exchange step of SURVEY 8e: every rank scores its stripe of the variables
-(v % world_size == rank, as score_main.cpp:136-139 stripes threads), then one
-all-gather (RCCL over xGMI on MI355X; gloo in the CPU tests) hands every rank
-the complete per-variable (set, score) lists in variable order, ready for
-ulg_search_load or a .pss writer.
+exchange step of SURVEY 8e.
 
-Wire format per entry: int64 [variable, set, float32 score bits].
+Scoring.  Every variable has its own cache and dominance check
+(score_main.cpp:143-155; the reference's threads stripe variables,
+:136-139), so ranks score disjoint variable sets with no communication.
+`assign` balances them by the parent sets each variable scores,
+sum_{L<=k} C(m_v, L) with m_v = |candidates(v) \ {v}|, longest
+first.  `ListExchange` then runs the ONE collective of the data path: an
+all-gather (RCCL over xGMI on MI355X; gloo in the CPU tests) of fixed-size
+per-rank blocks.  A block holds the rank's local offsets followed by its
+stored sets and scores, written straight from the scorer's device buffers
+(ulg_cbic_fetch with device pointers).  Block capacity is the a-priori bound
+"every scored set is stored", which every rank computes from (candidates, k),
+so no count exchange precedes the data.  After the gather every rank holds
+every variable's list in variable order, ready for ulg_search_load_scores
+(local best-score tables + search) or a .pss writer.
 
 triplet_astar shards the same way: its distinct clusters are
 independent exact A* problems (triplet_astar.cpp:285-674, one per cluster).
@@ -14,8 +23,11 @@ solves its share (ulg_triplet_solve), one all-gather of [cluster, parents...]
 rows fills every rank's memo (ulg_triplet_memo_put), and the sequential
 driver (ulg_triplet_astar) then runs on each rank with nothing left to search
 but the clusters that orientations add mid-sweep -- the MEC is the one a
-single GPU computes."""
+single GPU computes.  (That exchange is off the scoring path and sends a
+count first: allgather_rows.)"""
 from __future__ import annotations
+
+from math import comb
 
 import numpy as np
 import torch
@@ -23,43 +35,121 @@ import torch.distributed as dist
 
 
 def stripe(n: int, world_size: int, rank: int):
+    """The reference's thread striping (score_main.cpp:136-139): v % T."""
     return [v for v in range(n) if v % world_size == rank]
 
 
-def pack(variables, offsets, sets, scores, device="cpu") -> torch.Tensor:
-    """Local lists (variables[i] owns [offsets[i], offsets[i+1])) -> [count, 3] int64."""
-    offsets = np.asarray(offsets, dtype=np.int64)
-    count = int(offsets[-1])
-    out = np.empty((count, 3), dtype=np.int64)
-    for i, v in enumerate(variables):
-        out[offsets[i]:offsets[i + 1], 0] = v
-    out[:, 1] = np.asarray(sets[:count], dtype=np.uint64).view(np.int64)
-    out[:, 2] = np.asarray(scores[:count], dtype=np.float32).view(np.int32).astype(np.int64)
-    return torch.from_numpy(out).to(device)
+def var_weight(n: int, v: int, candidates: int, k: int) -> int:
+    """Parent sets the scorer evaluates for v: sum_{L<=k} C(m_v, L), the
+    empty set included (score_calculator.cpp:54-120)."""
+    m = bin(int(candidates) & ~(1 << v) & ((1 << n) - 1)).count("1")
+    kk = m if k < 1 or k > m else k
+    return sum(comb(m, L) for L in range(kk + 1))
 
 
-def pack_device(variables, offsets: torch.Tensor, sets: torch.Tensor, scores: torch.Tensor) -> torch.Tensor:
-    """Same as pack() for device tensors (ulg_cbic_fetch(device_ptrs=1) output):
-    offsets int64 [nv+1], sets int64 (uint64 bits), scores float32."""
-    count = int(offsets[-1].item())
-    dev = sets.device
-    per = (offsets[1:] - offsets[:-1]).to(torch.int64)
-    var = torch.repeat_interleave(torch.as_tensor(variables, dtype=torch.int64, device=dev), per)
-    out = torch.empty((count, 3), dtype=torch.int64, device=dev)
-    out[:, 0] = var
-    out[:, 1] = sets[:count]
-    out[:, 2] = scores[:count].view(torch.int32).to(torch.int64)
-    return out
+def assign(n: int, world_size: int, candidates, k: int):
+    """Deterministic balanced partition of the variables over ranks:
+    longest-processing-time first on var_weight (ties: lower variable, lower
+    rank).  Returns one ascending variable list per rank."""
+    w = [var_weight(n, v, candidates[v], k) for v in range(n)]
+    order = sorted(range(n), key=lambda v: (-w[v], v))
+    loads = [0] * world_size
+    parts = [[] for _ in range(world_size)]
+    for v in order:
+        r = min(range(world_size), key=lambda q: (loads[q], q))
+        parts[r].append(v)
+        loads[r] += w[v]
+    return [sorted(p) for p in parts]
 
 
-def allgather_lists(packed: torch.Tensor, world_size: int, group=None) -> torch.Tensor:
-    """One all-gather of variable-length [count, 3] blocks (counts first, then
-    the blocks padded to the largest); returns the concatenation in rank order."""
-    return allgather_rows(packed, world_size, group)
+class ListExchange:
+    """One all-gather of every rank's stored (set, score) lists.
+
+    Block layout (bytes; every rank computes the same sizes):
+      [0, hdr)                 int64 local offsets[nv_r + 1] (ulg_cbic_fetch)
+      [hdr, hdr + 8 cap)       uint64 stored sets
+      [hdr + 8 cap, + 4 cap)   float32 scores
+    cap = max over ranks of sum_{v in rank} var_weight (every scored set
+    stored), so a rank's lists always fit and no counts travel first."""
+
+    def __init__(self, n: int, parts, candidates, k: int, rank: int, device="cuda", comm_device=None):
+        self.n, self.parts, self.rank, self.ws = n, parts, rank, len(parts)
+        self.mine = parts[rank]
+        bounds = [sum(var_weight(n, v, candidates[v], k) for v in p) for p in parts]
+        self.cap = max(max(bounds), 1)
+        maxnv = max(len(p) for p in parts)
+        self.hdr = 16 * ((8 * (maxnv + 1) + 15) // 16)
+        self.block = 16 * ((self.hdr + 12 * self.cap + 15) // 16)
+        self.device = torch.device(device)
+        self.comm_device = torch.device(comm_device) if comm_device is not None else self.device
+        self.buf = torch.zeros(self.block, dtype=torch.uint8, device=self.device)
+        self.out = torch.empty(self.ws * self.block, dtype=torch.uint8, device=self.comm_device)
+        base = self.buf.data_ptr()
+        self.offs_ptr = base
+        self.sets_ptr = base + self.hdr
+        self.scores_ptr = base + self.hdr + 8 * self.cap
+
+    def fill(self, ctx, stored: int):
+        """Write this rank's lists (the last ctx.score over self.mine) into
+        the send block, straight from the scorer's device buffers."""
+        if stored > self.cap:
+            raise RuntimeError(f"shard block overflow: {stored} stored > capacity {self.cap}")
+        ctx.fetch_device(self.sets_ptr, self.scores_ptr, self.offs_ptr)
+
+    def fill_host(self, offsets, sets, scores):
+        """Same from host lists (local offsets[nv_r + 1], sets, scores), e.g.
+        the CPU oracle's in the gloo tests."""
+        offsets = np.asarray(offsets, dtype=np.int64)
+        cnt = int(offsets[-1])
+        if cnt > self.cap:
+            raise RuntimeError(f"shard block overflow: {cnt} stored > capacity {self.cap}")
+        b = np.zeros(self.block, dtype=np.uint8)
+        b[:8 * len(offsets)] = offsets.view(np.uint8)
+        b[self.hdr:self.hdr + 8 * cnt] = np.asarray(sets[:cnt], dtype=np.uint64).view(np.uint8)
+        o = self.hdr + 8 * self.cap
+        b[o:o + 4 * cnt] = np.asarray(scores[:cnt], dtype=np.float32).view(np.uint8)
+        self.buf.copy_(torch.from_numpy(b))
+
+    def allgather(self, group=None):
+        """The data-path collective: one all-gather of fixed-size blocks."""
+        src = self.buf if self.comm_device == self.device else self.buf.to(self.comm_device)
+        if self.comm_device.type != "cpu":
+            dist.all_gather_into_tensor(self.out, src, group=group)
+        else:
+            parts = list(self.out.view(self.ws, self.block).unbind(0))
+            dist.all_gather(parts, src, group=group)
+        return self.out
+
+    def assemble(self, device=None):
+        """-> (offsets[n+1] int64 numpy, sets int64 tensor, scores float32
+        tensor) in variable order, on `device` (default: where the gathered
+        blocks are)."""
+        dev = torch.device(device) if device is not None else self.out.device
+        blocks = self.out.view(self.ws, self.block)
+        hdr = blocks[:, :self.hdr].cpu().numpy().view(np.int64)  # one small D2H of the headers
+        src = blocks.to(dev) if blocks.device != dev else blocks
+        sets_all = src[:, self.hdr:self.hdr + 8 * self.cap].contiguous().view(torch.int64)  # [ws, cap]
+        scores_all = src[:, self.hdr + 8 * self.cap:self.hdr + 12 * self.cap].contiguous().view(torch.float32)
+        where = {}
+        for r, p in enumerate(self.parts):
+            for i, v in enumerate(p):
+                where[v] = (r, int(hdr[r, i]), int(hdr[r, i + 1]))
+        offsets = np.zeros(self.n + 1, dtype=np.int64)
+        idx = []
+        for v in range(self.n):
+            r, b, e = where[v]
+            offsets[v + 1] = offsets[v] + (e - b)
+            idx.append(torch.arange(r * self.cap + b, r * self.cap + e, dtype=torch.int64))
+        gi = torch.cat(idx).to(dev) if idx else torch.zeros(0, dtype=torch.int64, device=dev)
+        sets, scores = sets_all.reshape(-1)[gi], scores_all.reshape(-1)[gi]
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)  # libulg reads them on its own stream
+        return offsets, sets, scores
 
 
 def allgather_rows(packed: torch.Tensor, world_size: int, group=None) -> torch.Tensor:
-    """allgather_lists for int64 rows of any width."""
+    """All-gather of variable-length int64 [count, w] blocks (counts first,
+    then the blocks padded to the largest); the concatenation in rank order."""
     dev = packed.device
     w = packed.shape[1]
     cnt = torch.tensor([packed.shape[0]], dtype=torch.int64, device=dev)
@@ -78,20 +168,6 @@ def allgather_rows(packed: torch.Tensor, world_size: int, group=None) -> torch.T
         out = torch.cat(parts, 0)
     keep = torch.cat([torch.arange(r * mx, r * mx + counts[r], device=dev) for r in range(world_size)])
     return out[keep]
-
-
-def unpack(gathered: torch.Tensor, n: int):
-    """-> (offsets[n+1], sets uint64, scores float32) in variable order; the
-    order inside a variable is the order its owning rank produced."""
-    g = gathered.cpu().numpy()
-    order = np.argsort(g[:, 0], kind="stable")
-    g = g[order]
-    counts = np.bincount(g[:, 0], minlength=n)
-    offsets = np.zeros(n + 1, dtype=np.int64)
-    offsets[1:] = np.cumsum(counts)
-    sets = g[:, 1].view(np.uint64).copy()
-    scores = g[:, 2].astype(np.int32).view(np.float32).copy()
-    return offsets, sets, scores
 
 
 # ---- triplet_astar clusters -------------------------------------------------

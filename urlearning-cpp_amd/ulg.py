@@ -44,6 +44,7 @@ def lib():
         L.ulg_quantize_costs.argtypes = [P, P, P, I64]
         L.ulg_search_load.argtypes = [P, I, P, P, P]
         L.ulg_search_from_scores.argtypes = [P]
+        L.ulg_search_load_scores.argtypes = [P, I, P, P, P, I]
         L.ulg_bestscore_query.argtypes = [P, I64, P, P, P, P]
         L.ulg_pdb_build.argtypes = [P, I, C.c_uint64, C.c_uint64]
         L.ulg_pdb_query.argtypes = [P, I64, P, P, P]
@@ -58,6 +59,7 @@ def lib():
         L.ulg_astar_scc.argtypes = [P, P, I, I, C.c_uint64, C.c_uint64, P, P, C.POINTER(F), C.POINTER(I64),
                                     C.c_char_p, I64]
         L.ulg_set_option.argtypes = [P, C.c_char_p, I64]
+        L.ulg_get_info.argtypes = [P, C.c_char_p, C.POINTER(I64)]
         L.ulg_profile_enable.argtypes = [P, I]
         L.ulg_profile_get.argtypes = [P, C.c_char_p, C.POINTER(D), C.POINTER(I64), C.POINTER(D)]
         L.ulg_profile_dump.argtypes = [P, C.c_char_p, I64]
@@ -177,6 +179,25 @@ class Context:
         self._check(lib().ulg_search_from_scores(self._h), "ulg_search_from_scores")
         self.search_n = self.n
 
+    def search_load_scores(self, offsets, sets, scores, device_ptrs=False):
+        """ulg_search_load_scores: per-variable .pss-score lists in variable
+        order (offsets[n+1] on the host).  device_ptrs: sets/scores are
+        device addresses (ints, e.g. tensor.data_ptr()); else numpy arrays."""
+        o = np.ascontiguousarray(offsets, dtype=np.int64)
+        if device_ptrs:
+            sp, cp = C.c_void_p(int(sets)), C.c_void_p(int(scores))
+            keep = None
+        else:
+            s = np.ascontiguousarray(sets, dtype=np.uint64)
+            c = np.ascontiguousarray(scores, dtype=np.float32)
+            if s.size == 0:
+                s, c = np.zeros(1, dtype=np.uint64), np.zeros(1, dtype=np.float32)
+            sp, cp, keep = _ptr(s), _ptr(c), (s, c)
+        self._check(lib().ulg_search_load_scores(self._h, len(o) - 1, _ptr(o), sp, cp, 1 if device_ptrs else 0),
+                    "ulg_search_load_scores")
+        del keep
+        self.search_n = len(o) - 1
+
     def bestscore(self, variables, S):
         v = np.ascontiguousarray(variables, dtype=np.int32)
         s = np.ascontiguousarray([int(x) for x in S], dtype=np.uint64)
@@ -287,6 +308,12 @@ class Context:
 
     def set_option(self, name: str, value: int):
         self._check(lib().ulg_set_option(self._h, name.encode(), int(value)), "ulg_set_option")
+
+    def info(self, name: str) -> int:
+        """ulg_get_info: "out_of_time", "highest_completed_layer"."""
+        v = C.c_int64()
+        self._check(lib().ulg_get_info(self._h, name.encode(), C.byref(v)), "ulg_get_info")
+        return v.value
 
     # ---- profiling ----------------------------------------------------------
     def profile(self, on: bool = True):
