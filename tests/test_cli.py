@@ -171,3 +171,12 @@ def test_cli_c1_hepatitis_default_parent_limit(tmp_path):
             assert net.read_text() == ref["net"]
             assert (tmp_path / "net_exact.csv").read_text() == ref["net_csv"]
     os.remove(pss)
+
+
+def test_triplet_cli_rejects_running_time():
+    """triplet_astar's watchdog (triplet_astar.cpp:141,355) would end every
+    later A* of the driver without a goal -- a clock-dependent MEC -- so -r > 0
+    is refused loudly instead of being ignored."""
+    r = subprocess.run([os.path.join(PKG, "bin", "triplet_astar"), "x.pss", "-r", "5"], capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 2 and "not supported" in r.stderr

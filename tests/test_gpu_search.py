@@ -278,3 +278,34 @@ def test_gpu_search_sparse_skeleton_optimal_cost(ulg_ctx, oracle_built, symmetri
     ref = o.Search(n, offs, sets, costs).astar(edges=rows)
     assert ref["rc"] == 0
     assert abs(res["cost"] - ref["cost"]) <= 1e-6 * abs(ref["cost"]), (res["cost"], ref["cost"])
+
+
+@pytest.mark.parametrize("sparse", [False, True])
+def test_exact_astar_dense_and_indexed_forms_agree(ulg_ctx, oracle_built, monkeypatch, sparse):
+    """Scopes of <= 26 variables run the dense replay (node homes at
+    pext(S, scope), successor-cost rows); ULG_EXACT_SPARSE forces the
+    indexed form used for larger scopes.  Both give the oracle's DAG, order,
+    cost and expansion count, on a full skeleton and on a sparse one."""
+    import ulg
+    o = oracle_built
+    n, k = 18, 4
+    X, W = synth.gaussian_sem(n, 4000, 9350)
+    rows = synth.true_skeleton_edges(W, extra_frac=0.5, seed=4) if sparse else [(1 << n) - 1] * n
+    cands = ulg.candidates_from_edges(rows, n)
+    offs, sets, scores, costs = _oracle_pipeline(o, X, 2.0, k, cands)
+    ulg_ctx.search_load(offs, sets, costs)
+    ref = o.Search(n, offs, sets, costs).astar(edges=rows)
+    out = []
+    for force in (False, True):
+        if force:
+            monkeypatch.setenv("ULG_EXACT_SPARSE", "1")
+        else:
+            monkeypatch.delenv("ULG_EXACT_SPARSE", raising=False)
+        res = ulg_ctx.astar(edges=rows, mode=0)
+        assert [int(x) for x in res["vpar"]] == [int(x) for x in ref["vpar"]]
+        assert list(res["order"]) == list(ref["order"])
+        assert np.float32(res["cost"]).tobytes() == np.float32(ref["cost"]).tobytes()
+        assert res["expanded"] == ref["expanded"]
+        assert res["net_text"] == ref["net_text"]
+        out.append(res["expanded"])
+    assert out[0] == out[1]

@@ -20,6 +20,7 @@
 // contiguous entries.  Both passes stream the table once (HBM-bound).
 // Lookup: cost = ord_cost(T_v[pext(S, D_v)]).
 #include <hipcub/hipcub.hpp>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <cfloat>
@@ -281,21 +282,58 @@ __global__ void __launch_bounds__(1024) zeta_strided_reg_kernel(ZetaBArgs a) {
     for (int i = 0; i < 16; ++i) tv[base | ((uint64_t)((i << 6) | q) << bit_lo) | c] = r[i];
 }
 
+// successor-cost rows for the dense exact-order search: thread t of a chunk
+// fills row r = r0 + t / nl, column li: getScore(scc_li, S) with
+// S = pdep(r, scope) -- one contiguous row per popped node instead of one
+// random lattice read per successor
+__global__ void __launch_bounds__(kB) cost_rows_kernel(SearchDev d, const int *meta, int m, int nl, uint64_t r0,
+                                                       uint64_t cnt, float *out) {
+    __shared__ int bits[64], vars[64];
+    for (int i = threadIdx.x; i < m; i += kB) bits[i] = meta[i];
+    for (int i = threadIdx.x; i < nl; i += kB) vars[i] = meta[64 + i];
+    __syncthreads();
+    const uint64_t t = (uint64_t)blockIdx.x * kB + threadIdx.x;
+    if (t >= cnt * (uint64_t)nl) return;
+    const uint64_t r = r0 + t / (uint64_t)nl;
+    const int li = (int)(t % (uint64_t)nl);
+    uint64_t S = 0;
+    for (uint64_t x = r; x; x &= x - 1) S |= 1ull << bits[__builtin_ctzll(x)];
+    const int leaf = vars[li];
+    out[t] = ((S >> leaf) & 1ull) ? FLT_MAX : bs_cost(d, leaf, S);
+}
+
 __global__ void __launch_bounds__(kB) cost_table_kernel(const uint32_t *table, uint64_t total, float *costs) {
     const uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x;
     if (i < total) costs[i] = ord_cost(table[i]);
 }
 
+// getScore + getParents for one (variable, S) per block: the block scans the
+// variable's list for the first (cost, file order) stored subset of S
+// (sparse_parent_list.cpp:44-55 with the pinned N7 tie-break) -- the entry
+// whose cost the lattice holds, and the parent set behind it.
 __global__ void __launch_bounds__(kB) query_kernel(SearchDev d, int64_t count, const int *vars, const uint64_t *S,
                                                    float *costs, uint64_t *parents) {
-    const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
-    if (i >= count) return;
-    const int v = vars[i];
-    costs[i] = bs_cost(d, v, S[i]);
-    if (parents) {
-        // getParents: the first (cost, file order) stored subset -- its cost is the table's
-        const uint64_t key = bs_key_scan(d, v, S[i]);
-        parents[i] = (key == ~0ull) ? 0ull : d.sets[d.offsets[v] + (int64_t)(key & 0xffffffffull)];
+    __shared__ uint64_t red[kB / 64];
+    const int64_t q = blockIdx.x;
+    const int v = vars[q];
+    const uint64_t s = S[q];
+    const int64_t b = d.offsets[v], e = d.offsets[v + 1];
+    uint64_t best = ~0ull;
+    for (int64_t i = b + threadIdx.x; i < e; i += kB)
+        if ((d.sets[i] & ~s) == 0) {
+            const uint64_t k = ((uint64_t)ordkey(d.costs[i]) << 32) | (uint64_t)(i - b);
+            best = k < best ? k : best;
+        }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(best, off);
+        best = o < best ? o : best;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kB / 64; ++w) best = red[w] < best ? red[w] : best;
+        costs[q] = bs_cost(d, v, s);  // the lattice read (the scan's key cost where S is outside the tables)
+        parents[q] = (best == ~0ull) ? 0ull : d.sets[b + (int64_t)(best & 0xffffffffull)];
     }
 }
 
@@ -396,6 +434,7 @@ int search_build_tables(ulg_ctx *c, uint64_t scope) {
     s.tables_ready = false;
     s.pdb_ready = false;
     s.host_costs_ready = false;
+    s.rows_ready = false;
     s.support = support;
     s.mbits.assign(n, 0);
     s.tb_off.assign(n + 1, 0);
@@ -614,6 +653,74 @@ int search_cost_table_host(ulg_ctx *c) {
     return ULG_OK;
 }
 
+bool HostHuge::reserve(size_t want, bool pin) {
+    if (p && bytes >= want && pinned == pin) return true;
+    release();
+    const size_t huge = (size_t)2 << 20;
+    const size_t b = (want + huge - 1) / huge * huge;
+    void *q = mmap(nullptr, b, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (q == MAP_FAILED) return false;
+    (void)madvise(q, b, MADV_HUGEPAGE);
+    p = q;
+    bytes = b;
+    pinned = false;
+    if (pin) pinned = hipHostRegister(p, b, hipHostRegisterDefault) == hipSuccess;  // else pageable copies
+    return true;
+}
+
+void HostHuge::zero_prefix(size_t n) {
+    if (p && n) std::memset(p, 0, std::min(n, bytes));
+}
+
+void HostHuge::release() {
+    if (!p) return;
+    if (pinned) (void)hipHostUnregister(p);
+    munmap(p, bytes);
+    p = nullptr;
+    bytes = 0;
+    pinned = false;
+}
+
+int search_cost_rows_host(ulg_ctx *c, uint64_t scope, uint64_t scc) {
+    SearchState &s = *c->search;
+    if (s.rows_ready && s.rows_scope == scope && s.rows_scc == scc) return ULG_OK;
+    const int m = __builtin_popcountll(scope), nl = __builtin_popcountll(scc);
+    const uint64_t rows = 1ull << m, total = rows * (uint64_t)nl;
+    if (!s.host_rows.reserve((size_t)total * 4, true))
+        return set_err(c, ULG_ERR_HIP, "cannot map the host row table (" + std::to_string(total * 4 >> 20) + " MiB)");
+    std::vector<int> meta(128, 0);
+    {
+        int i = 0;
+        for (uint64_t x = scope; x; x &= x - 1) meta[i++] = __builtin_ctzll(x);
+        i = 0;
+        for (uint64_t x = scc; x; x &= x - 1) meta[64 + i++] = __builtin_ctzll(x);
+    }
+    // chunks of <= 64 Mi floats through one device staging buffer
+    const uint64_t chunk_rows = std::max<uint64_t>(1, std::min<uint64_t>(rows, (64ull << 20) / (uint64_t)nl));
+    int rc;
+    if ((rc = ensure(c, s.d_rows, (size_t)(chunk_rows * nl))) || (rc = ensure(c, s.d_rowmeta, 128))) return rc;
+    ULG_HIP(c, hipMemcpyAsync(s.d_rowmeta.p, meta.data(), 128 * 4, hipMemcpyHostToDevice, c->stream));
+    const SearchDev d = s.dev();
+    float *host = static_cast<float *>(s.host_rows.p);
+    for (uint64_t r0 = 0; r0 < rows; r0 += chunk_rows) {
+        const uint64_t cnt = std::min(chunk_rows, rows - r0);
+        const uint64_t work = cnt * (uint64_t)nl;
+        prof_begin(c, "bs_cost_rows");
+        cost_rows_kernel<<<(unsigned)((work + kB - 1) / kB), kB, 0, c->stream>>>(d, s.d_rowmeta.p, m, nl, r0, cnt,
+                                                                                 s.d_rows.p);
+        prof_end(c);
+        ULG_HIP(c, hipGetLastError());
+        ULG_HIP(c, hipMemcpyAsync(host + r0 * (uint64_t)nl, s.d_rows.p, (size_t)work * 4, hipMemcpyDeviceToHost,
+                                  c->stream));
+    }
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    s.rows_scope = scope;
+    s.rows_scc = scc;
+    s.rows_ready = true;
+    return ULG_OK;
+}
+
 int search_query(ulg_ctx *c, int64_t count, const int *vars, const uint64_t *S, float *costs, uint64_t *parents) {
     SearchState &s = *c->search;
     int rc;
@@ -622,8 +729,8 @@ int search_query(ulg_ctx *c, int64_t count, const int *vars, const uint64_t *S, 
         return rc;
     ULG_HIP(c, hipMemcpyAsync(s.q_vars.p, vars, (size_t)count * 4, hipMemcpyHostToDevice, c->stream));
     ULG_HIP(c, hipMemcpyAsync(s.q_sets.p, S, (size_t)count * 8, hipMemcpyHostToDevice, c->stream));
-    query_kernel<<<(unsigned)((count + kB - 1) / kB), kB, 0, c->stream>>>(s.dev(), count, s.q_vars.p, s.q_sets.p,
-                                                                       s.q_costs.p, s.q_par.p);
+    query_kernel<<<(unsigned)count, kB, 0, c->stream>>>(s.dev(), count, s.q_vars.p, s.q_sets.p, s.q_costs.p,
+                                                         s.q_par.p);
     ULG_HIP(c, hipGetLastError());
     if (costs) ULG_HIP(c, hipMemcpyAsync(costs, s.q_costs.p, (size_t)count * 4, hipMemcpyDeviceToHost, c->stream));
     if (parents) ULG_HIP(c, hipMemcpyAsync(parents, s.q_par.p, (size_t)count * 8, hipMemcpyDeviceToHost, c->stream));

@@ -8,21 +8,24 @@
 #include <cmath>
 #include <vector>
 
+#include "exact_heap.h"
 #include "search_internal.h"
 
 namespace ulg {
 namespace exact {
 
-struct Node {
-    float g, h;
-    uint64_t sub;
-    uint8_t leaf;
-    int32_t pq;
-};
+
 
 inline bool g_have_bmi2 = __builtin_cpu_supports("bmi2");
 
 __attribute__((target("bmi2"))) inline uint64_t pext_bmi2(uint64_t x, uint64_t m) { return __builtin_ia32_pext_di(x, m); }
+__attribute__((target("bmi2"))) inline uint64_t pdep_bmi2(uint64_t x, uint64_t m) { return __builtin_ia32_pdep_di(x, m); }
+inline uint64_t pdep64(uint64_t x, uint64_t m) {
+    uint64_t r = 0;
+    for (uint64_t b = m; b; b &= b - 1, x >>= 1)
+        if (x & 1ull) r |= b & (0 - b);
+    return r;
+}
 
 // Host view of the best-score lattice: cost per subset of D_v.
 struct HostTables {
@@ -138,145 +141,6 @@ struct SubsetIndex {
     }
     inline void prefetch(uint64_t S) const {
         if (dense) __builtin_prefetch(&slots[slot(S)]);
-    }
-};
-
-// PriorityQueue with the reference's heap algorithms and pqPos bookkeeping.
-// Heap entries carry their node's f = g + h and layer, so a comparison reads
-// the (mostly contiguous) heap array instead of two random Node records.
-// Invariant: every entry's f is its node's current g + h -- what the
-// reference's comparator reads through the node pointer.  A decrease-key
-// refreshes the entry at the node's recorded position; when that position is
-// stale (the reference's __down_heap does not record moves), the node's own
-// entry is found by a scan and refreshed, and the stale slot is sifted as the
-// reference sifts it.
-struct HeapEnt {
-    float f;
-    int32_t layer;
-    uint32_t idx;
-};
-
-struct Heap {
-    std::vector<HeapEnt> a;
-    std::vector<Node> *nodes;
-    bool hang = false;
-
-    inline HeapEnt ent(uint32_t x) const {
-        const Node &N = (*nodes)[x];
-        return HeapEnt{N.g + N.h, __builtin_popcountll(N.sub) & 0xff, x};
-    }
-    // CompareNodeStar: true if x has LOWER priority than y
-    static inline bool cns(const HeapEnt &A, const HeapEnt &B) {
-        const float diff = A.f - B.f;
-        if (std::fabs(diff) < FLT_EPSILON) return (B.layer - A.layer) > 0;
-        return diff > 0;
-    }
-    inline void setpos(const HeapEnt &e, int64_t p) { (*nodes)[e.idx].pq = (int32_t)p; }
-    void push_hole(int64_t hole, int64_t top, HeapEnt value) {
-        int64_t parent = (hole - 1) / 2;
-        while (hole > top && cns(a[parent], value)) {
-            a[hole] = a[parent];
-            setpos(a[hole], hole);
-            hole = parent;
-            parent = (hole - 1) / 2;
-        }
-        a[hole] = value;
-        setpos(value, hole);
-    }
-    void push(uint32_t x) {
-        const HeapEnt e = ent(x);
-        a.push_back(e);
-        push_hole((int64_t)a.size() - 1, 0, e);
-    }
-    void adjust(int64_t hole, int64_t len, HeapEnt value) {
-        const int64_t top = hole;
-        int64_t second = hole;
-        // the moved nodes' pq writes are deferred (in order) behind write
-        // prefetches: nothing reads pq during the sift
-        uint32_t mv_idx[64];
-        int64_t mv_pos[64];
-        int nm = 0;
-        while (second < (len - 1) / 2) {
-            // the grandchildren (4 contiguous entries): the heap outgrows the
-            // caches, and this descent is a chain of dependent loads
-            const int64_t gc = 4 * second + 3;
-            if (gc + 3 < len) {
-                __builtin_prefetch(&a[gc]);
-                __builtin_prefetch(&a[gc + 3]);
-            }
-            second = 2 * (second + 1);
-            if (cns(a[second], a[second - 1])) second--;
-            a[hole] = a[second];
-            __builtin_prefetch(&(*nodes)[a[hole].idx], 1);
-            mv_idx[nm] = a[hole].idx;
-            mv_pos[nm++] = hole;
-            hole = second;
-        }
-        if ((len & 1) == 0 && second == (len - 2) / 2) {
-            second = 2 * (second + 1);
-            a[hole] = a[second - 1];
-            mv_idx[nm] = a[hole].idx;
-            mv_pos[nm++] = hole;
-            hole = second - 1;
-        }
-        for (int i = 0; i < nm; ++i) (*nodes)[mv_idx[i]].pq = (int32_t)mv_pos[i];
-        push_hole(hole, top, value);
-    }
-    uint32_t pop() {
-        const uint32_t ret = a[0].idx;
-        const int64_t last = (int64_t)a.size() - 1;
-        const HeapEnt value = a[last];
-        a[last] = a[0];
-        adjust(0, last, value);
-        a.pop_back();
-        return ret;
-    }
-    void update(uint32_t x) {
-        const int64_t pos = (*nodes)[x].pq;
-        const float fx = (*nodes)[x].g + (*nodes)[x].h;
-        // the reference reads whatever node sits at the recorded position
-        // (capacity memory included, as the vector keeps it)
-        HeapEnt value = a.data()[pos];
-        if (value.idx == x && pos < (int64_t)a.size()) {
-            value.f = fx;
-            a[pos].f = fx;
-        } else {
-            for (HeapEnt &e : a)
-                if (e.idx == x) e.f = fx;
-            value.f = (*nodes)[value.idx].g + (*nodes)[value.idx].h;
-        }
-        const int64_t parent = (pos - 1) / 2;
-        if (pos > 0 && cns(a[parent], value)) {
-            int64_t par = (pos - 1) / 2, index = pos;
-            while (index > 0 && cns(a[par], value)) {
-                a[index] = a[par];
-                setpos(a[index], index);
-                index = par;
-                par = (par - 1) / 2;
-            }
-            if (pos != index) {
-                a[index] = value;
-                setpos(value, index);
-            }
-        } else {
-            // __down_heap as written: follows the left child only and does not
-            // record the moved value's position (priority_queue-inl.h:176-208)
-            const int64_t len = (int64_t)a.size();
-            int64_t index = pos, left = 2 * index + 1, right = 2 * index + 2, largest = len, guard = 0;
-            while (index < len) {
-                if ((right >= len) || ((left < len) && cns(a[right], a[left]))) largest = left;
-                if (largest < len && cns(value, a[largest])) {
-                    if (largest == index || ++guard > 128) { hang = true; break; }  // the reference would spin
-                    a[index] = a[largest];
-                    setpos(a[largest], index);
-                    index = largest;
-                    left = index * 2 + 1;
-                    right = index * 2 + 2;
-                } else
-                    break;
-            }
-            if (pos != index) a[index] = value;
-        }
     }
 };
 

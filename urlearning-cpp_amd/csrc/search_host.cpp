@@ -13,6 +13,8 @@
 // query kernel.
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
+#include <x86intrin.h>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -77,13 +79,20 @@ int astar_one(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool skele
     const uint64_t allVariables = ancestors | the_scc;
     const float upperBound = FLT_MAX;
     int64_t nexp = 0;
-    while (!open.a.empty()) {
+    // ULG_EXACT_PROF=1: cycle split of the replay (pop / successor loop /
+    // pushes / updates) on stderr -- diagnostics only
+    static const bool prof = std::getenv("ULG_EXACT_PROF") != nullptr;
+    uint64_t c_pop = 0, c_succ = 0, c_push = 0, c_upd = 0, t0 = 0, t1 = 0;
+    int64_t n_push = 0, n_upd = 0, n_succ = 0, n_closed = 0;
+    while (!open.empty()) {
         // the -r watchdog (astar_main.cpp:135-138,266): the loop ends without a goal
         if (deadline && (nexp & 4095) == 0 && Clock::now() > *deadline) {
             c->out_of_time = 1;
             break;
         }
+        if (prof) t0 = __rdtsc();
         const uint32_t ui = open.pop();
+        if (prof) { t1 = __rdtsc(); c_pop += t1 - t0; }
         ++nexp;
         const uint64_t variables = nodes[ui].sub;
         if (variables == allVariables) { goal = ui; break; }
@@ -116,19 +125,33 @@ int astar_one(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool skele
                 const float h = T.h(nv, &complete);
                 const uint32_t idx = (uint32_t)nodes.size();
                 nodes.push_back(Node{g, h, nv, (uint8_t)leaf, 0});
+                uint64_t tp = 0;
+                if (prof) tp = __rdtsc();
                 open.push(idx);
+                if (prof) { c_push += __rdtsc() - tp; ++n_push; }
                 generated.insert(nv, idx);
                 continue;
             }
-            if (nodes[si].pq == -2) continue;
+            if (nodes[si].pq == -2) { if (prof) ++n_closed; continue; }
             const float g = ug + T.bs(leaf, variables);
             if (g < nodes[si].g) {
                 nodes[si].leaf = (uint8_t)leaf;
                 nodes[si].g = g;
+                uint64_t tu = 0;
+                if (prof) tu = __rdtsc();
                 open.update((uint32_t)si);
+                if (prof) { c_upd += __rdtsc() - tu; ++n_upd; }
             }
         }
+        if (prof) { c_succ += __rdtsc() - t1; n_succ += __builtin_popcountll(leaves); }
     }
+    if (prof)
+        std::fprintf(stderr,
+                     "exact_prof expanded=%lld successors=%lld pushes=%lld updates=%lld closed_hits=%lld "
+                     "heap_peak=%zu | Gcycles pop=%.3f succ_loop=%.3f (push %.3f, update %.3f) stale_scans=%lld\n",
+                     (long long)nexp, (long long)n_succ, (long long)n_push, (long long)n_upd, (long long)n_closed,
+                     open.a.size(), c_pop * 1e-9, c_succ * 1e-9, c_push * 1e-9, c_upd * 1e-9,
+                     (long long)open.scans);
     *expanded += nexp;
     if (open.hang) *hang = true;
     if (goal < 0) return ULG_OK;
@@ -162,6 +185,157 @@ int astar_one(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool skele
     return ULG_OK;
 }
 
+// ---- the dense form of the same replay ---------------------------------------
+// Scopes of at most kDenseScopeBits variables: every node of the order lattice
+// has a fixed home, recs[pext(S, scope)] (16 B: g, h, the reference's pqPos,
+// leaf), so a successor is one random access that can be prefetched together
+// with its siblings', and the popped node's successor costs are one
+// contiguous row (search_cost_rows_host) instead of one lattice read per
+// successor.  Heap entries are (f, slot), 8 B; a node's layer is
+// popcount(slot), as pext keeps the bit count.  The heap algorithms,
+// comparator, first-generator-wins and no-reopen rule are exactly Heap's
+// (search_exact.h) and the reference's.
+constexpr int kDenseScopeBits = 26;
+constexpr uint64_t kDenseRowsMaxBytes = 8ull << 30;
+
+inline bool dense_eligible(uint64_t scope, uint64_t scc) {
+    const int m = __builtin_popcountll(scope);
+    return m <= kDenseScopeBits && ((1ull << m) * (uint64_t)__builtin_popcountll(scc) * 4) <= kDenseRowsMaxBytes;
+}
+
+// run_astar_on_one_scc (astar_main.cpp:216-546) over dense node homes
+int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool skeleton_good, uint64_t ancestors,
+                uint64_t the_scc, int64_t *expanded, bool *hang, ExactResult &res, const Clock::time_point *deadline) {
+    SearchState &s = *c->search;
+    const int n = T.n;
+    const uint64_t scope = ancestors | the_scc;
+    const int m = __builtin_popcountll(scope);
+    const uint64_t nslots = 1ull << m;
+    const int nl = __builtin_popcountll(the_scc);
+    const float *rows = static_cast<const float *>(s.host_rows.p);
+    HostHuge recmem, heapmem;
+    // the heap's buffer starts 8 B into a line, so a node's two children
+    // (2i+1, 2i+2) share 16 aligned bytes and its 16 great-great-grandchildren
+    // two lines
+    if (!recmem.reserve(nslots * sizeof(DenseRec), false) || !heapmem.reserve((nslots + 16) * sizeof(DEnt), false))
+        return set_err(c, ULG_ERR_HIP, "cannot map the dense search arrays");
+    DenseRec *recs = static_cast<DenseRec *>(recmem.p);
+    DenseHeap open;
+    open.recs = recs;
+    open.a = static_cast<DEnt *>(heapmem.p) + 1;
+    // slot bit of each variable, and its column in the row table
+    uint32_t sbit[64] = {0};
+    int col[64];
+    for (int v = 0; v < 64; ++v) col[v] = -1;
+    {
+        int i = 0;
+        for (uint64_t x = scope; x; x &= x - 1) sbit[__builtin_ctzll(x)] = 1u << i++;
+        i = 0;
+        for (uint64_t x = the_scc; x; x &= x - 1) col[__builtin_ctzll(x)] = i++;
+    }
+    auto slot_of = [&](uint64_t S) { return (uint32_t)(g_have_bmi2 ? pext_bmi2(S, scope) : pext64(S, scope)); };
+    const uint32_t root = slot_of(ancestors), goal_slot = (uint32_t)(nslots - 1);
+    const uint64_t r1 = the_scc >> 1;
+    recs[root] = DenseRec{0.0f, 0.0f, 0, (uint8_t)(r1 ? __builtin_ctzll(r1) + 1 : 0), {0, 0, 0}};
+    open.push(root);
+    int64_t goal = -1;
+    const float upperBound = FLT_MAX;
+    int64_t nexp = 0;
+    static const bool prof = std::getenv("ULG_EXACT_PROF") != nullptr;
+    uint64_t c_pop = 0, c_succ = 0, t0 = 0, t1 = 0;
+    int64_t n_push = 0, n_upd = 0, n_succ = 0;
+    while (open.len > 0) {
+        if (deadline && (nexp & 4095) == 0 && Clock::now() > *deadline) {
+            c->out_of_time = 1;
+            break;
+        }
+        if (prof) t0 = __rdtsc();
+        const uint32_t ui = open.pop();
+        if (prof) { t1 = __rdtsc(); c_pop += t1 - t0; }
+        ++nexp;
+        if (ui == goal_slot) { goal = ui; break; }
+        DenseRec &U = recs[ui];
+        if (U.g + U.h > upperBound) break;
+        U.pq = -1;
+        const float ug = U.g;
+        const uint64_t variables = g_have_bmi2 ? pdep_bmi2(ui, scope) : pdep64(ui, scope);
+        uint64_t leaves = the_scc & ~variables;
+        if (skeleton_good && variables != 0)
+            for (uint64_t x = leaves; x; x &= x - 1) {
+                const int leaf = __builtin_ctzll(x);
+                if ((variables & edges[leaf]) == 0) leaves &= ~(1ull << leaf);
+            }
+        const float *row = rows + (uint64_t)ui * (uint64_t)nl;
+        __builtin_prefetch(row);
+        __builtin_prefetch(row + nl - 1);
+        for (uint64_t x = leaves; x; x &= x - 1) __builtin_prefetch(&recs[ui | sbit[__builtin_ctzll(x)]], 1);
+        for (uint64_t x = leaves; x; x &= x - 1) {
+            const int leaf = __builtin_ctzll(x);
+            const uint32_t si = ui | sbit[leaf];
+            DenseRec &R = recs[si];
+            // getScore(leaf, S u {leaf}) == getScore(leaf, S): leaf is never in its own sets
+            const float g = ug + row[col[leaf]];
+            if (R.pq == 0) {
+                bool complete = false;
+                R.g = g;
+                R.h = T.h(variables | (1ull << leaf), &complete);
+                R.leaf = (uint8_t)leaf;
+                open.push(si);
+                if (prof) ++n_push;
+                continue;
+            }
+            if (R.pq == -1) continue;
+            if (g < R.g) {
+                R.leaf = (uint8_t)leaf;
+                R.g = g;
+                open.update(si);
+                if (prof) ++n_upd;
+            }
+        }
+        if (prof) { c_succ += __rdtsc() - t1; n_succ += __builtin_popcountll(leaves); }
+    }
+    if (prof)
+        std::fprintf(stderr,
+                     "exact_prof(dense) expanded=%lld successors=%lld pushes=%lld updates=%lld heap_peak=%lld | "
+                     "Gcycles pop=%.3f succ_loop=%.3f stale_scans=%lld\n",
+                     (long long)nexp, (long long)n_succ, (long long)n_push, (long long)n_upd, (long long)open.hwm,
+                     c_pop * 1e-9, c_succ * 1e-9, (long long)open.scans);
+    *expanded += nexp;
+    if (open.hang) *hang = true;
+    if (goal < 0) return ULG_OK;
+    // reconstructSolution (astar_main.cpp:140-166)
+    const int count = nl;
+    res.total.assign(n, 0);
+    res.opt.assign(n, 0);
+    std::vector<int> qv;
+    std::vector<uint64_t> qs;
+    std::vector<int> pos;
+    // count = |the_scc|: when the skeleton component overlaps the ancestors
+    // (-p/-s, astar_main.cpp:629-635) the walk reaches the root before count
+    // steps; like the indexed form it stops at the first subnetwork that is
+    // not in generatedNodes (the root never is, :236-237)
+    uint32_t cur = (uint32_t)goal;
+    for (int i = 0; i < count; ++i) {
+        const int leaf = recs[cur].leaf;
+        res.total[count - 1 - i] = leaf;
+        qv.push_back(leaf);
+        qs.push_back(g_have_bmi2 ? pdep_bmi2(cur, scope) : pdep64(cur, scope));
+        pos.push_back(count - 1 - i);
+        cur ^= sbit[leaf];
+        if (cur == root || recs[cur].pq == 0) break;  // the root is never in generatedNodes
+    }
+    if (!qv.empty()) {
+        std::vector<float> qc(qv.size());
+        std::vector<uint64_t> qp(qv.size());
+        int rc = search_query(c, (int64_t)qv.size(), qv.data(), qs.data(), qc.data(), qp.data());
+        if (rc) return rc;
+        for (size_t i = 0; i < qv.size(); ++i) res.opt[pos[i]] = qp[i];
+    }
+    res.found = true;
+    res.goal_g = recs[goal].g;
+    return ULG_OK;
+}
+
 uint64_t all_vars(int n) { return (n >= 64) ? ~0ull : ((1ull << n) - 1ull); }
 
 // New lists: tables over every variable when they fit the budget; otherwise
@@ -173,6 +347,7 @@ int lists_loaded(ulg_ctx *c) {
     s.tables_ready = false;
     s.pdb_ready = false;
     s.host_costs_ready = false;
+    s.rows_ready = false;
     s.triplet_memo.clear();
     const int rc = search_build_tables(c, all_vars(s.n));
     if (rc == ULG_ERR_UNSUPPORTED) {
@@ -379,12 +554,15 @@ int ulg_astar_scc(ulg_ctx *c, const uint64_t *edges, int pd_count, int mode, uin
     bool fail = false;
     for (uint64_t comp : comps) {
         // every lookup of this component's search lies inside ancestors | component
-        if ((rc = search_ensure_scope(c, ancestors | comp)) || (rc = search_cost_table_host(c))) return rc;
+        ExactResult r;
+        const bool dense = dense_eligible(ancestors | comp, comp) && !std::getenv("ULG_EXACT_SPARSE");
+        if ((rc = search_ensure_scope(c, ancestors | comp))) return rc;
+        if ((rc = dense ? search_cost_rows_host(c, ancestors | comp, comp) : search_cost_table_host(c))) return rc;
         HostTables T;
         host_tables(s, T);
-        ExactResult r;
-        if ((rc = astar_one(c, T, edges, good, ancestors, comp, expanded, &hang, r,
-                            c->time_limit_ms > 0 ? &deadline : nullptr)))
+        const Clock::time_point *dl = c->time_limit_ms > 0 ? &deadline : nullptr;
+        if ((rc = dense ? astar_dense(c, T, edges, good, ancestors, comp, expanded, &hang, r, dl)
+                        : astar_one(c, T, edges, good, ancestors, comp, expanded, &hang, r, dl)))
             return rc;
         if (!r.found) { fail = true; continue; }
         // each component rewrites netFile and netFile.csv (astar_main.cpp:470,519)

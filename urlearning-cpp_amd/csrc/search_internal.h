@@ -177,6 +177,22 @@ __device__ inline float pdb_h(const SearchDev &d, uint64_t S, int *complete) {
     return h;
 }
 
+// ---- host memory for the exact-order search -------------------------------------
+// Anonymous mapping with transparent huge pages requested (the replay's
+// random reads into GB-sized arrays would otherwise miss the TLB on almost
+// every access); optionally page-locked for the device copies.  Pages are
+// zero until touched.
+struct HostHuge {
+    void *p = nullptr;
+    size_t bytes = 0;
+    bool pinned = false;
+    // (re)maps at least `want` bytes; returns false if the mapping fails
+    bool reserve(size_t want, bool pin);
+    void zero_prefix(size_t n);  // memset the first n bytes
+    void release();
+    ~HostHuge() { release(); }
+};
+
 // ---- host state -----------------------------------------------------------------
 struct SearchState {
     int n = 0;
@@ -202,6 +218,13 @@ struct SearchState {
     float *host_costs = nullptr;
     uint64_t host_cost_cap = 0;
     bool host_costs_ready = false;
+    // exact-order search: one row of successor costs per subset of the scope,
+    // row[pext(S, scope)][i] = getScore(scc_i, S) (FLT_MAX for scc_i in S)
+    HostHuge host_rows;
+    DevBuf<float> d_rows;      // device staging for the row chunks
+    DevBuf<int> d_rowmeta;     // scope bit positions, scc variables
+    uint64_t rows_scope = 0, rows_scc = 0;
+    bool rows_ready = false;
     // pattern database
     int pd_count = 0;
     uint64_t ancestors = 0, scc = 0;
@@ -245,6 +268,9 @@ struct SearchState {
         release(q_vars); release(q_sets); release(q_par); release(q_costs);
         if (host_costs) (void)hipHostFree(host_costs);
         host_costs = nullptr;
+        release(d_rows); release(d_rowmeta);
+        host_rows.release();
+        rows_ready = false;
         host_cost_cap = 0;
     }
 };
@@ -257,6 +283,9 @@ int search_ensure_scope(ulg_ctx *c, uint64_t need);
 int search_build_pdb(ulg_ctx *c, int pd_count, uint64_t ancestors, uint64_t scc);
 int search_quantize_device(ulg_ctx *c, const float *d_scores, float *d_costs, int64_t count);
 int search_cost_table_host(ulg_ctx *c);
+// row table (SearchState::host_rows) for the dense exact-order search over
+// scope = ancestors | scc; the tables must cover scope
+int search_cost_rows_host(ulg_ctx *c, uint64_t scope, uint64_t scc);
 int search_query(ulg_ctx *c, int64_t count, const int *vars, const uint64_t *S, float *costs, uint64_t *parents);
 int search_pdb_query(ulg_ctx *c, int64_t count, const uint64_t *S, float *h, int *complete);
 

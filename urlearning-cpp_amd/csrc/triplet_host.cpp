@@ -100,7 +100,7 @@ void astar_cluster(const HostTables &T, uint64_t cluster, ClusterRun &R) {
     open.push(0);
     int64_t goal = -1, nexp = 0;
     const float upperBound = FLT_MAX;
-    while (!open.a.empty()) {
+    while (!open.empty()) {
         const uint32_t ui = open.pop();
         ++nexp;
         const uint64_t variables = nodes[ui].sub;
