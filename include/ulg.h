@@ -258,6 +258,11 @@ int ulg_triplet_memo_put(ulg_ctx *ctx, const uint64_t *clusters, int64_t nc,
  * finished so far -- the reference stops mid-layer, at a point that depends
  * on its clock; the exact-order A* checks it every 4096 pops and stops
  * without a goal for that component, as the reference's loop does.
+ * "sweep_table" (0/1, default 1): the GPU search (ULG_ASTAR_GPU) on a
+ * component without a skeleton filter first lays the component's successor
+ * costs out in its own (variable, layer, colex) order (m 2^(m-1) floats,
+ * cached until the tables change) when that fits the free HBM; 0 reads the
+ * binary-indexed lattice per predecessor instead.
  * All variants compute identical results; the knob exists for A/B timing. */
 int ulg_set_option(ulg_ctx *ctx, const char *name, int64_t value);
 /* Read-back of per-call state: "out_of_time" (1 if the last ulg_cbic_score or

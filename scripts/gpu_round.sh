@@ -7,6 +7,10 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 TAG=${TAG:-run}
+# heartbeat: long single tests print nothing until they finish
+( while sleep 45; do date +%T >> gpurun_out/${TAG}_heartbeat; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/${TAG}_pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -n 30 gpurun_out/${TAG}_pytest_gpu.log

@@ -124,3 +124,52 @@ def test_gpu_dag_valid_connected_sparse_skeleton(ulg_ctx):
     ex, gp = _pipeline(ulg_ctx, X, 5, rows)
     check_gpu_dag(ulg_ctx, (1 << n) - 1, gp, n)
     assert abs(gp["cost"] - ex["cost"]) <= 1e-6 * abs(ex["cost"])
+
+
+def _block_skeleton(n, blocks):
+    """Complete skeleton rows on each block of variables (no filter inside a
+    component, so the sweep-table launches run per component)."""
+    rows = [0] * n
+    for b in blocks:
+        m = sum(1 << v for v in b)
+        for v in b:
+            rows[v] = m
+    return rows
+
+
+@pytest.mark.parametrize("case", ["full", "blocks", "scoped"])
+def test_sweep_table_gives_identical_search(ulg_ctx, case):
+    """ulg_set_option("sweep_table"): the (variable, layer, colex) cost slices
+    hold exactly getScore's floats, so the sweep with and without them returns
+    the same goal cost bits, order and parent sets -- on a full skeleton, on
+    complete blocks (components whose variables are not 0..m-1, so the slices
+    map compact positions back through the component), and on those blocks
+    with a table budget below the all-variable tables (tables built per
+    component, scope != every variable)."""
+    import ulg
+    n, N, k = 20, 8000, 4
+    X, _ = synth.gaussian_sem(n, N, 9360)
+    if case in ("blocks", "scoped"):
+        edges = _block_skeleton(n, [[0, 3, 5, 6, 9, 12, 13, 17, 19], [1, 2, 4, 7, 8, 10, 11, 14, 15, 16, 18]])
+    else:
+        edges = [(1 << n) - 1] * n
+    ulg_ctx.load(X, 2.0)
+    ulg_ctx.score(list(range(n)), ulg.candidates_from_edges(edges, n), k)
+    if case == "scoped":
+        ulg_ctx.set_option("table_budget_kb", 4096)  # all-variable tables: 120 MiB
+    try:
+        ulg_ctx.search_from_scores()
+        res = []
+        for on in (0, 1, 1):  # the second 1 reuses the cached slices
+            ulg_ctx.set_option("sweep_table", on)
+            res.append(ulg_ctx.astar(edges=edges, mode=1, net_text=False))
+    finally:
+        ulg_ctx.set_option("sweep_table", 1)
+        ulg_ctx.set_option("table_budget_kb", 0)
+    for r in res[1:]:
+        assert np.float32(r["cost"]).tobytes() == np.float32(res[0]["cost"]).tobytes()
+        assert [int(x) for x in r["order"]] == [int(x) for x in res[0]["order"]]
+        assert [int(x) for x in r["vpar"]] == [int(x) for x in res[0]["vpar"]]
+        assert r["expanded"] == res[0]["expanded"]
+    ex = ulg_ctx.astar(edges=edges, mode=0, net_text=False)
+    assert abs(res[1]["cost"] - ex["cost"]) <= 1e-6 * abs(ex["cost"])

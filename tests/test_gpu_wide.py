@@ -93,3 +93,29 @@ def test_c1_hepatitis_default_parent_limit_matches_digest(ulg_ctx):
             for idx, (ps, pscore) in zip(np.unique(np.linspace(0, len(s) - 1, 64).astype(np.int64)), d["samples"]):
                 assert int(s[idx]) == ps
                 assert abs(float(sc[idx]) - pscore) <= REL_TOL * max(abs(pscore), 1.0), (v, ps, float(sc[idx]), pscore)
+
+
+def test_wide_hicover_prune_identical_lists(ulg_ctx):
+    """ulg_set_option("wide_prune"): the walks skip absent nodes below which no
+    present key reaches -ts.  The stored lists with and without the prune are
+    identical bit for bit, on C4's (n=30, N=100k, MMPC, -p = n-1) variables
+    whose unpruned walks finish in well under a second each."""
+    import ulg
+    n, N = 30, 100000
+    X, _ = synth.gaussian_sem(n, N, 9200)
+    ulg_ctx.load(X, 2.0)
+    rows = ulg_ctx.mmpc(0.01)
+    cands = ulg.candidates_from_edges(rows, n)
+    vs = [10, 14, 29, 4, 16, 27]
+    assert all(9 <= bin(cands[v] & ~(1 << v)).count("1") <= 12 for v in vs)
+    out = []
+    try:
+        for on in (0, 1):
+            ulg_ctx.set_option("wide_prune", on)
+            offs, sets, scores = ulg_ctx.score_all(vs, [cands[v] for v in vs], n - 1)
+            out.append((np.asarray(offs).copy(), np.asarray(sets).copy(), np.asarray(scores).copy()))
+    finally:
+        ulg_ctx.set_option("wide_prune", 1)
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1])
+    assert out[0][2].tobytes() == out[1][2].tobytes()

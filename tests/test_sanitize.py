@@ -22,8 +22,12 @@ OSAN = os.path.join(ORACLE, "build", "san")
 
 @pytest.fixture(scope="module")
 def san_built():
-    subprocess.run(["make", "-C", PKG, "sanitize"], check=True, stdout=subprocess.DEVNULL)
-    subprocess.run(["make", "-C", ORACLE, "sanitize"], check=True, stdout=subprocess.DEVNULL)
+    import fcntl
+    # one builder at a time (pytest-xdist workers share the output tree)
+    with open(os.path.join(PKG, ".sanitize.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-C", PKG, "sanitize"], check=True, stdout=subprocess.DEVNULL)
+        subprocess.run(["make", "-C", ORACLE, "sanitize"], check=True, stdout=subprocess.DEVNULL)
 
 
 def _run(cmd, **extra_env):

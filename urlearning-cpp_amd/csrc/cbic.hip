@@ -1309,6 +1309,8 @@ struct WideArgs {
     float *table;
     uint64_t *queue;          // 3 words per undecided set: slot, compact mask, vi | ts bits << 32
     unsigned long long *qcount;
+    const float *hmax;        // hi-cover tables (hikey_*_kernel) or null
+    const uint64_t *hoff;     // [nv] offset of a variable's table in hmax, ~0 = none
     double N;
     double lambda;
     int n, nv, S, L;
@@ -1448,9 +1450,28 @@ __global__ void __launch_bounds__(64) walk_wide_kernel(WideArgs a, uint64_t qbas
         Plocal = PHASE == 0 ? ((1ull << L) - 1ull) : (((1ull << L) - 1ull) << 1);
     }
     const uint64_t *toffv = a.tbl_off + (uint64_t)vi * a.S;
+    const float thr = -ts;
+    // Hi-cover prune: the walk's answer is only whether it visits a present key
+    // >= -ts (a "hi" key).  From a node T it can only visit subsets of T and
+    // variable 0 (U(T)), so an absent T whose U(T) holds no hi key is not
+    // expanded (marked checked, as its call would have been).  Expanding it
+    // could only change `checked` inside U(T), and every later difference
+    // stays inside U(T) (U is monotone), so the first hi key visited -- the
+    // decision -- is unchanged.  hmax[X] = max over the keys present when
+    // this phase runs of the subsets of the compact mask X.
+    const uint64_t ho = a.hoff ? a.hoff[vi] : ~0ull;
+    auto hi_in_cover = [&](uint64_t T) -> bool {
+        if (ho == ~0ull) return true;
+        uint64_t X = z ? 1ull : 0ull;  // variable 0 (compact bit 0 when it is a candidate)
+        for (uint64_t y = T & ~1ull; y; y &= y - 1) X |= 1ull << lc[__builtin_ctzll(y)];
+        return a.hmax[ho + X] >= thr;
+    };
+    if (!hi_in_cover(Plocal)) {  // no hi key below P at all: stored
+        a.table[slot] = -ts;
+        return;
+    }
     uint64_t *chk = bits + lid * wpl;
     chk[0] |= 1ull;  // checked.insert(empty_set)
-    const float thr = -ts;
 
     uint64_t Ts[LMAX + 1];
     uint8_t idxs[LMAX + 1], is[LMAX + 1], js[LMAX + 1], us[LMAX + 1], inner[LMAX + 1];
@@ -1510,6 +1531,11 @@ __global__ void __launch_bounds__(64) walk_wide_kernel(WideArgs a, uint64_t qbas
                 ++idxs[d];
                 continue;
             }
+            if (!hi_in_cover(T2)) {
+                chk[T2 >> 6] |= 1ull << (T2 & 63);
+                ++idxs[d];
+                continue;
+            }
             inner[d] = 1;
             is[d] = 0;
             js[d] = 0;
@@ -1544,6 +1570,88 @@ WideFn wide_fn(int L, int phase) {
 WideWalkFn wide_walk_fn(int L, int phase) {
     if (L <= 16) return phase == 0 ? walk_wide_kernel<16, 0> : walk_wide_kernel<16, 1>;
     return phase == 0 ? walk_wide_kernel<kWideMax, 0> : walk_wide_kernel<kWideMax, 1>;
+}
+
+// ---- hi-cover tables for the wide walks ---------------------------------
+// Per walking variable (m <= kHiMaxBits candidates), before each wide walk
+// launch: hmax[X] = max over the keys present in the cache when this phase
+// runs (layers < L, and in phase 1 the layer-L sets holding variable 0,
+// SURVEY N4) of their stored value, over every subset of the compact mask X;
+// absent keys count as -inf.  A subset-max (zeta) transform: the low
+// kHiTileBits bits per LDS tile, the rest kHiGroup bits per strided pass.
+constexpr int kHiTileBits = 12;
+constexpr int kHiMaxBits = 24;  // 64 MB of floats per variable at most
+constexpr int kHiGroup = 4;
+
+struct HiArgs {
+    const int *lvars;     // walking variables of this launch (batch index)
+    const int *prefix;    // [nl + 1]: tiles (tile pass) or blocks (strided pass) per variable
+    int nl;
+    const int *meta;
+    const uint64_t *tbl_off;
+    const float *table;
+    const uint64_t *binom;  // [64][64]
+    float *hmax;
+    const uint64_t *hoff;
+    int S, L, kmax, bit_lo;
+};
+
+__device__ __forceinline__ int hi_find(const int *prefix, int nl, int x) {
+    int lo = 0, hi = nl;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (prefix[mid] <= x) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+template <int PHASE>
+__global__ void __launch_bounds__(1024) hikey_tile_kernel(HiArgs a) {
+    __shared__ float t[1 << kHiTileBits];
+    const int li = hi_find(a.prefix, a.nl, blockIdx.x);
+    const int vi = a.lvars[li];
+    const int m = a.meta[vi * 4 + 1];
+    const bool z = a.meta[vi * 4 + 2] != 0;
+    const int tb = m < kHiTileBits ? m : kHiTileBits;
+    const int cnt = 1 << tb;
+    const uint64_t base = (uint64_t)(blockIdx.x - a.prefix[li]) << kHiTileBits;
+    const uint64_t *toff = a.tbl_off + (uint64_t)vi * a.S;
+    for (int i = threadIdx.x; i < cnt; i += 1024) {
+        const uint64_t X = base + (uint64_t)i;
+        const int l = __popcll(X);
+        float val = -INFINITY;
+        if (l <= a.kmax && (l < a.L || (PHASE == 1 && l == a.L && (X & 1ull) && z))) {
+            const float f = a.table[toff[l] + rank_colex64(X, a.binom)];
+            if (fbits(f) != kAbsentBits && f == f) val = f;  // absent or NaN: never >= -ts
+        }
+        t[i] = val;
+    }
+    __syncthreads();
+    for (int b = 0; b < tb; ++b) {
+        for (int i = threadIdx.x; i < cnt; i += 1024)
+            if (!((i >> b) & 1)) t[i | (1 << b)] = fmaxf(t[i | (1 << b)], t[i]);
+        __syncthreads();
+    }
+    float *h = a.hmax + a.hoff[vi] + base;
+    for (int i = threadIdx.x; i < cnt; i += 1024) h[i] = t[i];
+}
+
+__global__ void __launch_bounds__(256) hikey_strided_kernel(HiArgs a) {
+    const int li = hi_find(a.prefix, a.nl, blockIdx.x);
+    const int vi = a.lvars[li];
+    const int m = a.meta[vi * 4 + 1];
+    const int G = m - a.bit_lo < kHiGroup ? m - a.bit_lo : kHiGroup;
+    const uint64_t tid = (uint64_t)(blockIdx.x - a.prefix[li]) * 256 + threadIdx.x;
+    if (G <= 0 || tid >= (1ull << (m - G))) return;
+    const uint64_t lowm = (1ull << a.bit_lo) - 1ull;
+    const uint64_t base = ((tid & ~lowm) << G) | (tid & lowm);
+    float *h = a.hmax + a.hoff[vi];
+    float r[1 << kHiGroup];
+    for (int k = 0; k < (1 << G); ++k) r[k] = h[base + ((uint64_t)k << a.bit_lo)];
+    for (int b = 0; b < G; ++b)
+        for (int k = 0; k < (1 << G); ++k)
+            if (!((k >> b) & 1)) r[k | (1 << b)] = fmaxf(r[k | (1 << b)], r[k]);
+    for (int k = 0; k < (1 << G); ++k) h[base + ((uint64_t)k << a.bit_lo)] = r[k];
 }
 
 __global__ void empty_set_kernel(const uint64_t *tbl_off, int nv, int S, float *table) {
@@ -1876,9 +1984,10 @@ const char *kLayerNames[2][kMaxL + 1] = {
 // the queue length) the walks, in chunks whose checked bitsets fit the budget.
 // `bits` is this stream group's own slice of c->d_wbits (`slice` words): the
 // groups' walks run concurrently on their own streams.
-int score_wide_layer(ulg_ctx *c, int L, int ph, hipStream_t st, const uint64_t *d_work, uint64_t cnt, int nv, int S,
-                     uint64_t *queue, unsigned long long *qc, unsigned long long *errf, uint64_t *bits,
-                     uint64_t slice) {
+int score_wide_layer(ulg_ctx *c, int L, int ph, hipStream_t st, const uint64_t *d_work, const uint64_t *h_work,
+                     uint64_t cnt, int nv, int S, int kmax, uint64_t *queue, unsigned long long *qc,
+                     unsigned long long *errf, uint64_t *bits, uint64_t slice, int *d_hmeta,
+                     const std::vector<uint64_t> &hoff, const std::vector<int> &meta) {
     WideArgs wa;
     wa.gram = c->gram.p;
     wa.binom = c->d_binom64.p;
@@ -1889,6 +1998,8 @@ int score_wide_layer(ulg_ctx *c, int L, int ph, hipStream_t st, const uint64_t *
     wa.table = c->table.p;
     wa.queue = queue;
     wa.qcount = qc;
+    wa.hmax = nullptr;
+    wa.hoff = nullptr;
     wa.N = (double)c->N;
     wa.lambda = c->lambda;
     wa.n = c->n;
@@ -1907,6 +2018,52 @@ int score_wide_layer(ulg_ctx *c, int L, int ph, hipStream_t st, const uint64_t *
     ULG_HIP(c, hipMemcpyAsync(&qn, qc, 8, hipMemcpyDeviceToHost, st));
     ULG_HIP(c, hipStreamSynchronize(st));
     if (qn == 0) return ULG_OK;
+    if (d_hmeta) {
+        // hi-cover tables of this launch's variables: [lvars][tile prefix][one
+        // block prefix per strided pass], one upload
+        std::vector<int> lv;
+        for (int i = 0; i < nv; ++i)
+            if (h_work[i + 1] > h_work[i] && hoff[i] != ~0ull) lv.push_back(i);
+        const int nl = (int)lv.size();
+        if (nl > 0) {
+            int maxm = 0;
+            for (int vi : lv) maxm = std::max(maxm, meta[vi * 4 + 1]);
+            const int passes = maxm > kHiTileBits ? (maxm - kHiTileBits + kHiGroup - 1) / kHiGroup : 0;
+            std::vector<int> hm((size_t)nl + (size_t)(nl + 1) * (1 + passes), 0);
+            for (int i = 0; i < nl; ++i) hm[i] = lv[i];
+            int *tp = hm.data() + nl;
+            for (int i = 0; i < nl; ++i) {
+                const int m = meta[lv[i] * 4 + 1];
+                tp[i + 1] = tp[i] + (m <= kHiTileBits ? 1 : 1 << (m - kHiTileBits));
+            }
+            for (int p = 0; p < passes; ++p) {
+                int *bp = tp + (size_t)(nl + 1) * (1 + p);
+                const int bit_lo = kHiTileBits + p * kHiGroup;
+                for (int i = 0; i < nl; ++i) {
+                    const int m = meta[lv[i] * 4 + 1];
+                    const int G = std::min(kHiGroup, m - bit_lo);
+                    bp[i + 1] = bp[i] + (G > 0 ? (int)(((1ull << (m - G)) + 255) / 256) : 0);
+                }
+            }
+            ULG_HIP(c, hipMemcpyAsync(d_hmeta, hm.data(), hm.size() * 4, hipMemcpyHostToDevice, st));
+            HiArgs ha{d_hmeta, d_hmeta + nl, nl, c->d_meta.p, c->d_tbl_off.p, c->table.p, c->d_binom64.p,
+                      c->d_hmax.p, c->d_hoff.p, S, L, kmax, 0};
+            prof_begin_s(c, "wide_hicover", st);
+            if (ph == 0) hikey_tile_kernel<0><<<tp[nl], 1024, 0, st>>>(ha);
+            else hikey_tile_kernel<1><<<tp[nl], 1024, 0, st>>>(ha);
+            for (int p = 0; p < passes; ++p) {
+                ha.prefix = d_hmeta + nl + (size_t)(nl + 1) * (1 + p);
+                ha.bit_lo = kHiTileBits + p * kHiGroup;
+                const int nb = tp[(size_t)(nl + 1) * (1 + p) + nl];
+                if (nb > 0) hikey_strided_kernel<<<nb, 256, 0, st>>>(ha);
+            }
+            prof_end_s(c, st);
+            ULG_HIP(c, hipGetLastError());
+            ULG_HIP(c, hipStreamSynchronize(st));  // hm must outlive its copy
+            wa.hmax = c->d_hmax.p;
+            wa.hoff = c->d_hoff.p;
+        }
+    }
     // checked bitset: 2^q bits per walking set, q = L (P holds variable 0) or L + 1
     const int q = ph == 0 ? L : L + 1;
     const uint64_t wpl = q <= 6 ? 1ull : (1ull << (q - 6));
@@ -2130,10 +2287,28 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     // wide-layer walks: one checked-bitset slice per stream group, allocated
     // before any launch (2^q bits per walking set, q <= kmax + 1)
     uint64_t wslice = 0;
+    std::vector<uint64_t> hoff;
     if (kmax > kMaxL) {
         const uint64_t wpl_max = kmax + 1 <= 6 ? 1ull : (1ull << (kmax + 1 - 6));
         wslice = std::max<uint64_t>(kWideBitsWords / (uint64_t)G, wpl_max);
         if ((rc = ensure(c, c->d_wbits, (size_t)(G * wslice)))) return rc;
+        // hi-cover tables for the variables that reach a wide layer
+        if (c->wide_prune) {
+            hoff.assign(nv, ~0ull);
+            uint64_t htot = 0;
+            for (int i = 0; i < nv; ++i)
+                if (std::min(mv[i], max_parents) > kMaxL && mv[i] <= kHiMaxBits) {
+                    hoff[i] = htot;
+                    htot += 1ull << mv[i];
+                }
+            if (htot > 0) {
+                if ((rc = ensure(c, c->d_hmax, (size_t)htot)) || (rc = upload(c, c->d_hoff, c->mir_hoff, hoff)) ||
+                    (rc = ensure(c, c->d_hmeta, (size_t)G * (nv + (size_t)(nv + 1) * 8))))
+                    return rc;
+            } else {
+                hoff.clear();
+            }
+        }
     }
     // Small layers (L <= Ls, little work, latency-bound): one one-pass launch
     // per phase over all variables on the context stream -- no queue, no walk
@@ -2184,10 +2359,14 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
                 const uint64_t blocks = (cnt + kBlock - 1) / kBlock;
                 if (blocks > 0x7fffffffull) return set_err(c, ULG_ERR_UNSUPPORTED, "ulg_cbic_score: layer too large");
                 if (L > kMaxL) {
-                    if ((rc = score_wide_layer(c, L, ph, st, d_wk + wo, cnt, nv, S, c->d_wqueue.p + g * wqwords,
+                    if ((rc = score_wide_layer(c, L, ph, st, d_wk + wo, h_wk.data() + wo, cnt, nv, S, kmax,
+                                               c->d_wqueue.p + g * wqwords,
                                                c->d_qcount.p + (size_t)g * 2 * (kmax + 1) + (L * 2 + ph),
                                                c->d_qcount.p + nqc - 1, c->d_wbits.p + (size_t)g * wslice,
-                                               wslice)))
+                                               wslice,
+                                               hoff.empty() ? nullptr
+                                                            : c->d_hmeta.p + (size_t)g * (nv + (size_t)(nv + 1) * 8),
+                                               hoff, meta)))
                         return rc;
                     continue;
                 }

@@ -435,6 +435,7 @@ int search_build_tables(ulg_ctx *c, uint64_t scope) {
     s.pdb_ready = false;
     s.host_costs_ready = false;
     s.rows_ready = false;
+    s.sweep_ready = false;
     s.support = support;
     s.mbits.assign(n, 0);
     s.tb_off.assign(n + 1, 0);

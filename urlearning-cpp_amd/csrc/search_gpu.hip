@@ -41,12 +41,22 @@ struct LayerArgs {
     float *gcur;             // layer
     uint8_t *leaf;           // leaf bytes of this layer
     unsigned long long *reached;  // kCounters striped counters of reached nodes (null: the goal layer)
+    const float *w;          // sweep table (SearchState::d_sweep_w) or null
+    uint64_t w_half;         // 2^(m-1): one variable's slice group
+    uint64_t w_layer;        // sum_{q < layer-1} C(m-1, q): the slice of the predecessors' layer
 };
 
 constexpr int kCounters = 256;
 
 __device__ __forceinline__ uint64_t Bn(const uint64_t *b, int a, int k) { return b[a * 33 + k]; }
 
+// kW: the costs come from the sweep table -- the predecessor T \ a_j's cost
+// for leaf a_j sits at w[a_j][layer-1][rank of T \ a_j with a_j's position
+// closed], one contiguous slice per (variable, layer), so a launch's cost
+// reads stay inside its layer's slices (about a MALL's worth at C3) instead
+// of spreading over the whole binary-indexed lattice.  Only for launches
+// without the skeleton filter.
+template <bool kW>
 __global__ void __launch_bounds__(kB) layer_pull_kernel(LayerArgs a) {
     __shared__ uint64_t binom[33 * 33];
     __shared__ int cv[kMaxM];
@@ -98,11 +108,17 @@ __global__ void __launch_bounds__(kB) layer_pull_kernel(LayerArgs a) {
         connected = seen == Tg;
     }
     // rank(T \ a_j) = sum_{i<j} C(a_i, i+1) + sum_{i>j} C(a_i, i)   (a_0 < a_1 < ...)
-    uint64_t suffix = 0;
+    // the same rank in the universe without a_j (elements above a_j move down
+    // one): sum_{i<j} C(a_i, i+1) + sum_{i>j} C(a_i - 1, i)
+    uint64_t suffix = 0, suffixc = 0;
     if (connected) {
         int i = 0;
         for (uint64_t x = Tc; x; x &= x - 1, ++i)
-            if (i >= 1) suffix += Bn(binom, __builtin_ctzll(x), i);
+            if (i >= 1) {
+                const int ai = __builtin_ctzll(x);
+                suffix += Bn(binom, ai, i);
+                if (kW) suffixc += Bn(binom, ai - 1, i);
+            }
     }
     uint64_t prefix = 0;
     float best = FLT_MAX;
@@ -112,22 +128,38 @@ __global__ void __launch_bounds__(kB) layer_pull_kernel(LayerArgs a) {
     for (int j = 0; j < (connected ? L : 0); ++j) {
         const int aj = __builtin_ctzll(x);
         x &= x - 1;  // x now holds a_{j+1}, ...
-        const int leaf = cv[aj];
-        const uint64_t P = Tg & ~(1ull << leaf);
-        bool ok = !(a.skeleton && P != 0 && (P & a.edges[leaf]) == 0);
-        if (ok) {
+        if (kW) {
             const float gp = a.gprev[prefix + suffix];
             if (gp < FLT_MAX) {
                 reached = true;
-                const float cand = gp + bs_cost(a.d, leaf, P);
+                const float cand = gp + a.w[(uint64_t)aj * a.w_half + a.w_layer + prefix + suffixc];
                 if (cand < best || bestj == 255) {
                     best = cand;
                     bestj = j;
                 }
             }
+        } else {
+            const int leaf = cv[aj];
+            const uint64_t P = Tg & ~(1ull << leaf);
+            bool ok = !(a.skeleton && P != 0 && (P & a.edges[leaf]) == 0);
+            if (ok) {
+                const float gp = a.gprev[prefix + suffix];
+                if (gp < FLT_MAX) {
+                    reached = true;
+                    const float cand = gp + bs_cost(a.d, leaf, P);
+                    if (cand < best || bestj == 255) {
+                        best = cand;
+                        bestj = j;
+                    }
+                }
+            }
         }
         // advance to j+1: a_{j+1} leaves the suffix, a_j joins the prefix
-        if (x) suffix -= Bn(binom, __builtin_ctzll(x), j + 1);
+        if (x) {
+            const int an = __builtin_ctzll(x);
+            suffix -= Bn(binom, an, j + 1);
+            if (kW) suffixc -= Bn(binom, an - 1, j + 1);
+        }
         prefix += Bn(binom, aj, j + 1);
     }
     a.gcur[r] = reached ? best : FLT_MAX;
@@ -138,6 +170,39 @@ __global__ void __launch_bounds__(kB) layer_pull_kernel(LayerArgs a) {
         if ((threadIdx.x & 63) == __ffsll((long long)__ballot(true)) - 1 && b)
             atomicAdd(&a.reached[blockIdx.x % kCounters], (unsigned long long)__popcll(b));
     }
+}
+
+// Sweep table of one component: thread f of variable slot j (blockIdx.y)
+// holds getScore(v_j, P) for the f-th (m-1)-bit set in (layer, colex) order,
+// P mapped back to the variables with v_j's position opened.  Blocks are
+// dispatched j-major, so the running blocks read one variable's lattice
+// (64 MB at C3) at a time.
+__global__ void __launch_bounds__(kB) sweep_w_kernel(SearchDev d, const uint64_t *gbinom, const uint64_t *loffm1,
+                                                     const int *comp_vars, int m, uint64_t half, float *w) {
+    __shared__ uint64_t binom[33 * 33];
+    __shared__ uint64_t lo[kMaxM + 1];
+    __shared__ int cv[kMaxM];
+    for (int e = threadIdx.x; e < m * 33; e += kB) binom[e] = gbinom[e];
+    for (int i = threadIdx.x; i <= m; i += kB) lo[i] = loffm1[i];
+    for (int i = threadIdx.x; i < m; i += kB) cv[i] = comp_vars[i];
+    __syncthreads();
+    const uint64_t f = (uint64_t)blockIdx.x * kB + threadIdx.x;
+    const int j = blockIdx.y;
+    if (f >= half) return;
+    int p = 0;
+    while (p + 1 < m && lo[p + 1] <= f) ++p;
+    uint64_t rr = f - lo[p], x = 0;
+    int c = m - 2;
+    for (int i = p; i >= 1; --i) {
+        while (Bn(binom, c, i) > rr) --c;
+        x |= 1ull << c;
+        rr -= Bn(binom, c, i);
+        --c;
+    }
+    const uint64_t Pc = ((x >> j) << (j + 1)) | (x & ((1ull << j) - 1ull));
+    uint64_t Pg = 0;
+    for (uint64_t y = Pc; y; y &= y - 1) Pg |= 1ull << cv[__builtin_ctzll(y)];
+    w[(uint64_t)j * half + f] = bs_cost(d, cv[j], Pg);
 }
 
 // walk the leaf pointers from the goal back to the root (one thread)
@@ -266,12 +331,48 @@ int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, flo
             if (comp & ~(edges[b] | (1ull << b))) complete = false;
         }
         const int filt = edges && !complete ? 1 : 0;
+        // sweep table for launches without the filter (full / complete skeleton)
+        const uint64_t half = m >= 1 ? (1ull << (m - 1)) : 1ull;
+        std::vector<uint64_t> loffm1(kMaxM + 1, 0);
+        for (int p = 0; p < m; ++p) loffm1[p + 1] = loffm1[p] + binom64(m - 1, p);
+        bool use_w = !filt && m >= 2 && c->sweep_table != 0;
+        if (use_w && !(s.sweep_ready && s.sweep_comp == comp)) {
+            s.sweep_ready = false;
+            size_t free_b = 0, tot_b = 0;
+            e = hipMemGetInfo(&free_b, &tot_b);
+            const uint64_t need = (uint64_t)m * half;
+            if (e != hipSuccess || need * 4 + ((size_t)1 << 30) > free_b + (size_t)s.d_sweep_w.cap * 4) {
+                use_w = false;  // no room: the lattice-read launches
+            } else {
+                DevBuf<uint64_t> d_lo;
+                if ((rc = ensure(c, s.d_sweep_w, (size_t)need)) || (rc = ensure(c, d_lo, kMaxM + 1))) {
+                    release(d_lo);
+                    cleanup();
+                    return rc;
+                }
+                e = hipMemcpyAsync(d_lo.p, loffm1.data(), (kMaxM + 1) * 8, hipMemcpyHostToDevice, c->stream);
+                if (e == hipSuccess) {
+                    prof_begin(c, "search_sweep_w");
+                    sweep_w_kernel<<<dim3((unsigned)((half + kB - 1) / kB), (unsigned)m), kB, 0, c->stream>>>(
+                        dv, d_bn.p, d_lo.p, d_cv.p, m, half, s.d_sweep_w.p);
+                    prof_end(c);
+                    e = hipGetLastError();
+                }
+                if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+                release(d_lo);
+                if (e != hipSuccess) { cleanup(); return set_err(c, ULG_ERR_HIP, hipGetErrorString(e)); }
+                s.sweep_ready = true;
+                s.sweep_comp = comp;
+            }
+        }
         for (int d = 1; d <= m; ++d) {
             const uint64_t cnt = binom64(m, d);
             LayerArgs a{dv, d_bn.p, d_cv.p, d_edges.p, filt, symmetric && filt ? 1 : 0, m, d, cnt, gprev, gcur,
-                        d_leaf.p + loff[d], d < m ? d_acc.p : nullptr};
+                        d_leaf.p + loff[d], d < m ? d_acc.p : nullptr,
+                        use_w ? s.d_sweep_w.p : nullptr, half, loffm1[d - 1]};
             prof_begin(c, "search_layer_pull");
-            layer_pull_kernel<<<(unsigned)((cnt + kB - 1) / kB), kB, 0, c->stream>>>(a);
+            if (use_w) layer_pull_kernel<true><<<(unsigned)((cnt + kB - 1) / kB), kB, 0, c->stream>>>(a);
+            else layer_pull_kernel<false><<<(unsigned)((cnt + kB - 1) / kB), kB, 0, c->stream>>>(a);
             prof_end(c);
             std::swap(gprev, gcur);
         }

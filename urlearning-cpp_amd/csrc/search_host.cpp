@@ -348,6 +348,7 @@ int lists_loaded(ulg_ctx *c) {
     s.pdb_ready = false;
     s.host_costs_ready = false;
     s.rows_ready = false;
+    s.sweep_ready = false;
     s.triplet_memo.clear();
     const int rc = search_build_tables(c, all_vars(s.n));
     if (rc == ULG_ERR_UNSUPPORTED) {

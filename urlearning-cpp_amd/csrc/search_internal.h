@@ -225,6 +225,12 @@ struct SearchState {
     DevBuf<int> d_rowmeta;     // scope bit positions, scc variables
     uint64_t rows_scope = 0, rows_scc = 0;
     bool rows_ready = false;
+    // GPU sweep: the component's successor costs in the sweep's own order,
+    // sweep_w[j][p][colex rank of P among the (m-1)-subsets of comp \ {v_j}]
+    // = getScore(v_j, P), |P| = p (one contiguous slice per variable and layer)
+    DevBuf<float> d_sweep_w;
+    uint64_t sweep_comp = 0;
+    bool sweep_ready = false;
     // pattern database
     int pd_count = 0;
     uint64_t ancestors = 0, scc = 0;
@@ -269,6 +275,8 @@ struct SearchState {
         if (host_costs) (void)hipHostFree(host_costs);
         host_costs = nullptr;
         release(d_rows); release(d_rowmeta);
+        release(d_sweep_w);
+        sweep_ready = false;
         host_rows.release();
         rows_ready = false;
         host_cost_cap = 0;

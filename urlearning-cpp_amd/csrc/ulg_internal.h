@@ -75,7 +75,9 @@ struct ulg_ctx {
     int64_t time_limit_ms = 0;     // -r: wall-clock budget per scoring call / search (0 = none)
     int out_of_time = 0;           // the last scoring call or search ran out of its budget
     int completed_layer = -1;      // highest fully scored layer of the last scoring call
-    uint64_t table_budget_kb = 0;  // best-score table budget in KiB (0 = half the free HBM)  // see ScoreArgs::variant (ulg_set_option "score_variant")
+    uint64_t table_budget_kb = 0;  // best-score table budget in KiB (0 = half the free HBM)
+    int sweep_table = 1;
+    int wide_prune = 1;            // wide walks: skip absent nodes whose subsets hold no key >= -ts           // GPU search: successor costs in the sweep's (layer, colex) order
     ulg::DevBuf<float> table;
     ulg::DevBuf<uint64_t> d_tbl_off, d_work, d_blk;
     ulg::DevBuf<uint8_t> d_cand;  // [nv][64] compact index -> variable
@@ -107,7 +109,10 @@ struct ulg_ctx {
     std::set<std::string> prof_only;  // ulg_profile_select: time only these kernels
     bool prof_skip = false;
     std::vector<hipEvent_t> event_pool;
-    ulg::Mirror mir_tbl_off, mir_work, mir_cand, mir_meta, mir_workg;
+    ulg::Mirror mir_tbl_off, mir_work, mir_cand, mir_meta, mir_workg, mir_hoff;
+    ulg::DevBuf<float> d_hmax;      // wide walks: hi-cover tables (subset max of the present keys)
+    ulg::DevBuf<uint64_t> d_hoff;   // [nv] table offsets, ~0 = no table
+    ulg::DevBuf<int> d_hmeta;       // per stream group: launch variables and tile / block prefixes
     std::map<std::string, std::vector<double>> prof_ms;
 };
 
