@@ -231,6 +231,32 @@ int ulg_triplet_solve(ulg_ctx *ctx, const uint64_t *clusters, int64_t nc,
 int ulg_triplet_memo_put(ulg_ctx *ctx, const uint64_t *clusters, int64_t nc,
                          int pd_count, const uint64_t *parents);
 
+/* ---- order-graph sweep with variable-sharded tables ----------
+ * Replaces run_astar_on_one_scc (astar_main.cpp:216-546) for a full skeleton
+ * when one GPU cannot hold every variable's best-score lattice (n >= 31: at
+ * n = 32, 32 x 2^31 x 4 B = 275 GB).  Every rank holds every variable's
+ * parent-set lists (after the list all-gather) but builds the tables and
+ * sweep slices of its own variables only.  Layer by layer (1..n):
+ *   ulg_sweep_shard_layer writes, for each of the layer's C(n, layer) nodes
+ *     in colex order, this rank's best candidate over the leaves it owns as
+ *     a key (ordered cost << 8 | leaf position; 0xFFFFFFFFFF = none) into
+ *     keys_dev (device memory, int64-compatible: every key is < 2^40);
+ *   the caller MIN-all-reduces keys_dev over the ranks (one RCCL all-reduce
+ *     per layer: the smallest cost, then the smallest leaf position -- the
+ *     single-GPU sweep's first-strict-minimum rule);
+ *   ulg_sweep_shard_commit turns the reduced keys into the layer's g and
+ *     leaf bytes (every rank holds all of them).
+ * ulg_sweep_shard_end reconstructs the DAG as ULG_ASTAR_GPU does; the result
+ * equals the single-GPU ulg_astar(..., ULG_ASTAR_GPU, ...) on a full skeleton
+ * bit for bit.  *max_layer_nodes = the largest C(n, layer) (size keys_dev for
+ * it).  NaN costs are not supported (their key order differs from the
+ * single-GPU float compare). */
+int ulg_sweep_shard_begin(ulg_ctx *ctx, uint64_t own, int64_t *max_layer_nodes);
+int ulg_sweep_shard_layer(ulg_ctx *ctx, int layer, uint64_t *keys_dev);
+int ulg_sweep_shard_commit(ulg_ctx *ctx, int layer, const uint64_t *keys_dev);
+int ulg_sweep_shard_end(ulg_ctx *ctx, uint64_t *vpar, int *order, float *goal_cost,
+                        int64_t *expanded);
+
 /* ---- tuning knobs -------------------------------------------------------
  * "score_variant" (0..7, 13, 16, 17; default 17): bit 0 = fully unrolled
  * presence gather in the scorer (layers <= 6), bit 1 = stack-machine

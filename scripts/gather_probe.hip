@@ -76,6 +76,7 @@ int main() {
     CK(hipEventCreate(&e1));
     const unsigned blocks = (unsigned)(cnt / 256);
     std::printf("{\"launches\": [");
+    bool first = true;
     auto timed = [&](const char *name, uint64_t bytes, auto launch) {
         CK(hipDeviceSynchronize());
         CK(hipEventRecord(e0));
@@ -84,7 +85,6 @@ int main() {
         CK(hipEventSynchronize(e1));
         float ms = 0.f;
         CK(hipEventElapsedTime(&ms, e0, e1));
-        static bool first = true;
         std::printf("%s{\"name\": \"%s\", \"known_read_bytes\": %llu, \"ms\": %.4f}", first ? "" : ", ", name,
                     (unsigned long long)bytes, ms);
         first = false;

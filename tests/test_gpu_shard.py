@@ -122,3 +122,58 @@ def test_bench_two_ranks_on_one_gpu_matches_one_rank():
     assert two["astar"]["lists_sha256"] == one["astar"]["lists_sha256"]
     assert two["astar"]["gpu_search"]["goal_cost"] == one["astar"]["gpu_search"]["goal_cost"]
     assert two["shard_step"]["exchange_ms"] > 0
+    assert two["astar"]["table_sharded_sweep"]["same_as_replica"] is True
+
+
+def _sweep_worker(rank, world, port, out_dir, n, N, k, seed):
+    sys.path[:0] = [os.path.join(ROOT, "urlearning-cpp_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    import shard
+    import synth
+    import ulg
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    X, _ = synth.gaussian_sem(n, N, seed)
+    ctx = ulg.Context(0)
+    ctx.load(X, 2.0)
+    ctx.score(list(range(n)), [(1 << n) - 1] * n, k)
+    ctx.search_from_scores()
+    masks = shard.table_owners(n, world)
+    res = shard.sharded_sweep(ctx, n, masks[rank], device="cuda", comm_device="cpu")
+    np.savez(os.path.join(out_dir, f"s{rank}.npz"), cost=np.float32(res["cost"]), vpar=res["vpar"],
+             order=res["order"], exp=np.int64(res["expanded"]), own=np.uint64(masks[rank]))
+    # the tables are back to every variable for the next search on this context
+    ctx.set_option("sweep_table", 1)
+    again = ctx.astar(edges=[(1 << n) - 1] * n, mode=1, net_text=False)
+    assert np.float32(again["cost"]).tobytes() == np.float32(res["cost"]).tobytes()
+    ctx.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,n,N,k,seed", [(2, 20, 10000, 4, 9200), (3, 22, 6000, 5, 9751)])
+def test_table_sharded_sweep_equals_single_gpu(tmp_path, ulg_ctx, world, n, N, k, seed):
+    """SURVEY 8e's n >= 31 path, rehearsed at small n: each rank holds the
+    best-score tables and sweep slices of its own variables only
+    (ulg_sweep_shard_begin), one MIN all-reduce per layer combines the ranks'
+    (cost, leaf) keys.  Cost bits, order, parent sets and the reached-node
+    count equal the single-GPU sweep's; the owned variables partition 0..n-1."""
+    import synth
+    mp.start_processes(_sweep_worker, args=(world, _free_port(), str(tmp_path), n, N, k, seed), nprocs=world,
+                       join=True, start_method="spawn")
+    X, _ = synth.gaussian_sem(n, N, seed)
+    ulg_ctx.load(X, 2.0)
+    ulg_ctx.score(list(range(n)), [(1 << n) - 1] * n, k)
+    ulg_ctx.search_from_scores()
+    ref = ulg_ctx.astar(edges=[(1 << n) - 1] * n, mode=1, net_text=False)
+    owned = 0
+    for r in range(world):
+        d = np.load(tmp_path / f"s{r}.npz")
+        assert np.float32(d["cost"]).tobytes() == np.float32(ref["cost"]).tobytes(), r
+        assert [int(x) for x in d["order"]] == [int(x) for x in ref["order"]], r
+        assert [int(x) for x in d["vpar"]] == [int(x) for x in ref["vpar"]], r
+        assert int(d["exp"]) == ref["expanded"], r
+        assert owned & int(d["own"]) == 0
+        owned |= int(d["own"])
+    assert owned == (1 << n) - 1

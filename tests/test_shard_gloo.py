@@ -160,3 +160,21 @@ def test_triplet_memo_exchange_complete_on_every_rank(tmp_path, world):
         assert np.array_equal(d["cl"][order], np.sort(d["all"]))
         for c, row in zip(d["cl"], d["pa"]):
             assert [int(x) for x in row] == [(int(c) * 2654435761 + v) & ((1 << n) - 1) for v in range(n)]
+
+
+def test_table_owners_partition_balanced():
+    import shard
+    for n, ws in [(32, 8), (30, 4), (25, 3), (5, 8)]:
+        masks = shard.table_owners(n, ws)
+        assert len(masks) == ws
+        acc = 0
+        for m in masks:
+            assert acc & m == 0
+            acc |= m
+        assert acc == (1 << n) - 1
+        sizes = [bin(m).count("1") for m in masks]
+        assert max(sizes) - min(sizes) <= 1  # full skeleton: every table is 2^(n-1)
+    # a sparse skeleton: balanced on 2^{m_v}
+    cands = [(1 << 10) - 1] + [0b11] * 9
+    masks = shard.table_owners(10, 2, cands)
+    assert masks[0] == 1 and masks[1] == ((1 << 10) - 1) & ~1

@@ -1310,7 +1310,8 @@ struct WideArgs {
     uint64_t *queue;          // 3 words per undecided set: slot, compact mask, vi | ts bits << 32
     unsigned long long *qcount;
     const float *hmax;        // hi-cover tables (hikey_*_kernel) or null
-    const uint64_t *hoff;     // [nv] offset of a variable's table in hmax, ~0 = none
+    const float *pval;        // the same variables' present keys by compact mask (absent bits otherwise)
+    const uint64_t *hoff;     // [nv] offset of a variable's tables in hmax / pval, ~0 = none
     double N;
     double lambda;
     int n, nv, S, L;
@@ -1459,26 +1460,28 @@ __global__ void __launch_bounds__(64) walk_wide_kernel(WideArgs a, uint64_t qbas
     // stays inside U(T) (U is monotone), so the first hi key visited -- the
     // decision -- is unchanged.  hmax[X] = max over the keys present when
     // this phase runs of the subsets of the compact mask X.
+    // With the tables, a node also carries its compact mask Tc (variable 0 is
+    // compact bit 0 when it is a candidate), and the presence test is one read
+    // of pval[Tc] instead of a colex rank over the node's bits.
     const uint64_t ho = a.hoff ? a.hoff[vi] : ~0ull;
-    auto hi_in_cover = [&](uint64_t T) -> bool {
-        if (ho == ~0ull) return true;
-        uint64_t X = z ? 1ull : 0ull;  // variable 0 (compact bit 0 when it is a candidate)
-        for (uint64_t y = T & ~1ull; y; y &= y - 1) X |= 1ull << lc[__builtin_ctzll(y)];
-        return a.hmax[ho + X] >= thr;
-    };
-    if (!hi_in_cover(Plocal)) {  // no hi key below P at all: stored
+    const bool dense = ho != ~0ull;
+    const uint64_t zb = z ? 1ull : 0ull;
+    auto cbit = [&](int u) -> uint64_t { return u == 0 ? zb : (1ull << lc[u]); };
+    auto hi_in_cover = [&](uint64_t Tc) -> bool { return !dense || a.hmax[ho + (Tc | zb)] >= thr; };
+    if (!hi_in_cover(cm)) {  // no hi key below P at all: stored
         a.table[slot] = -ts;
         return;
     }
     uint64_t *chk = bits + lid * wpl;
     chk[0] |= 1ull;  // checked.insert(empty_set)
 
-    uint64_t Ts[LMAX + 1];
+    uint64_t Ts[LMAX + 1], Tcs[LMAX + 1];
     uint8_t idxs[LMAX + 1], is[LMAX + 1], js[LMAX + 1], us[LMAX + 1], inner[LMAX + 1];
     uint8_t pvs[LMAX * (LMAX + 1) / 2 + 1];
     for (int i = 0; i < L; ++i) pvs[i] = (uint8_t)(i + (PHASE == 0 ? 0 : 1));
     int d = 0;
     Ts[0] = Plocal;
+    Tcs[0] = cm;
     idxs[0] = 0;
     inner[0] = 0;
     bool dom = false;
@@ -1504,10 +1507,24 @@ __global__ void __launch_bounds__(64) walk_wide_kernel(WideArgs a, uint64_t qbas
                 ++idxs[d];
                 continue;
             }
+            const uint64_t T2c = Tcs[d] ^ cbit(u);
             // is T2 in the cache as it stood when P was scored?
             bool present = false;
             const int pc = __popcll(T2);
-            if (pc < L || (PHASE == 1 && pc == L && (T2 & 1ull))) {
+            if (dense) {
+                // pval holds exactly the keys of that cache (hikey_tile_kernel);
+                // variable 0 outside the candidates is never a key's member
+                if (!(PHASE == 1 && (T2 & 1ull) && !z)) {
+                    const float val = a.pval[ho + T2c];
+                    if (fbits(val) != kAbsentBits) {
+                        present = true;
+                        if (val >= thr) {
+                            dom = true;
+                            break;
+                        }
+                    }
+                }
+            } else if (pc < L || (PHASE == 1 && pc == L && (T2 & 1ull))) {
                 if (!(PHASE == 1 && (T2 & 1ull) && !z)) {
                     uint64_t rk = 0, rem = T2;
                     int j = 0;
@@ -1531,7 +1548,7 @@ __global__ void __launch_bounds__(64) walk_wide_kernel(WideArgs a, uint64_t qbas
                 ++idxs[d];
                 continue;
             }
-            if (!hi_in_cover(T2)) {
+            if (!hi_in_cover(T2c)) {
                 chk[T2 >> 6] |= 1ull << (T2 & 63);
                 ++idxs[d];
                 continue;
@@ -1554,6 +1571,7 @@ __global__ void __launch_bounds__(64) walk_wide_kernel(WideArgs a, uint64_t qbas
         pvs[po + mm + js[d]] = pi;
         ++js[d];
         Ts[d + 1] = Ts[d] ^ (1ull << us[d]);
+        Tcs[d + 1] = Tcs[d] ^ cbit(us[d]);
         idxs[d + 1] = 0;
         inner[d + 1] = 0;
         ++d;
@@ -1592,6 +1610,7 @@ struct HiArgs {
     const float *table;
     const uint64_t *binom;  // [64][64]
     float *hmax;
+    float *pval;
     const uint64_t *hoff;
     int S, L, kmax, bit_lo;
 };
@@ -1619,11 +1638,13 @@ __global__ void __launch_bounds__(1024) hikey_tile_kernel(HiArgs a) {
     for (int i = threadIdx.x; i < cnt; i += 1024) {
         const uint64_t X = base + (uint64_t)i;
         const int l = __popcll(X);
-        float val = -INFINITY;
+        float val = -INFINITY, pv = absent_f();
         if (l <= a.kmax && (l < a.L || (PHASE == 1 && l == a.L && (X & 1ull) && z))) {
             const float f = a.table[toff[l] + rank_colex64(X, a.binom)];
+            pv = f;
             if (fbits(f) != kAbsentBits && f == f) val = f;  // absent or NaN: never >= -ts
         }
+        a.pval[a.hoff[vi] + X] = pv;
         t[i] = val;
     }
     __syncthreads();
@@ -1999,6 +2020,7 @@ int score_wide_layer(ulg_ctx *c, int L, int ph, hipStream_t st, const uint64_t *
     wa.queue = queue;
     wa.qcount = qc;
     wa.hmax = nullptr;
+    wa.pval = nullptr;
     wa.hoff = nullptr;
     wa.N = (double)c->N;
     wa.lambda = c->lambda;
@@ -2047,7 +2069,7 @@ int score_wide_layer(ulg_ctx *c, int L, int ph, hipStream_t st, const uint64_t *
             }
             ULG_HIP(c, hipMemcpyAsync(d_hmeta, hm.data(), hm.size() * 4, hipMemcpyHostToDevice, st));
             HiArgs ha{d_hmeta, d_hmeta + nl, nl, c->d_meta.p, c->d_tbl_off.p, c->table.p, c->d_binom64.p,
-                      c->d_hmax.p, c->d_hoff.p, S, L, kmax, 0};
+                      c->d_hmax.p, c->d_hmax.p + c->hmax_half, c->d_hoff.p, S, L, kmax, 0};
             prof_begin_s(c, "wide_hicover", st);
             if (ph == 0) hikey_tile_kernel<0><<<tp[nl], 1024, 0, st>>>(ha);
             else hikey_tile_kernel<1><<<tp[nl], 1024, 0, st>>>(ha);
@@ -2061,6 +2083,7 @@ int score_wide_layer(ulg_ctx *c, int L, int ph, hipStream_t st, const uint64_t *
             ULG_HIP(c, hipGetLastError());
             ULG_HIP(c, hipStreamSynchronize(st));  // hm must outlive its copy
             wa.hmax = c->d_hmax.p;
+            wa.pval = c->d_hmax.p + c->hmax_half;
             wa.hoff = c->d_hoff.p;
         }
     }
@@ -2302,7 +2325,8 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
                     htot += 1ull << mv[i];
                 }
             if (htot > 0) {
-                if ((rc = ensure(c, c->d_hmax, (size_t)htot)) || (rc = upload(c, c->d_hoff, c->mir_hoff, hoff)) ||
+                c->hmax_half = htot;  // d_hmax = [hi-cover maxima][present values]
+                if ((rc = ensure(c, c->d_hmax, (size_t)(2 * htot))) || (rc = upload(c, c->d_hoff, c->mir_hoff, hoff)) ||
                     (rc = ensure(c, c->d_hmeta, (size_t)G * (nv + (size_t)(nv + 1) * 8))))
                     return rc;
             } else {

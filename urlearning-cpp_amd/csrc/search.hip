@@ -55,8 +55,9 @@ __global__ void __launch_bounds__(kB) support_kernel(const uint64_t *sets, const
 
 __global__ void __launch_bounds__(kB) scatter_kernel(const uint64_t *sets, const float *costs, const int64_t *offsets,
                                                      int n, const uint64_t *support, const uint64_t *tb_off,
-                                                     uint32_t *table) {
+                                                     uint32_t *table, uint64_t tvars) {
     const int v = blockIdx.y;
+    if (!((tvars >> v) & 1ull)) return;  // no table for v (sharded tables)
     const int64_t b = offsets[v], e = offsets[v + 1];
     const uint64_t D = support[v];
     for (int64_t i = b + (int64_t)blockIdx.x * kB + threadIdx.x; i < e; i += (int64_t)gridDim.x * kB) {
@@ -169,12 +170,13 @@ __device__ __forceinline__ void min4(uint32_t (&r)[16]) {
 // one (global table index, packed key) per stored set inside the tables' scope
 __global__ void __launch_bounds__(kB) entries_kernel(const uint64_t *sets, const float *costs, const int64_t *offsets,
                                                      int n, const uint64_t *support, const uint64_t *tb_off,
-                                                     uint64_t *idx, uint32_t *key) {
+                                                     uint64_t *idx, uint32_t *key, uint64_t tvars) {
     const int v = blockIdx.y;
     const int64_t b = offsets[v], e = offsets[v + 1];
     const uint64_t D = support[v];
+    const bool own = (tvars >> v) & 1ull;
     for (int64_t i = b + (int64_t)blockIdx.x * kB + threadIdx.x; i < e; i += (int64_t)gridDim.x * kB) {
-        if (sets[i] & ~D) {
+        if (!own || (sets[i] & ~D)) {
             idx[i] = ~0ull;  // outside the scope: sorts past every slot
             key[i] = 0xFFFFFFFFu;
             continue;
@@ -396,9 +398,10 @@ __global__ void __launch_bounds__(kB) pdb_query_kernel(SearchDev d, int64_t coun
 
 namespace ulg {
 
-int search_build_tables(ulg_ctx *c, uint64_t scope) {
+int search_build_tables(ulg_ctx *c, uint64_t scope, uint64_t tvars) {
     SearchState &s = *c->search;
     const int n = s.n;
+    tvars &= (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
     int rc;
     // support D_v
     if ((rc = ensure(c, s.d_support, (size_t)n))) return rc;
@@ -415,12 +418,15 @@ int search_build_tables(ulg_ctx *c, uint64_t scope) {
     ULG_HIP(c, hipStreamSynchronize(c->stream));
     // memory check before touching the current tables: 4 B ordered cost + 4 B
     // device float cost + 4 B pinned host cost per entry
+    // variables outside tvars get no table (0 entries; their lookups scan the lists)
     uint64_t total = 0;
     for (int v = 0; v < n; ++v) {
         const int m = __builtin_popcountll(support[v]);
+        if (!((tvars >> v) & 1ull)) continue;
         if (m > 40) return set_err(c, ULG_ERR_UNSUPPORTED, "best-score table over more than 40 candidate parents");
         total += 1ull << m;
     }
+    if (total == 0) return set_err(c, ULG_ERR_ARG, "best-score tables for no variable");
     uint64_t budget = c->table_budget_kb << 10;
     if (budget == 0) {
         size_t free_b = 0, tot_b = 0;
@@ -440,16 +446,20 @@ int search_build_tables(ulg_ctx *c, uint64_t scope) {
     s.mbits.assign(n, 0);
     s.tb_off.assign(n + 1, 0);
     for (int v = 0; v < n; ++v) {
-        s.mbits[v] = __builtin_popcountll(s.support[v]);
-        s.tb_off[v + 1] = s.tb_off[v] + (1ull << s.mbits[v]);
+        const bool own = (tvars >> v) & 1ull;
+        s.mbits[v] = own ? __builtin_popcountll(s.support[v]) : 0;
+        s.tb_off[v + 1] = s.tb_off[v] + (own ? (1ull << s.mbits[v]) : 0ull);
     }
+    s.table_vars = tvars;
     s.table_entries = total;
     if ((rc = ensure(c, s.d_table, total)) || (rc = ensure(c, s.d_tb_off, (size_t)n + 1)) ||
         (rc = ensure(c, s.d_mbits, (size_t)n)))
         return rc;
     ULG_HIP(c, hipMemcpyAsync(s.d_tb_off.p, s.tb_off.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, c->stream));
     ULG_HIP(c, hipMemcpyAsync(s.d_mbits.p, s.mbits.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
-    const int minm = *std::min_element(s.mbits.begin(), s.mbits.end());
+    int minm = 64;
+    for (int v = 0; v < n; ++v)
+        if ((tvars >> v) & 1ull) minm = std::min(minm, s.mbits[v]);
     std::vector<int> tiles_prefix(n + 1, 0), blocks_prefix(n + 1, 0);
     if ((rc = ensure(c, s.d_prefix, (size_t)2 * (n + 1)))) return rc;
     if (minm >= kRegTileBits) {
@@ -461,7 +471,7 @@ int search_build_tables(ulg_ctx *c, uint64_t scope) {
             return rc;
         prof_begin(c, "bs_entries");
         entries_kernel<<<dim3(gx, n), kB, 0, c->stream>>>(s.d_sets.p, s.d_costs.p, s.d_offsets.p, n, s.d_support.p,
-                                                         s.d_tb_off.p, s.e_idx.p, s.e_key.p);
+                                                         s.d_tb_off.p, s.e_idx.p, s.e_key.p, tvars);
         prof_end(c);
         int end_bit = 1;
         while (end_bit < 64 && (1ull << (end_bit - 1)) <= total) ++end_bit;  // ~0 sorts past every slot
@@ -486,12 +496,12 @@ int search_build_tables(ulg_ctx *c, uint64_t scope) {
     prof_end(c);
     prof_begin(c, "bs_scatter");
     scatter_kernel<<<dim3(gx, n), kB, 0, c->stream>>>(s.d_sets.p, s.d_costs.p, s.d_offsets.p, n, s.d_support.p,
-                                                     s.d_tb_off.p, s.d_table.p);
+                                                     s.d_tb_off.p, s.d_table.p, tvars);
     prof_end(c);
     // pass A tiles
     for (int v = 0; v < n; ++v) {
         const int m = s.mbits[v];
-        tiles_prefix[v + 1] = tiles_prefix[v] + (m <= kTileBits ? 1 : (1 << (m - kTileBits)));
+        tiles_prefix[v + 1] = tiles_prefix[v] + (!((tvars >> v) & 1ull) ? 0 : m <= kTileBits ? 1 : (1 << (m - kTileBits)));
     }
     ULG_HIP(c, hipMemcpyAsync(s.d_prefix.p, tiles_prefix.data(), (size_t)(n + 1) * 4, hipMemcpyHostToDevice, c->stream));
     const int maxm0 = *std::max_element(s.mbits.begin(), s.mbits.end());
@@ -542,8 +552,9 @@ int search_build_tables(ulg_ctx *c, uint64_t scope) {
 
 int search_ensure_scope(ulg_ctx *c, uint64_t need) {
     SearchState &s = *c->search;
-    if (s.tables_ready && (need & ~s.scope) == 0) return ULG_OK;
-    return search_build_tables(c, need);
+    const uint64_t all = (s.n >= 64) ? ~0ull : ((1ull << s.n) - 1ull);
+    if (s.tables_ready && (need & ~s.scope) == 0 && s.table_vars == all) return ULG_OK;
+    return search_build_tables(c, need, all);
 }
 
 int search_build_pdb(ulg_ctx *c, int pd_count, uint64_t ancestors, uint64_t scc) {

@@ -178,7 +178,8 @@ __global__ void __launch_bounds__(kB) layer_pull_kernel(LayerArgs a) {
 // dispatched j-major, so the running blocks read one variable's lattice
 // (64 MB at C3) at a time.
 __global__ void __launch_bounds__(kB) sweep_w_kernel(SearchDev d, const uint64_t *gbinom, const uint64_t *loffm1,
-                                                     const int *comp_vars, int m, uint64_t half, float *w) {
+                                                     const int *comp_vars, int m, uint64_t half, float *w,
+                                                     const int *jlist) {
     __shared__ uint64_t binom[33 * 33];
     __shared__ uint64_t lo[kMaxM + 1];
     __shared__ int cv[kMaxM];
@@ -187,7 +188,7 @@ __global__ void __launch_bounds__(kB) sweep_w_kernel(SearchDev d, const uint64_t
     for (int i = threadIdx.x; i < m; i += kB) cv[i] = comp_vars[i];
     __syncthreads();
     const uint64_t f = (uint64_t)blockIdx.x * kB + threadIdx.x;
-    const int j = blockIdx.y;
+    const int j = jlist ? jlist[blockIdx.y] : (int)blockIdx.y;  // slice blockIdx.y holds position j
     if (f >= half) return;
     int p = 0;
     while (p + 1 < m && lo[p + 1] <= f) ++p;
@@ -202,7 +203,101 @@ __global__ void __launch_bounds__(kB) sweep_w_kernel(SearchDev d, const uint64_t
     const uint64_t Pc = ((x >> j) << (j + 1)) | (x & ((1ull << j) - 1ull));
     uint64_t Pg = 0;
     for (uint64_t y = Pc; y; y &= y - 1) Pg |= 1ull << cv[__builtin_ctzll(y)];
-    w[(uint64_t)j * half + f] = bs_cost(d, cv[j], Pg);
+    w[(uint64_t)blockIdx.y * half + f] = bs_cost(d, cv[j], Pg);
+}
+
+// ---- sweep with the tables sharded by variable (n >= 31) --------------
+// Rank r holds the best-score tables (and sweep slices) of its own variables
+// only.  Per layer every rank computes, for every node T, the best candidate
+// over the leaves it owns as the key (ordkey(cost) << 8 | leaf position), the
+// caller MIN-all-reduces the keys over the ranks (the smallest cost, then the
+// smallest leaf position: the single-GPU sweep's first-strict-minimum rule),
+// and commit turns the reduced keys into the layer's g and leaf bytes.
+constexpr uint64_t kUnreachedKey = 0xFFFFFFFFFFull;  // above every (ordkey << 8 | j)
+
+struct ShardArgs {
+    const uint64_t *binom;  // [33][33]
+    const int *wslot;       // [m]: slice of compact position j, -1 if not owned
+    int m, layer;
+    uint64_t count;
+    const float *gprev;
+    const float *w;
+    uint64_t w_half, w_layer;
+    uint64_t *keys;
+};
+
+__global__ void __launch_bounds__(kB) layer_shard_kernel(ShardArgs a) {
+    __shared__ uint64_t binom[33 * 33];
+    __shared__ int ws[kMaxM];
+    {
+        const int cols = a.layer + 1;
+        for (int e = threadIdx.x; e < a.m * cols; e += kB) {
+            const int r = e / cols, i = e - r * cols;
+            binom[r * 33 + i] = a.binom[r * 33 + i];
+        }
+    }
+    for (int i = threadIdx.x; i < a.m; i += kB) ws[i] = a.wslot[i];
+    __syncthreads();
+    const uint64_t r = (uint64_t)blockIdx.x * kB + threadIdx.x;
+    const int L = a.layer;
+    if (r >= a.count) return;
+    uint64_t Tc = 0;
+    {
+        uint64_t rr = r;
+        int c = a.m - 1;
+        for (int i = L; i >= 1; --i) {
+            while (Bn(binom, c, i) > rr) --c;
+            Tc |= 1ull << c;
+            rr -= Bn(binom, c, i);
+            --c;
+        }
+    }
+    uint64_t suffix = 0, suffixc = 0;
+    {
+        int i = 0;
+        for (uint64_t x = Tc; x; x &= x - 1, ++i)
+            if (i >= 1) {
+                const int ai = __builtin_ctzll(x);
+                suffix += Bn(binom, ai, i);
+                suffixc += Bn(binom, ai - 1, i);
+            }
+    }
+    uint64_t prefix = 0, best = kUnreachedKey;
+    uint64_t x = Tc;
+    for (int j = 0; j < L; ++j) {
+        const int aj = __builtin_ctzll(x);
+        x &= x - 1;
+        const int sl = ws[aj];
+        if (sl >= 0) {
+            const float gp = a.gprev[prefix + suffix];
+            if (gp < FLT_MAX) {
+                const float cand = gp + a.w[(uint64_t)sl * a.w_half + a.w_layer + prefix + suffixc];
+                const uint64_t k = ((uint64_t)ordkey(cand) << 8) | (uint64_t)j;
+                best = k < best ? k : best;
+            }
+        }
+        if (x) {
+            const int an = __builtin_ctzll(x);
+            suffix -= Bn(binom, an, j + 1);
+            suffixc -= Bn(binom, an - 1, j + 1);
+        }
+        prefix += Bn(binom, aj, j + 1);
+    }
+    a.keys[r] = best;
+}
+
+__global__ void __launch_bounds__(kB) shard_commit_kernel(const uint64_t *keys, uint64_t count, float *g, uint8_t *leaf,
+                                                          unsigned long long *reached) {
+    const uint64_t r = (uint64_t)blockIdx.x * kB + threadIdx.x;
+    bool hit = false;
+    if (r < count) {
+        const uint64_t k = keys[r];
+        hit = k != kUnreachedKey;
+        g[r] = hit ? ord_cost((uint32_t)(k >> 8)) : FLT_MAX;
+        leaf[r] = hit ? (uint8_t)(k & 0xffull) : (uint8_t)255;
+    }
+    const unsigned long long b = __ballot(hit);
+    if (reached && (threadIdx.x & 63) == 0 && b) atomicAdd(&reached[blockIdx.x % kCounters], (unsigned long long)__popcll(b));
 }
 
 // walk the leaf pointers from the goal back to the root (one thread)
@@ -354,7 +449,7 @@ int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, flo
                 if (e == hipSuccess) {
                     prof_begin(c, "search_sweep_w");
                     sweep_w_kernel<<<dim3((unsigned)((half + kB - 1) / kB), (unsigned)m), kB, 0, c->stream>>>(
-                        dv, d_bn.p, d_lo.p, d_cv.p, m, half, s.d_sweep_w.p);
+                        dv, d_bn.p, d_lo.p, d_cv.p, m, half, s.d_sweep_w.p, nullptr);
                     prof_end(c);
                     e = hipGetLastError();
                 }
@@ -417,4 +512,193 @@ int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, flo
     return ULG_OK;
 }
 
+// ---- variable-sharded sweep -------------------------------------------------
+namespace {
+std::vector<uint64_t> layer_offsets(int m) {
+    std::vector<uint64_t> loff(m + 2, 0);
+    for (int d = 0; d <= m; ++d) loff[d + 1] = loff[d] + binom64(m, d);
+    return loff;
+}
+}  // namespace
+
+int sweep_shard_begin(ulg_ctx *c, uint64_t own, int64_t *max_nodes) {
+    SearchState &s = *c->search;
+    const int n = s.n;
+    const uint64_t all = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+    if (n < 2 || n > kMaxM) return set_err(c, ULG_ERR_UNSUPPORTED, "ulg_sweep_shard_begin: 2..32 variables");
+    if (own == 0 || (own & ~all)) return set_err(c, ULG_ERR_ARG, "ulg_sweep_shard_begin: bad variable mask");
+    s.shard_active = false;
+    // this rank's tables (every stored set of its variables, over every variable)
+    int rc = search_build_tables(c, all, own);
+    if (rc) return rc;
+    s.sweep_ready = false;  // d_sweep_w now holds this rank's slices
+    const int m = n;
+    const uint64_t half = 1ull << (m - 1);
+    std::vector<int> wslot(m, -1), jlist;
+    for (int v = 0; v < m; ++v)
+        if ((own >> v) & 1ull) {
+            wslot[v] = (int)jlist.size();
+            jlist.push_back(v);
+        }
+    const int nown = (int)jlist.size();
+    std::vector<uint64_t> bn(33 * 33, 0);
+    for (int a = 0; a <= 32; ++a)
+        for (int b = 0; b <= 32; ++b) bn[a * 33 + b] = binom64(a, b);
+    const std::vector<uint64_t> loff = layer_offsets(m);
+    std::vector<uint64_t> loffm1(kMaxM + 1, 0);
+    for (int p = 0; p < m; ++p) loffm1[p + 1] = loffm1[p] + binom64(m - 1, p);
+    uint64_t maxl = 1;
+    for (int d = 0; d <= m; ++d) maxl = std::max<uint64_t>(maxl, binom64(m, d));
+    std::vector<int> cv(m);
+    for (int v = 0; v < m; ++v) cv[v] = v;
+    DevBuf<uint64_t> d_lo;
+    DevBuf<int> d_jl;
+    if ((rc = ensure(c, s.d_sweep_w, (size_t)((uint64_t)nown * half))) || (rc = ensure(c, d_lo, kMaxM + 1)) ||
+        (rc = ensure(c, d_jl, (size_t)nown)) || (rc = ensure(c, s.shard_bn, bn.size())) ||
+        (rc = ensure(c, s.shard_loff, loff.size())) || (rc = ensure(c, s.shard_wslot, (size_t)m)) ||
+        (rc = ensure(c, s.shard_cv, (size_t)m)) || (rc = ensure(c, s.shard_chain, kMaxM)) ||
+        (rc = ensure(c, s.shard_g0, (size_t)maxl)) || (rc = ensure(c, s.shard_g1, (size_t)maxl)) ||
+        (rc = ensure(c, s.shard_leaf, (size_t)loff[m + 1])) || (rc = ensure(c, s.shard_acc, kCounters))) {
+        release(d_lo);
+        release(d_jl);
+        return rc;
+    }
+    hipError_t e = hipMemcpyAsync(d_lo.p, loffm1.data(), (kMaxM + 1) * 8, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_jl.p, jlist.data(), (size_t)nown * 4, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.shard_bn.p, bn.data(), bn.size() * 8, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.shard_loff.p, loff.data(), loff.size() * 8, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.shard_wslot.p, wslot.data(), (size_t)m * 4, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.shard_cv.p, cv.data(), (size_t)m * 4, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(s.shard_acc.p, 0, kCounters * 8, c->stream);
+    const float zero = 0.0f;  // root: g = 0 (astar_main.cpp:236)
+    if (e == hipSuccess) e = hipMemcpyAsync(s.shard_g0.p, &zero, 4, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) {
+        prof_begin(c, "search_sweep_w");
+        sweep_w_kernel<<<dim3((unsigned)((half + kB - 1) / kB), (unsigned)nown), kB, 0, c->stream>>>(
+            s.dev(), s.shard_bn.p, d_lo.p, s.shard_cv.p, m, half, s.d_sweep_w.p, d_jl.p);
+        prof_end(c);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    release(d_lo);
+    release(d_jl);
+    if (e != hipSuccess) return set_err(c, ULG_ERR_HIP, hipGetErrorString(e));
+    prof_collect(c);
+    s.shard_own = own;
+    s.shard_layer = 0;
+    s.shard_active = true;
+    *max_nodes = (int64_t)maxl;
+    return ULG_OK;
+}
+
+int sweep_shard_layer(ulg_ctx *c, int layer, uint64_t *keys) {
+    SearchState &s = *c->search;
+    const int m = s.n;
+    if (!s.shard_active || layer != s.shard_layer + 1 || layer > m)
+        return set_err(c, ULG_ERR_STATE, "ulg_sweep_shard_layer: layers go 1..n, each after the previous commit");
+    const uint64_t cnt = binom64(m, layer);
+    const float *gprev = (layer & 1) ? s.shard_g0.p : s.shard_g1.p;  // layer d's g lives in g[d & 1]
+    uint64_t wl = 0;
+    for (int p = 0; p < layer - 1; ++p) wl += binom64(m - 1, p);
+    ShardArgs a{s.shard_bn.p, s.shard_wslot.p, m, layer, cnt, gprev, s.d_sweep_w.p, 1ull << (m - 1), wl, keys};
+    prof_begin(c, "search_shard_layer");
+    layer_shard_kernel<<<(unsigned)((cnt + kB - 1) / kB), kB, 0, c->stream>>>(a);
+    prof_end(c);
+    ULG_HIP(c, hipGetLastError());
+    ULG_HIP(c, hipStreamSynchronize(c->stream));  // the caller's collective reads the keys next
+    prof_collect(c);
+    return ULG_OK;
+}
+
+int sweep_shard_commit(ulg_ctx *c, int layer, const uint64_t *keys) {
+    SearchState &s = *c->search;
+    const int m = s.n;
+    if (!s.shard_active || layer != s.shard_layer + 1 || layer > m)
+        return set_err(c, ULG_ERR_STATE, "ulg_sweep_shard_commit: commit the layer just computed");
+    const uint64_t cnt = binom64(m, layer);
+    float *gcur = (layer & 1) ? s.shard_g1.p : s.shard_g0.p;
+    const std::vector<uint64_t> loff = layer_offsets(m);
+    prof_begin(c, "search_shard_commit");
+    shard_commit_kernel<<<(unsigned)((cnt + kB - 1) / kB), kB, 0, c->stream>>>(
+        keys, cnt, gcur, s.shard_leaf.p + loff[layer], layer < m ? s.shard_acc.p : nullptr);
+    prof_end(c);
+    ULG_HIP(c, hipGetLastError());
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    s.shard_layer = layer;
+    return ULG_OK;
+}
+
+int sweep_shard_end(ulg_ctx *c, uint64_t *vpar, int *order, float *goal_cost, int64_t *expanded) {
+    SearchState &s = *c->search;
+    const int n = s.n, m = n;
+    if (!s.shard_active || s.shard_layer != m) return set_err(c, ULG_ERR_STATE, "ulg_sweep_shard_end: layers not done");
+    reconstruct_kernel<<<1, 1, 0, c->stream>>>(s.shard_leaf.p, s.shard_loff.p, s.shard_bn.p, m, s.shard_chain.p);
+    ULG_HIP(c, hipGetLastError());
+    float g = 0.0f;
+    std::vector<int> chain(m);
+    std::vector<unsigned long long> acc(kCounters, 0);
+    const float *ggoal = (m & 1) ? s.shard_g1.p : s.shard_g0.p;
+    ULG_HIP(c, hipMemcpyAsync(&g, ggoal, 4, hipMemcpyDeviceToHost, c->stream));
+    ULG_HIP(c, hipMemcpyAsync(chain.data(), s.shard_chain.p, (size_t)m * 4, hipMemcpyDeviceToHost, c->stream));
+    ULG_HIP(c, hipMemcpyAsync(acc.data(), s.shard_acc.p, kCounters * 8, hipMemcpyDeviceToHost, c->stream));
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    s.shard_active = false;
+    if (!(g < FLT_MAX) || std::find(chain.begin(), chain.end(), -1) != chain.end())
+        return set_err(c, ULG_ERR_STATE, "ulg_sweep_shard_end: no goal");
+    std::vector<int> total(n, 0), qv(m);
+    std::vector<uint64_t> qs(m), qp(m);
+    std::vector<float> qc(m);
+    uint64_t remaining = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+    for (int i = m - 1; i >= 0; --i) {
+        const int leaf = chain[i];
+        total[i] = leaf;
+        qv[i] = leaf;
+        qs[i] = remaining;
+        remaining &= ~(1ull << leaf);
+    }
+    int rc = search_query(c, m, qv.data(), qs.data(), qc.data(), qp.data());
+    if (rc) return rc;
+    for (int v = 0; v < n; ++v) vpar[v] = 0;
+    for (int i = 0; i < m; ++i) vpar[total[i]] = qp[i];
+    for (int v = 0; v < n; ++v) order[v] = total[v];
+    *goal_cost = g;
+    int64_t reached = 1;  // the root
+    for (unsigned long long x : acc) reached += (int64_t)x;
+    *expanded = reached;
+    return ULG_OK;
+}
+
 }  // namespace ulg
+
+extern "C" {
+
+int ulg_sweep_shard_begin(ulg_ctx *c, uint64_t own, int64_t *max_layer_nodes) {
+    if (!c || !max_layer_nodes) return ULG_ERR_ARG;
+    if (!c->search || !c->search->lists_ready) return set_err(c, ULG_ERR_STATE, "ulg_sweep_shard_begin: no parent-set lists");
+    ULG_HIP(c, hipSetDevice(c->device));
+    return ulg::sweep_shard_begin(c, own, max_layer_nodes);
+}
+
+int ulg_sweep_shard_layer(ulg_ctx *c, int layer, uint64_t *keys_dev) {
+    if (!c || !keys_dev) return ULG_ERR_ARG;
+    if (!c->search) return set_err(c, ULG_ERR_STATE, "ulg_sweep_shard_layer: no search state");
+    ULG_HIP(c, hipSetDevice(c->device));
+    return ulg::sweep_shard_layer(c, layer, keys_dev);
+}
+
+int ulg_sweep_shard_commit(ulg_ctx *c, int layer, const uint64_t *keys_dev) {
+    if (!c || !keys_dev) return ULG_ERR_ARG;
+    if (!c->search) return set_err(c, ULG_ERR_STATE, "ulg_sweep_shard_commit: no search state");
+    ULG_HIP(c, hipSetDevice(c->device));
+    return ulg::sweep_shard_commit(c, layer, keys_dev);
+}
+
+int ulg_sweep_shard_end(ulg_ctx *c, uint64_t *vpar, int *order, float *goal_cost, int64_t *expanded) {
+    if (!c || !vpar || !order || !goal_cost || !expanded) return ULG_ERR_ARG;
+    if (!c->search) return set_err(c, ULG_ERR_STATE, "ulg_sweep_shard_end: no search state");
+    ULG_HIP(c, hipSetDevice(c->device));
+    return ulg::sweep_shard_end(c, vpar, order, goal_cost, expanded);
+}
+
+}  // extern "C"

@@ -116,6 +116,7 @@ struct SearchDev {
     const float *pd;         // pattern databases
     const uint64_t *gmeta;   // groups[kMaxGroups], pd_off[kMaxGroups]
     uint64_t scope;          // the tables hold every stored set inside scope
+    uint64_t table_vars;     // variables that have a table (all but in the sharded sweep)
     int tables;              // 1 if the tables are built (for scope)
     int pd_count;
     int n;
@@ -151,11 +152,12 @@ __device__ inline uint64_t bs_index(const SearchDev &d, int v, uint64_t S) {
     return D == (all & ~(1ull << v)) ? (((v < 63 ? (x >> (v + 1)) : 0ull) << v) | (x & lo)) : pext_sparse(x, D);
 }
 
-// getScore(v, S): one 4-B read of the lattice when S lies inside the tables'
-// scope (every stored set that can be a subset of S is in the table), else
-// the list scan.
+// getScore(v, S): one 4-B read of the lattice when v has a table and S lies
+// inside the tables' scope (every stored set that can be a subset of S is in
+// the table), else the list scan.
 __device__ inline float bs_cost(const SearchDev &d, int v, uint64_t S) {
-    if (d.tables && (S & ~d.scope) == 0) return ord_cost(d.table[d.tb_off[v] + bs_index(d, v, S)]);
+    if (d.tables && (S & ~d.scope) == 0 && ((d.table_vars >> v) & 1ull))
+        return ord_cost(d.table[d.tb_off[v] + bs_index(d, v, S)]);
     return key_cost(bs_key_scan(d, v, S));
 }
 
@@ -213,6 +215,7 @@ struct SearchState {
     bool lists_ready = false;   // the per-variable lists are on the device
     bool tables_ready = false;  // the lattice tables are built for `scope`
     uint64_t scope = 0;         // tables cover every stored set inside scope
+    uint64_t table_vars = 0;    // variables with a table (every variable, except for ulg_sweep_shard_*)
     // host copy of the per-subset best costs (exact-order search)
     DevBuf<float> d_cost_table;
     float *host_costs = nullptr;
@@ -231,6 +234,17 @@ struct SearchState {
     DevBuf<float> d_sweep_w;
     uint64_t sweep_comp = 0;
     bool sweep_ready = false;
+    // variable-sharded sweep (ulg_sweep_shard_*): this rank's tables and
+    // sweep slices cover `shard_own`; the layers' g and leaf bytes are the
+    // all-reduced ones
+    bool shard_active = false;
+    uint64_t shard_own = 0;
+    int shard_layer = 0;
+    DevBuf<float> shard_g0, shard_g1;
+    DevBuf<uint8_t> shard_leaf;
+    DevBuf<uint64_t> shard_bn, shard_loff;
+    DevBuf<int> shard_wslot, shard_cv, shard_chain;
+    DevBuf<unsigned long long> shard_acc;
     // pattern database
     int pd_count = 0;
     uint64_t ancestors = 0, scc = 0;
@@ -259,6 +273,7 @@ struct SearchState {
         d.offsets = d_offsets.p;
         d.costs = d_costs.p;
         d.scope = scope;
+        d.table_vars = table_vars;
         d.tables = tables_ready ? 1 : 0;
         d.pd = d_pd.p;
         d.gmeta = d_groups.p;
@@ -277,6 +292,9 @@ struct SearchState {
         release(d_rows); release(d_rowmeta);
         release(d_sweep_w);
         sweep_ready = false;
+        release(shard_g0); release(shard_g1); release(shard_leaf); release(shard_bn); release(shard_loff);
+        release(shard_wslot); release(shard_cv); release(shard_chain); release(shard_acc);
+        shard_active = false;
         host_rows.release();
         rows_ready = false;
         host_cost_cap = 0;
@@ -285,7 +303,7 @@ struct SearchState {
 
 // Builds the lattice tables over the stored sets inside `scope`; returns
 // ULG_ERR_UNSUPPORTED (tables untouched) if they would exceed the budget.
-int search_build_tables(ulg_ctx *c, uint64_t scope);
+int search_build_tables(ulg_ctx *c, uint64_t scope, uint64_t tvars = ~0ull);
 // Tables covering `need` (rebuilt for exactly `need` if the current ones do not).
 int search_ensure_scope(ulg_ctx *c, uint64_t need);
 int search_build_pdb(ulg_ctx *c, int pd_count, uint64_t ancestors, uint64_t scc);

@@ -359,7 +359,7 @@ void set_parallel(Triplet &t) {
     const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
     t.threads = e ? std::max(1, std::atoi(e)) : std::min(8, hw);
     const uint64_t all = (t.n >= 64) ? ~0ull : ((1ull << t.n) - 1ull);
-    t.parallel_ok = t.threads > 1 && t.s->tables_ready && (t.s->scope & all) == all &&
+    t.parallel_ok = t.threads > 1 && t.s->tables_ready && (t.s->scope & all) == all && t.s->table_vars == all &&
                     search_cost_table_host(t.c) == ULG_OK;
 }
 

@@ -110,7 +110,8 @@ struct ulg_ctx {
     bool prof_skip = false;
     std::vector<hipEvent_t> event_pool;
     ulg::Mirror mir_tbl_off, mir_work, mir_cand, mir_meta, mir_workg, mir_hoff;
-    ulg::DevBuf<float> d_hmax;      // wide walks: hi-cover tables (subset max of the present keys)
+    ulg::DevBuf<float> d_hmax;      // wide walks: hi-cover tables (subset max of the present keys), then the present keys
+    uint64_t hmax_half = 0;         // entries of each half of d_hmax
     ulg::DevBuf<uint64_t> d_hoff;   // [nv] table offsets, ~0 = no table
     ulg::DevBuf<int> d_hmeta;       // per stream group: launch variables and tile / block prefixes
     std::map<std::string, std::vector<double>> prof_ms;

@@ -62,6 +62,53 @@ def assign(n: int, world_size: int, candidates, k: int):
     return [sorted(p) for p in parts]
 
 
+def table_owners(n: int, world_size: int, candidates=None):
+    """Variables whose best-score tables and sweep slices each rank holds in
+    the variable-sharded sweep (n >= 31): longest-processing-time
+    on the table size 2^{m_v} (every variable's is 2^{n-1} on a full
+    skeleton, so this is a balanced stripe).  Returns one bit mask per rank."""
+    cands = candidates if candidates is not None else [(1 << n) - 1] * n
+    w = [1 << bin(int(cands[v]) & ~(1 << v) & ((1 << n) - 1)).count("1") for v in range(n)]
+    order = sorted(range(n), key=lambda v: (-w[v], v))
+    loads = [0] * world_size
+    masks = [0] * world_size
+    for v in order:
+        r = min(range(world_size), key=lambda q: (loads[q], q))
+        masks[r] |= 1 << v
+        loads[r] += w[v]
+    return masks
+
+
+def sharded_sweep(ctx, n: int, own: int, device="cuda", comm_device=None, keys=None):
+    """The GPU order-graph sweep with the tables sharded by variable
+    (ulg_sweep_shard_*): per layer this rank's best (cost, leaf) keys over the
+    leaves it owns, ONE MIN all-reduce of the layer's keys over the ranks
+    (RCCL over xGMI; gloo copies through the host), then the commit.  Every
+    rank returns the single-GPU ULG_ASTAR_GPU result.  `keys`: a reusable
+    int64 device buffer of at least the largest layer."""
+    comm_device = comm_device or device
+    maxl = ctx.sweep_shard_begin(own)
+    if keys is None or keys.numel() < maxl:
+        keys = torch.empty(maxl, dtype=torch.int64, device=device)
+    stage = torch.empty(maxl, dtype=torch.int64, device=comm_device) if comm_device != device else None
+    for L in range(1, n + 1):
+        cnt = comb(n, L)
+        view = keys[:cnt]
+        ctx.sweep_shard_layer(L, view.data_ptr())  # synchronised: the keys are complete
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            if stage is None:
+                dist.all_reduce(view, op=dist.ReduceOp.MIN)
+                torch.cuda.synchronize()
+            else:
+                st = stage[:cnt]
+                st.copy_(view)
+                dist.all_reduce(st, op=dist.ReduceOp.MIN)
+                view.copy_(st)
+                torch.cuda.synchronize()
+        ctx.sweep_shard_commit(L, view.data_ptr())
+    return ctx.sweep_shard_end()
+
+
 class ListExchange:
     """One all-gather of every rank's stored (set, score) lists.
 

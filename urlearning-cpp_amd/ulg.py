@@ -58,6 +58,10 @@ def lib():
         L.ulg_pss_format_lists.argtypes = [P, I, P, P, P, C.c_char_p, P, P, C.POINTER(C.c_void_p), C.POINTER(I64)]
         L.ulg_astar_scc.argtypes = [P, P, I, I, C.c_uint64, C.c_uint64, P, P, C.POINTER(F), C.POINTER(I64),
                                     C.c_char_p, I64]
+        L.ulg_sweep_shard_begin.argtypes = [P, C.c_uint64, C.POINTER(I64)]
+        L.ulg_sweep_shard_layer.argtypes = [P, I, P]
+        L.ulg_sweep_shard_commit.argtypes = [P, I, P]
+        L.ulg_sweep_shard_end.argtypes = [P, P, P, C.POINTER(F), C.POINTER(I64)]
         L.ulg_set_option.argtypes = [P, C.c_char_p, I64]
         L.ulg_get_info.argtypes = [P, C.c_char_p, C.POINTER(I64)]
         L.ulg_profile_enable.argtypes = [P, I]
@@ -241,6 +245,29 @@ class Context:
                                             len(buf) if buf is not None else 0), "ulg_astar_scc")
         return {"vpar": vpar, "order": order, "cost": cost.value, "expanded": exp.value,
                 "net_text": buf.value.decode() if buf is not None else None}
+
+    def sweep_shard_begin(self, own: int) -> int:
+        """This rank's tables and sweep slices for the variables in `own`
+        (ulg_sweep_shard_begin); returns the largest layer's node count."""
+        mx = C.c_int64()
+        self._check(lib().ulg_sweep_shard_begin(self._h, int(own), C.byref(mx)), "ulg_sweep_shard_begin")
+        return mx.value
+
+    def sweep_shard_layer(self, layer: int, keys_ptr: int):
+        self._check(lib().ulg_sweep_shard_layer(self._h, int(layer), C.c_void_p(keys_ptr)), "ulg_sweep_shard_layer")
+
+    def sweep_shard_commit(self, layer: int, keys_ptr: int):
+        self._check(lib().ulg_sweep_shard_commit(self._h, int(layer), C.c_void_p(keys_ptr)), "ulg_sweep_shard_commit")
+
+    def sweep_shard_end(self):
+        n = self.search_n
+        vpar = np.zeros(n, dtype=np.uint64)
+        order = np.zeros(n, dtype=np.int32)
+        cost = C.c_float()
+        exp = C.c_int64()
+        self._check(lib().ulg_sweep_shard_end(self._h, _ptr(vpar), _ptr(order), C.byref(cost), C.byref(exp)),
+                    "ulg_sweep_shard_end")
+        return {"vpar": vpar, "order": order, "cost": cost.value, "expanded": exp.value}
 
     def _names_arg(self, names):
         arr = (C.c_char_p * len(names))(*[x.encode() for x in names])
