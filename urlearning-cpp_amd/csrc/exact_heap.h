@@ -59,8 +59,8 @@ struct Heap {
     // CompareNodeStar: true if x has LOWER priority than y
     static inline bool cns(const HeapEnt &A, const HeapEnt &B) {
         const float diff = A.f - B.f;
-        if (std::fabs(diff) < FLT_EPSILON) return (B.layer - A.layer) > 0;
-        return diff > 0;
+        const bool tie = std::fabs(diff) < FLT_EPSILON;
+        return (tie & ((B.layer - A.layer) > 0)) | (!tie & (diff > 0));
     }
     inline void setpos(const HeapEnt &e, int64_t p) { (*nodes)[e.idx].pq = (int32_t)p; }
     void push_hole(int64_t hole, int64_t top, HeapEnt value) {
@@ -99,7 +99,7 @@ struct Heap {
                 __builtin_prefetch(&a[gc + 3]);
             }
             second = 2 * (second + 1);
-            if (cns(a[second], a[second - 1])) second--;
+            second -= (int64_t)cns(a[second], a[second - 1]);
             a[hole] = a[second];
             __builtin_prefetch(&(*nodes)[a[hole].idx], 1);
             mv_idx[nm] = a[hole].idx;
@@ -190,9 +190,14 @@ struct DenseRec {
 };
 static_assert(sizeof(DenseRec) == 16, "DenseRec is one quarter cache line");
 
+// slot (< 2^27) and layer (|S|, the comparator's depth) in one word, so a
+// comparison never touches the node record or counts bits
 struct DEnt {
     float f;
-    uint32_t slot;
+    uint32_t key;  // slot | layer << 27
+    static constexpr uint32_t kSlotMask = (1u << 27) - 1u;
+    inline uint32_t slot() const { return key & kSlotMask; }
+    inline uint32_t layer() const { return key >> 27; }
 };
 
 struct DenseHeap {
@@ -202,13 +207,19 @@ struct DenseHeap {
     bool hang = false;
     int64_t scans = 0;
 
+    // CompareNodeStar, evaluated without branches: the heap descent picks a
+    // child per level on it, and that choice is a coin flip for a predictor
     static inline bool cns(const DEnt &A, const DEnt &B) {
         const float diff = A.f - B.f;
-        if (std::fabs(diff) < FLT_EPSILON) return (__builtin_popcount(B.slot) - __builtin_popcount(A.slot)) > 0;
-        return diff > 0;
+        const bool tie = std::fabs(diff) < FLT_EPSILON;
+        const bool deeper = B.layer() > A.layer();
+        const bool worse = diff > 0.0f;
+        return (tie & deeper) | (!tie & worse);
     }
-    inline DEnt ent(uint32_t x) const { return DEnt{recs[x].g + recs[x].h, x}; }
-    inline void setpos(const DEnt &e, int64_t p) { recs[e.slot].pq = (int32_t)(p + 1); }
+    inline DEnt ent(uint32_t x) const {
+        return DEnt{recs[x].g + recs[x].h, x | ((uint32_t)__builtin_popcount(x) << 27)};
+    }
+    inline void setpos(const DEnt &e, int64_t p) { recs[e.slot()].pq = (int32_t)(p + 1); }
     void push_hole(int64_t hole, int64_t top, DEnt value) {
         int64_t parent = (hole - 1) / 2;
         while (hole > top && cns(a[parent], value)) {
@@ -242,17 +253,17 @@ struct DenseHeap {
                 __builtin_prefetch(&a[g4 + 15]);
             }
             second = 2 * (second + 1);
-            if (cns(a[second], a[second - 1])) second--;
+            second -= (int64_t)cns(a[second], a[second - 1]);
             a[hole] = a[second];
-            __builtin_prefetch(&recs[a[hole].slot], 1);
-            mv_slot[nm] = a[hole].slot;
+            __builtin_prefetch(&recs[a[hole].slot()], 1);
+            mv_slot[nm] = a[hole].slot();
             mv_pos[nm++] = hole;
             hole = second;
         }
         if ((n & 1) == 0 && second == (n - 2) / 2) {
             second = 2 * (second + 1);
             a[hole] = a[second - 1];
-            mv_slot[nm] = a[hole].slot;
+            mv_slot[nm] = a[hole].slot();
             mv_pos[nm++] = hole;
             hole = second - 1;
         }
@@ -260,7 +271,7 @@ struct DenseHeap {
         push_hole(hole, top, value);
     }
     uint32_t pop() {
-        const uint32_t ret = a[0].slot;
+        const uint32_t ret = a[0].slot();
         const int64_t last = len - 1;
         const DEnt value = a[last];
         a[last] = a[0];
@@ -276,14 +287,14 @@ struct DenseHeap {
             return;
         }
         DEnt value = a[pos];
-        if (value.slot == x && pos < len) {
+        if (value.slot() == x && pos < len) {
             value.f = fx;
             a[pos].f = fx;
         } else {
             ++scans;
             for (int64_t i = 0; i < len; ++i)
-                if (a[i].slot == x) a[i].f = fx;
-            value.f = recs[value.slot].g + recs[value.slot].h;
+                if (a[i].slot() == x) a[i].f = fx;
+            value.f = recs[value.slot()].g + recs[value.slot()].h;
         }
         const int64_t parent = (pos - 1) / 2;
         if (pos > 0 && cns(a[parent], value)) {

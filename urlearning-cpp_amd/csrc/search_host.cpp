@@ -223,6 +223,7 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
     DenseHeap open;
     open.recs = recs;
     open.a = static_cast<DEnt *>(heapmem.p) + 1;
+
     // slot bit of each variable, and its column in the row table
     uint32_t sbit[64] = {0};
     int col[64];

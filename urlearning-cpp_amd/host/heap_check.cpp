@@ -106,7 +106,7 @@ int main(int argc, char **argv) {
             }
             if (op % 97 == 0)
                 for (int64_t i = 0; i < h.len; ++i)
-                    if (nodes[h.a[i].idx].sub != d.a[i].slot || h.a[i].f != d.a[i].f) {
+                    if (nodes[h.a[i].idx].sub != d.a[i].slot() || h.a[i].f != d.a[i].f) {
                         std::printf("FAIL op %ld: heap slot %lld differs\n", op, (long long)i);
                         return 1;
                     }
