@@ -1428,7 +1428,8 @@ __global__ void __launch_bounds__(kBlock) score_wide_kernel(WideArgs a) {
 // (BIC_OLS.cpp:234 with best starting at 0 < -ts).
 template <int LMAX, int PHASE>
 __global__ void __launch_bounds__(64) walk_wide_kernel(WideArgs a, uint64_t qbase, uint64_t qn, uint64_t *bits,
-                                                       uint64_t wpl, unsigned long long *err) {
+                                                       uint64_t wpl, unsigned long long *err,
+                                                       unsigned long long *wstats) {
     const uint64_t lid = (uint64_t)blockIdx.x * 64 + threadIdx.x;
     const uint64_t qi = qbase + lid;
     if (qi >= qn) return;
@@ -1577,10 +1578,17 @@ __global__ void __launch_bounds__(64) walk_wide_kernel(WideArgs a, uint64_t qbas
         ++d;
     }
     a.table[slot] = dom ? absent_f() : -ts;
+    if (wstats) {  // ULG_WALK_STATS: walks, steps, max steps, walks over 2^20 steps
+        atomicAdd(&wstats[0], 1ull);
+        atomicAdd(&wstats[1], (unsigned long long)steps);
+        atomicMax(&wstats[2], (unsigned long long)steps);
+        if (steps > (1ull << 20)) atomicAdd(&wstats[3], 1ull);
+    }
 }
 
 using WideFn = void (*)(WideArgs);
-using WideWalkFn = void (*)(WideArgs, uint64_t, uint64_t, uint64_t *, uint64_t, unsigned long long *);
+using WideWalkFn = void (*)(WideArgs, uint64_t, uint64_t, uint64_t *, uint64_t, unsigned long long *,
+                           unsigned long long *);
 WideFn wide_fn(int L, int phase) {
     if (L <= 16) return phase == 0 ? score_wide_kernel<16, 0> : score_wide_kernel<16, 1>;
     return phase == 0 ? score_wide_kernel<kWideMax, 0> : score_wide_kernel<kWideMax, 1>;
@@ -2092,13 +2100,29 @@ int score_wide_layer(ulg_ctx *c, int L, int ph, hipStream_t st, const uint64_t *
     const uint64_t wpl = q <= 6 ? 1ull : (1ull << (q - 6));
     const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(qn, slice / wpl));  // slice >= wpl
     const WideWalkFn wf = wide_walk_fn(L, ph);
+    static const bool wstat = std::getenv("ULG_WALK_STATS") != nullptr;  // diagnostics: synchronises
+    unsigned long long *ws = nullptr;
+    if (wstat) {
+        int rc2;
+        if ((rc2 = ensure(c, c->d_stats, 16))) return rc2;
+        ws = c->d_stats.p;
+        ULG_HIP(c, hipMemsetAsync(ws, 0, 32, st));
+    }
     for (uint64_t base = 0; base < qn; base += per) {
         const uint64_t k = std::min<uint64_t>(per, qn - base);
         ULG_HIP(c, hipMemsetAsync(bits, 0, (size_t)(k * wpl * 8), st));
         prof_begin_s(c, ph == 0 ? "walk_wide_var0" : "walk_wide_rest", st);
-        hipLaunchKernelGGL(wf, dim3((unsigned)((k + 63) / 64)), dim3(64), 0, st, wa, base, base + k, bits, wpl, errf);
+        hipLaunchKernelGGL(wf, dim3((unsigned)((k + 63) / 64)), dim3(64), 0, st, wa, base, base + k, bits, wpl, errf,
+                           ws);
         prof_end_s(c, st);
         ULG_HIP(c, hipGetLastError());
+    }
+    if (wstat) {
+        unsigned long long h[4];
+        ULG_HIP(c, hipMemcpyAsync(h, ws, 32, hipMemcpyDeviceToHost, st));
+        ULG_HIP(c, hipStreamSynchronize(st));
+        std::fprintf(stderr, "walk_stats L=%d phase=%d queued=%llu walks=%llu steps=%llu max=%llu over2^20=%llu\n", L, ph,
+                     qn, h[0], h[1], h[2], h[3]);
     }
     return ULG_OK;
 }
