@@ -288,7 +288,8 @@ int ulg_sweep_shard_end(ulg_ctx *ctx, uint64_t *vpar, int *order, float *goal_co
  * component without a skeleton filter first lays the component's successor
  * costs out in its own (variable, layer, colex) order (m 2^(m-1) floats,
  * cached until the tables change) when that fits the free HBM; 0 reads the
- * binary-indexed lattice per predecessor instead.
+ * binary-indexed lattice per predecessor instead; 2 uses the slices with
+ * 64-bit index arithmetic (1 = 32-bit).
  * All variants compute identical results; the knob exists for A/B timing. */
 int ulg_set_option(ulg_ctx *ctx, const char *name, int64_t value);
 /* Read-back of per-call state: "out_of_time" (1 if the last ulg_cbic_score or

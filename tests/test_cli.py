@@ -64,6 +64,8 @@ def test_cli_end_to_end_matches_oracle_and_golden(tmp_path, oracle_built, fig, l
     pss, ref_pss = tmp_path / "gpu.pss", tmp_path / "ref.pss"
     r = _run([SCORE, csv, str(pss), "-f", "cBIC", "--lambda", lam, "-k", str(skel)])
     assert r.returncode == 0, r.stderr
+    m = _metrics(r.stderr)
+    assert m["tool"] == "score" and m["n"] == 4 and m["stored"] > 0 and m["scored"] == 4 * 8
     subprocess.run([o.REF_SCORE, csv, str(ref_pss), "-f", "cBIC", "--lambda", lam, "-k", str(skel)], check=True,
                    stdout=subprocess.DEVNULL)
     # the .pss text is the reference's format; same sets, same "%f" scores
@@ -72,12 +74,22 @@ def test_cli_end_to_end_matches_oracle_and_golden(tmp_path, oracle_built, fig, l
         net = tmp_path / f"net_{mode}"
         r = _run([ASTAR, str(pss), "-k", str(skel), "-n", str(net), "--mode", mode])
         assert r.returncode == 0, r.stderr
+        m = _metrics(r.stderr)
+        assert m["tool"] == "astar" and m["mode"] == mode and m["expanded"] > 0
         if mode == "exact":
             assert read_matrix(str(net) + ".csv") == fig_dag(fig)
             ref_net = tmp_path / "ref_net"
             subprocess.run([o.REF_ASTAR, str(pss), "-k", str(skel), "-n", str(ref_net)], check=True,
                            stdout=subprocess.DEVNULL)
             assert net.read_text() == ref_net.read_text()
+
+
+def _metrics(stderr):
+    """The command lines' one machine-readable line (stderr, 'ulg_metrics {json}')."""
+    import json
+    lines = [ln for ln in stderr.splitlines() if ln.startswith("ulg_metrics ")]
+    assert len(lines) == 1, stderr
+    return json.loads(lines[0][len("ulg_metrics "):])
 
 
 @pytest.mark.parametrize("bad", ["1,x", ",1", "1,", "a"])

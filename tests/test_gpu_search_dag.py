@@ -160,7 +160,7 @@ def test_sweep_table_gives_identical_search(ulg_ctx, case):
     try:
         ulg_ctx.search_from_scores()
         res = []
-        for on in (0, 1, 1):  # the second 1 reuses the cached slices
+        for on in (0, 1, 1, 2):  # the second 1 reuses the cached slices; 2 = 64-bit index arithmetic
             ulg_ctx.set_option("sweep_table", on)
             res.append(ulg_ctx.astar(edges=edges, mode=1, net_text=False))
     finally:

@@ -206,6 +206,38 @@ __global__ void __launch_bounds__(kB) sweep_w_kernel(SearchDev d, const uint64_t
     w[(uint64_t)blockIdx.y * half + f] = bs_cost(d, cv[j], Pg);
 }
 
+// The same slices when every v_j's lattice is exactly over comp \ {v_j}
+// (D_v = the rest of the component, the tables' scope covers it): then slice
+// entry (j, p, r) is lattice entry i of v_j with popcount(i) = p and colex
+// rank r, so each thread reads one lattice entry in order (coalesced) and
+// writes it to its slice; a wave's 64 consecutive i land in 7 contiguous
+// runs (one per popcount of their low 6 bits).
+constexpr int kScatterPer = 16;
+__global__ void __launch_bounds__(kB) sweep_w_scatter_kernel(const uint32_t *table, const uint64_t *tb_off,
+                                                             const uint64_t *gbinom, const uint64_t *loffm1,
+                                                             const int *comp_vars, const int *jlist, int m,
+                                                             uint64_t half, float *w) {
+    __shared__ uint32_t binom[33 * 33];
+    __shared__ uint32_t lo[kMaxM + 1];
+    for (int e = threadIdx.x; e < m * 33; e += kB) binom[e] = (uint32_t)gbinom[e];
+    for (int i = threadIdx.x; i <= m; i += kB) lo[i] = (uint32_t)loffm1[i];
+    __syncthreads();
+    const int j = jlist ? jlist[blockIdx.y] : (int)blockIdx.y;
+    const uint32_t *tv = table + tb_off[comp_vars[j]];
+    float *wj = w + (uint64_t)blockIdx.y * half;
+    // kScatterPer entries per thread, kB apart (each pass is one coalesced
+    // sweep of the block's range): the LDS preload is paid once per block
+    const uint64_t base = (uint64_t)blockIdx.x * kB * kScatterPer;
+    for (int k = 0; k < kScatterPer; ++k) {
+        const uint64_t i = base + (uint64_t)k * kB + threadIdx.x;
+        if (i >= half) return;
+        uint32_t rank = 0;
+        int t = 0;
+        for (uint64_t x = i; x; x &= x - 1) rank += binom[__builtin_ctzll(x) * 33 + (++t)];
+        wj[lo[t] + rank] = ord_cost(tv[i]);
+    }
+}
+
 // ---- sweep with the tables sharded by variable (n >= 31) --------------
 // Rank r holds the best-score tables (and sweep slices) of its own variables
 // only.  Per layer every rank computes, for every node T, the best candidate
@@ -300,6 +332,83 @@ __global__ void __launch_bounds__(kB) shard_commit_kernel(const uint64_t *keys, 
     if (reached && (threadIdx.x & 63) == 0 && b) atomicAdd(&reached[blockIdx.x % kCounters], (unsigned long long)__popcll(b));
 }
 
+// The sweep-slice launch in 32-bit index arithmetic: on a component of
+// m <= 32 variables every colex rank of a layer, C(m, L) <= C(32, 16) < 2^32,
+// and every slice offset below 2^(m-1) fit in 32 bits, so the unrank and the
+// per-leaf rank updates are single VALU ops (the 64-bit form spends ~1000 VALU
+// instructions per node, PMC pass profiles/r2/pmc_r2.json).  Same results as
+// layer_pull_kernel<true>.
+constexpr int kPullPer = 1;  // nodes per thread, kB apart (4 measured slower: 1.53 -> 2.06 ms per C3 sweep)
+__global__ void __launch_bounds__(kB) layer_pull_w32_kernel(LayerArgs a) {
+    __shared__ uint32_t binom[33 * 33];
+    {
+        const int cols = a.layer + 1;
+        for (int e = threadIdx.x; e < a.m * cols; e += kB) {
+            const int r = e / cols, i = e - r * cols;
+            binom[r * 33 + i] = (uint32_t)a.binom[r * 33 + i];
+        }
+    }
+    __syncthreads();
+    const int L = a.layer;
+    for (int k = 0; k < kPullPer; ++k) {
+    const uint32_t r = (blockIdx.x * kPullPer + k) * kB + threadIdx.x;
+    if ((uint64_t)r >= a.count) return;
+    uint32_t Tc = 0;
+    {
+        uint32_t rr = r;
+        int c = a.m - 1;
+        for (int i = L; i >= 1; --i) {
+            while (binom[c * 33 + i] > rr) --c;
+            Tc |= 1u << c;
+            rr -= binom[c * 33 + i];
+            --c;
+        }
+    }
+    uint32_t suffix = 0, suffixc = 0;
+    {
+        int i = 0;
+        for (uint32_t x = Tc; x; x &= x - 1, ++i)
+            if (i >= 1) {
+                const int ai = __builtin_ctz(x);
+                suffix += binom[ai * 33 + i];
+                suffixc += binom[(ai - 1) * 33 + i];
+            }
+    }
+    const uint32_t wl = (uint32_t)a.w_layer;
+    uint32_t prefix = 0;
+    float best = FLT_MAX;
+    int bestj = 255;
+    bool reached = false;
+    uint32_t x = Tc;
+    for (int j = 0; j < L; ++j) {
+        const int aj = __builtin_ctz(x);
+        x &= x - 1;
+        const float gp = a.gprev[prefix + suffix];
+        if (gp < FLT_MAX) {
+            reached = true;
+            const float cand = gp + a.w[(uint64_t)aj * a.w_half + (wl + prefix + suffixc)];
+            if (cand < best || bestj == 255) {
+                best = cand;
+                bestj = j;
+            }
+        }
+        if (x) {
+            const int an = __builtin_ctz(x);
+            suffix -= binom[an * 33 + j + 1];
+            suffixc -= binom[(an - 1) * 33 + j + 1];
+        }
+        prefix += binom[aj * 33 + j + 1];
+    }
+    a.gcur[r] = reached ? best : FLT_MAX;
+    a.leaf[r] = (uint8_t)(reached ? bestj : 255);
+    if (a.reached) {
+        const unsigned long long b = __ballot(reached);
+        if ((threadIdx.x & 63) == __ffsll((long long)__ballot(true)) - 1 && b)
+            atomicAdd(&a.reached[blockIdx.x % kCounters], (unsigned long long)__popcll(b));
+    }
+    }
+}
+
 // walk the leaf pointers from the goal back to the root (one thread)
 __global__ void reconstruct_kernel(const uint8_t *leaf, const uint64_t *layer_off, const uint64_t *binom, int m,
                                    int *chain) {
@@ -354,6 +463,16 @@ int components_gpu(const uint64_t *edges, int n, std::vector<uint64_t> &out) {
 }
 }  // namespace
 
+// every variable of comp has a lattice over exactly the rest of comp
+bool sweep_scatter_ok(const SearchState &s, uint64_t comp) {
+    if (!s.tables_ready || (comp & ~s.scope)) return false;
+    for (uint64_t x = comp; x; x &= x - 1) {
+        const int v = __builtin_ctzll(x);
+        if (!((s.table_vars >> v) & 1ull) || s.support[v] != (comp & ~(1ull << v))) return false;
+    }
+    return true;
+}
+
 int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, float *goal_cost, int64_t *expanded) {
     SearchState &s = *c->search;
     const int n = s.n;
@@ -365,15 +484,13 @@ int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, flo
     std::vector<uint64_t> bn(33 * 33, 0);
     for (int a = 0; a <= 32; ++a)
         for (int b = 0; b <= 32; ++b) bn[a * 33 + b] = binom64(a, b);
-    DevBuf<uint64_t> d_bn, d_edges, d_layer_off;
-    DevBuf<int> d_cv, d_chain;
-    DevBuf<float> d_g0, d_g1;
-    DevBuf<uint8_t> d_leaf;
-    DevBuf<unsigned long long> d_acc;
-    auto cleanup = [&]() {
-        release(d_bn); release(d_edges); release(d_layer_off); release(d_cv); release(d_chain);
-        release(d_g0); release(d_g1); release(d_leaf); release(d_acc);
-    };
+    // the sweep's buffers persist in the search state (no allocation per call)
+    DevBuf<uint64_t> &d_bn = s.gs_bn, &d_edges = s.gs_edges, &d_layer_off = s.gs_layer_off;
+    DevBuf<int> &d_cv = s.gs_cv, &d_chain = s.gs_chain;
+    DevBuf<float> &d_g0 = s.gs_g0, &d_g1 = s.gs_g1;
+    DevBuf<uint8_t> &d_leaf = s.gs_leaf;
+    DevBuf<unsigned long long> &d_acc = s.gs_acc;
+    auto cleanup = [&]() {};
     int rc;
     if ((rc = ensure(c, d_bn, bn.size())) || (rc = ensure(c, d_edges, 64)) || (rc = ensure(c, d_cv, kMaxM)) ||
         (rc = ensure(c, d_chain, kMaxM)) || (rc = ensure(c, d_acc, kCounters))) {
@@ -448,8 +565,14 @@ int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, flo
                 e = hipMemcpyAsync(d_lo.p, loffm1.data(), (kMaxM + 1) * 8, hipMemcpyHostToDevice, c->stream);
                 if (e == hipSuccess) {
                     prof_begin(c, "search_sweep_w");
-                    sweep_w_kernel<<<dim3((unsigned)((half + kB - 1) / kB), (unsigned)m), kB, 0, c->stream>>>(
-                        dv, d_bn.p, d_lo.p, d_cv.p, m, half, s.d_sweep_w.p, nullptr);
+                    if (sweep_scatter_ok(s, comp))
+                        sweep_w_scatter_kernel<<<dim3((unsigned)((half + kB * kScatterPer - 1) / (kB * kScatterPer)),
+                                                      (unsigned)m), kB, 0,
+                                                 c->stream>>>(s.d_table.p, s.d_tb_off.p, d_bn.p, d_lo.p, d_cv.p,
+                                                              nullptr, m, half, s.d_sweep_w.p);
+                    else
+                        sweep_w_kernel<<<dim3((unsigned)((half + kB - 1) / kB), (unsigned)m), kB, 0, c->stream>>>(
+                            dv, d_bn.p, d_lo.p, d_cv.p, m, half, s.d_sweep_w.p, nullptr);
                     prof_end(c);
                     e = hipGetLastError();
                 }
@@ -466,7 +589,9 @@ int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, flo
                         d_leaf.p + loff[d], d < m ? d_acc.p : nullptr,
                         use_w ? s.d_sweep_w.p : nullptr, half, loffm1[d - 1]};
             prof_begin(c, "search_layer_pull");
-            if (use_w) layer_pull_kernel<true><<<(unsigned)((cnt + kB - 1) / kB), kB, 0, c->stream>>>(a);
+            if (use_w && c->sweep_table == 1)
+                layer_pull_w32_kernel<<<(unsigned)((cnt + kB * kPullPer - 1) / (kB * kPullPer)), kB, 0, c->stream>>>(a);
+            else if (use_w) layer_pull_kernel<true><<<(unsigned)((cnt + kB - 1) / kB), kB, 0, c->stream>>>(a);
             else layer_pull_kernel<false><<<(unsigned)((cnt + kB - 1) / kB), kB, 0, c->stream>>>(a);
             prof_end(c);
             std::swap(gprev, gcur);
@@ -574,8 +699,18 @@ int sweep_shard_begin(ulg_ctx *c, uint64_t own, int64_t *max_nodes) {
     if (e == hipSuccess) e = hipMemcpyAsync(s.shard_g0.p, &zero, 4, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) {
         prof_begin(c, "search_sweep_w");
-        sweep_w_kernel<<<dim3((unsigned)((half + kB - 1) / kB), (unsigned)nown), kB, 0, c->stream>>>(
-            s.dev(), s.shard_bn.p, d_lo.p, s.shard_cv.p, m, half, s.d_sweep_w.p, d_jl.p);
+        bool scatter = true;
+        for (uint64_t x = own; x; x &= x - 1) {
+            const int v = __builtin_ctzll(x);
+            if (s.support[v] != (all & ~(1ull << v))) scatter = false;
+        }
+        if (scatter)
+            sweep_w_scatter_kernel<<<dim3((unsigned)((half + kB * kScatterPer - 1) / (kB * kScatterPer)), (unsigned)nown),
+                                     kB, 0, c->stream>>>(
+                s.d_table.p, s.d_tb_off.p, s.shard_bn.p, d_lo.p, s.shard_cv.p, d_jl.p, m, half, s.d_sweep_w.p);
+        else
+            sweep_w_kernel<<<dim3((unsigned)((half + kB - 1) / kB), (unsigned)nown), kB, 0, c->stream>>>(
+                s.dev(), s.shard_bn.p, d_lo.p, s.shard_cv.p, m, half, s.d_sweep_w.p, d_jl.p);
         prof_end(c);
         e = hipGetLastError();
     }

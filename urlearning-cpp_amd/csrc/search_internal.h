@@ -232,6 +232,12 @@ struct SearchState {
     // sweep_w[j][p][colex rank of P among the (m-1)-subsets of comp \ {v_j}]
     // = getScore(v_j, P), |P| = p (one contiguous slice per variable and layer)
     DevBuf<float> d_sweep_w;
+    // GPU sweep scratch, kept across calls
+    DevBuf<uint64_t> gs_bn, gs_edges, gs_layer_off;
+    DevBuf<int> gs_cv, gs_chain;
+    DevBuf<float> gs_g0, gs_g1;
+    DevBuf<uint8_t> gs_leaf;
+    DevBuf<unsigned long long> gs_acc;
     uint64_t sweep_comp = 0;
     bool sweep_ready = false;
     // variable-sharded sweep (ulg_sweep_shard_*): this rank's tables and
@@ -292,6 +298,8 @@ struct SearchState {
         release(d_rows); release(d_rowmeta);
         release(d_sweep_w);
         sweep_ready = false;
+        release(gs_bn); release(gs_edges); release(gs_layer_off); release(gs_cv); release(gs_chain);
+        release(gs_g0); release(gs_g1); release(gs_leaf); release(gs_acc);
         release(shard_g0); release(shard_g1); release(shard_leaf); release(shard_bn); release(shard_loff);
         release(shard_wslot); release(shard_cv); release(shard_chain); release(shard_acc);
         shard_active = false;

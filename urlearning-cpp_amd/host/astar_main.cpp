@@ -144,6 +144,12 @@ int main(int argc, char **argv) {
     std::printf("Nodes expanded: %lld\n", (long long)expanded);
     std::printf("Timing: read .pss %.3f s, HIP init %.3f s, GPU best-score tables %.3f s, search (%s) %.3f s (%.3g expansions/s)\n",
                 tr - t0, t1 - tr, t2 - t1, mode.c_str(), t3 - t2, (double)expanded / (t3 - t2));
+    // one machine-readable line on stderr (stdout keeps the reference's text)
+    std::fprintf(stderr,
+                 "ulg_metrics {\"tool\": \"astar\", \"mode\": \"%s\", \"n\": %d, \"cost\": %.6f, \"expanded\": %lld, "
+                 "\"read_s\": %.6f, \"init_s\": %.6f, \"tables_s\": %.6f, \"search_s\": %.6f, \"expansions_per_s\": %.6g}\n",
+                 mode.c_str(), n, (double)cost, (long long)expanded, tr - t0, t1 - tr, t2 - t1, t3 - t2,
+                 (double)expanded / (t3 - t2));
     const std::string net = args.get("netFile");
     if (!net.empty()) {
         std::string txt(text.data());

@@ -161,5 +161,11 @@ int main(int argc, char **argv) {
                 "file write %.3f s (%lld bytes)\n",
                 (long long)scored, (long long)stored, t1 - t0, (double)scored / (t1 - t0), t2 - t1, t3 - t2,
                 (long long)len);
+    std::fprintf(stderr,
+                 "ulg_metrics {\"tool\": \"score\", \"n\": %d, \"N\": %lld, \"k\": %d, \"lambda\": %g, "
+                 "\"scored\": %lld, \"stored\": %lld, \"score_s\": %.6f, \"sets_per_s\": %.6g, \"format_s\": %.6f, "
+                 "\"write_s\": %.6f, \"bytes\": %lld, \"out_of_time\": %d}\n",
+                 n, (long long)N, maxp, lambda, (long long)scored, (long long)stored, t1 - t0,
+                 (double)scored / (t1 - t0), t2 - t1, t3 - t2, (long long)len, (int)oot);
     return 0;
 }

@@ -111,6 +111,10 @@ int main(int argc, char **argv) {
                 (long long)stats[1], (long long)stats[2]);
     std::printf("Timing: read .pss %.3f s, HIP init %.3f s, GPU best-score tables %.3f s, triplet search %.3f s\n",
                 tr - t0, t1 - tr, t2 - t1, t3 - t2);
+    std::fprintf(stderr,
+                 "ulg_metrics {\"tool\": \"triplet_astar\", \"n\": %d, \"runs\": %lld, \"distinct\": %lld, "
+                 "\"expanded\": %lld, \"read_s\": %.6f, \"init_s\": %.6f, \"tables_s\": %.6f, \"search_s\": %.6f}\n",
+                 n, (long long)stats[0], (long long)stats[1], (long long)stats[2], tr - t0, t1 - tr, t2 - t1, t3 - t2);
     const std::string net = args.get("netFile");
     if (!net.empty()) {
         std::string csv;
