@@ -1312,6 +1312,7 @@ struct WideArgs {
     const float *hmax;        // hi-cover tables (hikey_*_kernel) or null
     const float *pval;        // the same variables' present keys by compact mask (absent bits otherwise)
     const uint64_t *hoff;     // [nv] offset of a variable's tables in hmax / pval, ~0 = none
+    int reduced;              // walk_wide_kernel: skip the reference's no-op re-tests
     double N;
     double lambda;
     int n, nv, S, L;
@@ -1476,14 +1477,24 @@ __global__ void __launch_bounds__(64) walk_wide_kernel(WideArgs a, uint64_t qbas
     uint64_t *chk = bits + lid * wpl;
     chk[0] |= 1ull;  // checked.insert(empty_set)
 
+    // Re-test skipping (a.reduced): the inner loop calls fb(T2, npv) once per
+    // appended entry, with npv = the first j appended entries + zero padding.
+    // In call j >= 2 the positions below j-1 were tested by the earlier calls
+    // (each is now checked, or a present key below -ts: testing it again
+    // changes nothing) and the positions from j on are zeros, whose child
+    // T2 ^ {0} call 1 already tested at its position 1.  So call 1 tests
+    // positions 0 and 1 and call j >= 2 only position j-1: the same tests in
+    // the same order, minus the no-ops (O(m) instead of O(m^2) per expanded
+    // node).  ends[d] is where the current call at depth d stops.
     uint64_t Ts[LMAX + 1], Tcs[LMAX + 1];
-    uint8_t idxs[LMAX + 1], is[LMAX + 1], js[LMAX + 1], us[LMAX + 1], inner[LMAX + 1];
+    uint8_t idxs[LMAX + 1], is[LMAX + 1], js[LMAX + 1], us[LMAX + 1], inner[LMAX + 1], ends[LMAX + 1];
     uint8_t pvs[LMAX * (LMAX + 1) / 2 + 1];
     for (int i = 0; i < L; ++i) pvs[i] = (uint8_t)(i + (PHASE == 0 ? 0 : 1));
     int d = 0;
     Ts[0] = Plocal;
     Tcs[0] = cm;
     idxs[0] = 0;
+    ends[0] = (uint8_t)L;
     inner[0] = 0;
     bool dom = false;
     uint64_t steps = 0;
@@ -1495,7 +1506,7 @@ __global__ void __launch_bounds__(64) walk_wide_kernel(WideArgs a, uint64_t qbas
         const int mm = L - d;
         const int po = d * L - d * (d - 1) / 2;  // pvs offset of depth d
         if (!inner[d]) {
-            if (idxs[d] == mm) {  // fb returns
+            if (idxs[d] == ends[d]) {  // fb returns
                 if (d == 0) break;
                 --d;
                 const uint64_t c = Ts[d + 1];
@@ -1573,7 +1584,14 @@ __global__ void __launch_bounds__(64) walk_wide_kernel(WideArgs a, uint64_t qbas
         ++js[d];
         Ts[d + 1] = Ts[d] ^ (1ull << us[d]);
         Tcs[d + 1] = Tcs[d] ^ cbit(us[d]);
-        idxs[d + 1] = 0;
+        if (a.reduced) {
+            const int j = js[d];  // this is call j of fb(T2, npv)
+            idxs[d + 1] = (uint8_t)(j == 1 ? 0 : j - 1);
+            ends[d + 1] = (uint8_t)(j == 1 ? (mm - 1 < 2 ? mm - 1 : 2) : j);
+        } else {
+            idxs[d + 1] = 0;
+            ends[d + 1] = (uint8_t)(mm - 1);
+        }
         inner[d + 1] = 0;
         ++d;
     }
@@ -2030,6 +2048,7 @@ int score_wide_layer(ulg_ctx *c, int L, int ph, hipStream_t st, const uint64_t *
     wa.hmax = nullptr;
     wa.pval = nullptr;
     wa.hoff = nullptr;
+    wa.reduced = c->wide_reduced;
     wa.N = (double)c->N;
     wa.lambda = c->lambda;
     wa.n = c->n;
