@@ -971,12 +971,18 @@ __device__ __forceinline__ void sl_clear(typename Sliced<L, K>::Vec &v, uint32_t
 }
 __device__ __forceinline__ bool wave_any(uint32_t x) { return __ballot(x != 0u) != 0ull; }
 
+// [idx_lo, idx_hi): the positions this call can change anything at.  The
+// j-th call fb(T2, npv) of a node's inner loop sees the positions below j-1
+// already tested by its earlier calls (closed, or present below -ts) and zeros
+// from j on, whose child T2 ^ {0} call 1 tested at its position 1 -- so call 1
+// walks positions 0..1 and call j >= 2 position j-1 only (the reference's
+// remaining re-tests are no-ops; the same tests in the same order).
 template <int L, int K, int M, bool DIAG = false>
 __device__ __forceinline__ void walk_sliced(uint32_t T, uint32_t pv, uint32_t act, const typename Sliced<L, K>::Vec &hiV,
                                             typename Sliced<L, K>::Vec &openV, uint32_t &alive, uint32_t &dom,
-                                            uint32_t &pts) {
+                                            uint32_t &pts, int idx_lo = 0, int idx_hi = M) {
 #pragma nounroll
-    for (int idx = 0; idx < M; ++idx) {
+    for (int idx = idx_lo; idx < idx_hi; ++idx) {
         act &= alive;
         if (!wave_any(act)) return;
         if constexpr (DIAG) ++pts;
@@ -998,7 +1004,8 @@ __device__ __forceinline__ void walk_sliced(uint32_t T, uint32_t pv, uint32_t ac
                 if (pi == u) continue;
                 npv |= pi << (4 * j);
                 ++j;
-                walk_sliced<L, K, M - 1, DIAG>(T2, npv, x, hiV, openV, alive, dom, pts);
+                if (j == 1) walk_sliced<L, K, M - 1, DIAG>(T2, npv, x, hiV, openV, alive, dom, pts, 0, M - 1 < 2 ? M - 1 : 2);
+                else walk_sliced<L, K, M - 1, DIAG>(T2, npv, x, hiV, openV, alive, dom, pts, j - 1, j);
                 sl_clear<L, K>(openV, T2, x);  // checked.insert(T2) for the sets that ran the call
                 x &= alive;
                 if (!wave_any(x)) break;
