@@ -306,6 +306,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-search", action="store_true")
     ap.add_argument("--score-variant", type=int, default=None, help="A/B knob (ulg_set_option score_variant)")
+    ap.add_argument("--option", action="append", default=[], help="A/B knob name=value (ulg_set_option)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo + --device: rehearse the N>1 code path with several ranks on one GPU")
     ap.add_argument("--device", type=int, default=None, help="GPU for every rank (default LOCAL_RANK)")
@@ -337,6 +338,9 @@ def main():
     ctx = ulg.Context(local)
     if args.score_variant is not None:
         ctx.set_option("score_variant", args.score_variant)
+    for kv in args.option:
+        k_, v_ = kv.split("=", 1)
+        ctx.set_option(k_, int(v_))
     ctx.load(X, lam)
     cands_all = [(1 << n) - 1] * n
     skel_note = "full n x n skeleton"

@@ -497,7 +497,18 @@ struct ScoreArgs {
     double N;
     double lambda;
     int n, nv, S;
+    int xcd;                    // remap blocks so each XCD takes a contiguous run of sets
 };
+
+// Blocks are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8),
+// and each XCD has its own L2.  With xcd set, XCD x takes the x-th contiguous
+// eighth of the launch's blocks -- the sets of a few variables, whose slabs
+// then stay in that XCD's L2 -- through a bijection of [0, nb).
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, int on) {
+    if (!on) return b;
+    const uint32_t x = b & 7u, k = b >> 3, q = nb >> 3, r = nb & 7u;
+    return x * q + (x < r ? x : r) + k;
+}
 
 // bitset words per lane over the subsets of L + 1 local bits
 __host__ __device__ constexpr int bits_words(int L) { return (L + 1) <= 6 ? 1 : (1 << ((L + 1) - 6)); }
@@ -549,7 +560,7 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
     for (int i = threadIdx.x; i <= a.nv * a.S; i += kBlock) toff[i] = a.tbl_off[i];
     __syncthreads();
 
-    const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t gid = (uint64_t)xcd_block(blockIdx.x, gridDim.x, a.xcd) * kBlock + threadIdx.x;
     if (gid >= work[a.nv]) return;
     int lo = 0, hi = a.nv;
     while (hi - lo > 1) {
@@ -2299,6 +2310,7 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     sa.n = n;
     sa.nv = nv;
     sa.S = S;
+    sa.xcd = c->score_xcd;
     // queue entries address the table with 32 bits; beyond that the one-pass
     // form (identical results) is used
     const int variant = (c->score_variant & 16) && (total_slots >> 32) ? 1 : c->score_variant;

@@ -44,6 +44,7 @@ struct LayerArgs {
     const float *w;          // sweep table (SearchState::d_sweep_w) or null
     uint64_t w_half;         // 2^(m-1): one variable's slice group
     uint64_t w_layer;        // sum_{q < layer-1} C(m-1, q): the slice of the predecessors' layer
+    int xcd;                 // contiguous runs of nodes per XCD (layer_pull_w32_kernel)
 };
 
 constexpr int kCounters = 256;
@@ -350,8 +351,16 @@ __global__ void __launch_bounds__(kB) layer_pull_w32_kernel(LayerArgs a) {
     }
     __syncthreads();
     const int L = a.layer;
+    // block b runs on XCD b % 8; with xcd, XCD x takes the x-th contiguous
+    // eighth of the layer (colex-near nodes share predecessors and slice runs
+    // in that XCD's L2)
+    uint32_t bl = blockIdx.x;
+    if (a.xcd) {
+        const uint32_t nb = gridDim.x, x = bl & 7u, kk = bl >> 3, q = nb >> 3, rr = nb & 7u;
+        bl = x * q + (x < rr ? x : rr) + kk;
+    }
     for (int k = 0; k < kPullPer; ++k) {
-    const uint32_t r = (blockIdx.x * kPullPer + k) * kB + threadIdx.x;
+    const uint32_t r = (bl * kPullPer + k) * kB + threadIdx.x;
     if ((uint64_t)r >= a.count) return;
     uint32_t Tc = 0;
     {
@@ -587,7 +596,7 @@ int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, flo
             const uint64_t cnt = binom64(m, d);
             LayerArgs a{dv, d_bn.p, d_cv.p, d_edges.p, filt, symmetric && filt ? 1 : 0, m, d, cnt, gprev, gcur,
                         d_leaf.p + loff[d], d < m ? d_acc.p : nullptr,
-                        use_w ? s.d_sweep_w.p : nullptr, half, loffm1[d - 1]};
+                        use_w ? s.d_sweep_w.p : nullptr, half, loffm1[d - 1], c->sweep_xcd};
             prof_begin(c, "search_layer_pull");
             if (use_w && c->sweep_table == 1)
                 layer_pull_w32_kernel<<<(unsigned)((cnt + kB * kPullPer - 1) / (kB * kPullPer)), kB, 0, c->stream>>>(a);

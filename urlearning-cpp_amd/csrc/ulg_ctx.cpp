@@ -175,6 +175,16 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         c->table_budget_kb = (uint64_t)value;
         return ULG_OK;
     }
+    if (std::strcmp(name, "sweep_xcd") == 0) {
+        if (value < 0 || value > 1) return set_err(c, ULG_ERR_ARG, "sweep_xcd must be 0 or 1");
+        c->sweep_xcd = (int)value;
+        return ULG_OK;
+    }
+    if (std::strcmp(name, "score_xcd") == 0) {
+        if (value < 0 || value > 1) return set_err(c, ULG_ERR_ARG, "score_xcd must be 0 or 1");
+        c->score_xcd = (int)value;
+        return ULG_OK;
+    }
     if (std::strcmp(name, "wide_reduced") == 0) {
         if (value < 0 || value > 1) return set_err(c, ULG_ERR_ARG, "wide_reduced must be 0 or 1");
         c->wide_reduced = (int)value;

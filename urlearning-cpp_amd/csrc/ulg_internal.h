@@ -78,7 +78,9 @@ struct ulg_ctx {
     uint64_t table_budget_kb = 0;  // best-score table budget in KiB (0 = half the free HBM)
     int sweep_table = 1;
     int wide_prune = 1;            // wide walks: skip absent nodes whose subsets hold no key >= -ts
-    int wide_reduced = 1;          // wide walks: skip the recursion's no-op re-tests           // GPU search: successor costs in the sweep's (layer, colex) order
+    int wide_reduced = 1;          // wide walks: skip the recursion's no-op re-tests
+    int score_xcd = 1;             // scoring kernels: contiguous runs of sets per XCD
+    int sweep_xcd = 1;             // GPU sweep launches: contiguous runs of nodes per XCD           // GPU search: successor costs in the sweep's (layer, colex) order
     ulg::DevBuf<float> table;
     ulg::DevBuf<uint64_t> d_tbl_off, d_work, d_blk;
     ulg::DevBuf<uint8_t> d_cand;  // [nv][64] compact index -> variable
