@@ -75,7 +75,7 @@ def main():
     kernels = {
         "score_layer_6_rest": lambda k: k.startswith("void (anonymous namespace)::score_layer_kernel<6, 1"),
         "walk_6_rest": lambda k: "walk_sliced_kernel<6, 1" in k,
-        "layer_pull_kernel(sweep table)": lambda k: "layer_pull_kernel<true>" in k,
+        "layer_pull_kernel(sweep table)": lambda k: "layer_pull_w32_kernel" in k,
     }
     per = {}
     for nm, pred in kernels.items():
@@ -133,7 +133,7 @@ def bench_traffic(summary_path, out_dir):
     sweeps = p["dispatches_b_fetch"] // n
     per_sweep = n * (2 * 1024 * p["FETCH_SIZE"] + 1024 * p["WRITE_SIZE"])
     algo = sum(math.comb(n, L) * (8 * L + 5) for L in range(1, n + 1))
-    json.dump({"kernel": "layer_pull_kernel<true>", "config_id": "c3", "n": n, "sweeps": sweeps,
+    json.dump({"kernel": "layer_pull_w32_kernel", "config_id": "c3", "n": n, "sweeps": sweeps,
                "fetch_kib_per_sweep": n * p["FETCH_SIZE"], "write_kib_per_sweep": n * p["WRITE_SIZE"],
                "traffic_bytes_per_sweep": per_sweep, "algorithmic_bytes_per_sweep": algo,
                "correction": note, "sources": ["profiles/r2/pmc_b_fetch.csv", "profiles/r2/pmc_b_write.csv"]},

@@ -98,7 +98,8 @@ def test_c1_hepatitis_default_parent_limit_matches_digest(ulg_ctx):
 def test_wide_hicover_prune_identical_lists(ulg_ctx):
     """ulg_set_option("wide_prune"): the walks skip absent nodes below which no
     present key reaches -ts; "wide_reduced": they skip the recursion's no-op
-    re-tests.  The stored lists with and without either are identical bit for
+    re-tests; "wide_lds": walks over 2^13 steps are replayed with their bitsets
+    in LDS.  The stored lists with and without either are identical bit for
     bit, on C4's (n=30, N=100k, MMPC, -p = n-1) variables
     whose unpruned walks finish in well under a second each."""
     import ulg
@@ -111,14 +112,16 @@ def test_wide_hicover_prune_identical_lists(ulg_ctx):
     assert all(9 <= bin(cands[v] & ~(1 << v)).count("1") <= 12 for v in vs)
     out = []
     try:
-        for prune, reduced in ((0, 0), (1, 0), (0, 1), (1, 1)):
+        for prune, reduced, lds in ((0, 0, 0), (1, 0, 0), (0, 1, 0), (1, 1, 0), (1, 1, 1)):
             ulg_ctx.set_option("wide_prune", prune)
             ulg_ctx.set_option("wide_reduced", reduced)
+            ulg_ctx.set_option("wide_lds", lds)
             offs, sets, scores = ulg_ctx.score_all(vs, [cands[v] for v in vs], n - 1)
             out.append((np.asarray(offs).copy(), np.asarray(sets).copy(), np.asarray(scores).copy()))
     finally:
         ulg_ctx.set_option("wide_prune", 1)
         ulg_ctx.set_option("wide_reduced", 1)
+        ulg_ctx.set_option("wide_lds", 1)
     for o in out[1:]:
         assert np.array_equal(out[0][0], o[0])
         assert np.array_equal(out[0][1], o[1])

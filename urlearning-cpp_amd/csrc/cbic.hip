@@ -1448,7 +1448,8 @@ __global__ void __launch_bounds__(kBlock) score_wide_kernel(WideArgs a) {
 template <int LMAX, int PHASE>
 __global__ void __launch_bounds__(64) walk_wide_kernel(WideArgs a, uint64_t qbase, uint64_t qn, uint64_t *bits,
                                                        uint64_t wpl, unsigned long long *err,
-                                                       unsigned long long *wstats) {
+                                                       unsigned long long *wstats, uint64_t budget,
+                                                       uint64_t *squeue, unsigned long long *scount) {
     const uint64_t lid = (uint64_t)blockIdx.x * 64 + threadIdx.x;
     const uint64_t qi = qbase + lid;
     if (qi >= qn) return;
@@ -1520,6 +1521,15 @@ __global__ void __launch_bounds__(64) walk_wide_kernel(WideArgs a, uint64_t qbas
         if (++steps > kWideStepCap) {
             atomicOr(err, 1ull);
             break;
+        }
+        if (budget && steps > budget && dense) {
+            // a long walk: hand it to walk_wide_lds_kernel, which replays it
+            // from the start with every bitset in LDS (same walk)
+            const unsigned long long pos = atomicAdd(scount, 1ull);
+            squeue[3 * pos] = e[0];
+            squeue[3 * pos + 1] = e[1];
+            squeue[3 * pos + 2] = e[2];
+            return;
         }
         const int mm = L - d;
         const int po = d * L - d * (d - 1) / 2;  // pvs offset of depth d
@@ -1624,7 +1634,7 @@ __global__ void __launch_bounds__(64) walk_wide_kernel(WideArgs a, uint64_t qbas
 
 using WideFn = void (*)(WideArgs);
 using WideWalkFn = void (*)(WideArgs, uint64_t, uint64_t, uint64_t *, uint64_t, unsigned long long *,
-                           unsigned long long *);
+                           unsigned long long *, uint64_t, uint64_t *, unsigned long long *);
 WideFn wide_fn(int L, int phase) {
     if (L <= 16) return phase == 0 ? score_wide_kernel<16, 0> : score_wide_kernel<16, 1>;
     return phase == 0 ? score_wide_kernel<kWideMax, 0> : score_wide_kernel<kWideMax, 1>;
@@ -1632,6 +1642,138 @@ WideFn wide_fn(int L, int phase) {
 WideWalkFn wide_walk_fn(int L, int phase) {
     if (L <= 16) return phase == 0 ? walk_wide_kernel<16, 0> : walk_wide_kernel<16, 1>;
     return phase == 0 ? walk_wide_kernel<kWideMax, 0> : walk_wide_kernel<kWideMax, 1>;
+}
+
+// ---- long wide walks in LDS -----------------------------------------------
+// A wide walk is one lane's sequential DFS; the few long ones set a layer's
+// time (C4: 0.6 M steps for one set at L = 17), and in walk_wide_kernel every
+// step waits on scratch memory and global bitsets (~1 us).  Walks over
+// kStragBudget steps (only where q = |local bits| <= kStragQMax and the
+// hi-cover tables exist) are re-queued and replayed here from the start, one
+// workgroup per set: the 64 lanes first lay out, over the 2^q local subsets,
+// bitsets of `present`, `hi` (present and >= -ts) and `cover` (some key >= -ts
+// among its subsets and variable 0) from pval / hmax, then lane 0 runs the
+// same reduced walk with `checked`, those bitsets and its frame stack in LDS.
+constexpr int kStragQMax = 18;                 // 4 bitsets of 2^18 bits = 128 KiB of LDS
+constexpr uint64_t kStragBudget = 1ull << 13;  // steps before a walk moves here
+constexpr int kStragState = 32 * 4 + 7 * 32 + 32 * 33 / 2 + 16;  // Ts, 6 x u8 frames, pvs, lc
+
+template <int PHASE>
+__global__ void __launch_bounds__(64) walk_wide_lds_kernel(WideArgs a, const uint64_t *sq) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int L = a.L;
+    const int q = PHASE == 0 ? L : L + 1;
+    const uint32_t nw = (1u << q) >> 6;
+    uint64_t *chk = reinterpret_cast<uint64_t *>(smem);
+    uint64_t *pres = chk + nw, *hib = pres + nw, *cov = hib + nw;
+    uint32_t *Ts = reinterpret_cast<uint32_t *>(cov + nw);
+    uint8_t *idxs = reinterpret_cast<uint8_t *>(Ts + 32);
+    uint8_t *is = idxs + 32, *js = is + 32, *us = js + 32, *inner = us + 32, *ends = inner + 32, *lc = ends + 32;
+    uint8_t *pvs = lc + 32;
+    const uint64_t *e = sq + 3 * (uint64_t)blockIdx.x;
+    const uint64_t slot = e[0], cm = e[1];
+    const int vi = (int)(uint32_t)e[2];
+    const float ts = __uint_as_float((uint32_t)(e[2] >> 32));
+    const float thr = -ts;
+    const bool z = a.meta[vi * 4 + 2] != 0;
+    const uint64_t zb = z ? 1ull : 0ull;
+    const uint64_t ho = a.hoff[vi];
+    if (threadIdx.x == 0) {
+        uint64_t rem = cm;
+        const int first = PHASE == 0 ? 0 : 1;
+        lc[0] = 0;
+        for (int i = first; i < L + first; ++i) {
+            lc[i] = (uint8_t)__builtin_ctzll(rem);
+            rem &= rem - 1;
+        }
+    }
+    __syncthreads();
+    for (uint32_t w = threadIdx.x; w < nw; w += 64) {
+        uint64_t pw = 0, hw = 0, cw = 0;
+        for (int b = 0; b < 64; ++b) {
+            const uint32_t t = (w << 6) | (uint32_t)b;
+            uint64_t X = (t & 1u) ? zb : 0ull;  // local bit 0 = variable 0
+            for (uint32_t y = t & ~1u; y; y &= y - 1) X |= 1ull << lc[__builtin_ctz(y)];
+            if (!(PHASE == 1 && (t & 1u) && !z)) {
+                const float val = a.pval[ho + X];
+                if (fbits(val) != kAbsentBits) {
+                    pw |= 1ull << b;
+                    if (val >= thr) hw |= 1ull << b;
+                }
+            }
+            if (a.hmax[ho + (X | zb)] >= thr) cw |= 1ull << b;
+        }
+        pres[w] = pw;
+        hib[w] = hw;
+        cov[w] = cw;
+        chk[w] = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    auto bit = [](const uint64_t *v, uint32_t t) -> bool { return (v[t >> 6] >> (t & 63)) & 1ull; };
+    chk[0] |= 1ull;  // checked.insert(empty_set)
+    for (int i = 0; i < L; ++i) pvs[i] = (uint8_t)(i + (PHASE == 0 ? 0 : 1));
+    int d = 0;
+    Ts[0] = PHASE == 0 ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
+    idxs[0] = 0;
+    ends[0] = (uint8_t)L;
+    inner[0] = 0;
+    bool dom = false;
+    while (true) {
+        const int mm = L - d;
+        const int po = d * L - d * (d - 1) / 2;
+        if (!inner[d]) {
+            if (idxs[d] == ends[d]) {
+                if (d == 0) break;
+                --d;
+                const uint32_t c = Ts[d + 1];
+                chk[c >> 6] |= 1ull << (c & 63);
+                continue;
+            }
+            const uint8_t u = pvs[po + idxs[d]];
+            const uint32_t T2 = Ts[d] ^ (1u << u);
+            if (bit(chk, T2)) {
+                ++idxs[d];
+                continue;
+            }
+            if (bit(pres, T2)) {
+                if (bit(hib, T2)) {
+                    dom = true;
+                    break;
+                }
+                ++idxs[d];
+                continue;
+            }
+            if (!bit(cov, T2)) {
+                chk[T2 >> 6] |= 1ull << (T2 & 63);
+                ++idxs[d];
+                continue;
+            }
+            inner[d] = 1;
+            is[d] = 0;
+            js[d] = 0;
+            us[d] = u;
+            for (int k = 0; k < mm - 1; ++k) pvs[po + mm + k] = 0;
+            continue;
+        }
+        if (is[d] == mm) {
+            inner[d] = 0;
+            ++idxs[d];
+            continue;
+        }
+        const uint8_t pi = pvs[po + is[d]];
+        ++is[d];
+        if (pi == us[d]) continue;
+        pvs[po + mm + js[d]] = pi;
+        ++js[d];
+        Ts[d + 1] = Ts[d] ^ (1u << us[d]);
+        const int j = js[d];
+        idxs[d + 1] = (uint8_t)(j == 1 ? 0 : j - 1);
+        ends[d + 1] = (uint8_t)(j == 1 ? (mm - 1 < 2 ? mm - 1 : 2) : j);
+        inner[d + 1] = 0;
+        ++d;
+    }
+    a.table[slot] = dom ? absent_f() : -ts;
 }
 
 // ---- hi-cover tables for the wide walks ---------------------------------
@@ -2052,7 +2194,7 @@ const char *kLayerNames[2][kMaxL + 1] = {
 int score_wide_layer(ulg_ctx *c, int L, int ph, hipStream_t st, const uint64_t *d_work, const uint64_t *h_work,
                      uint64_t cnt, int nv, int S, int kmax, uint64_t *queue, unsigned long long *qc,
                      unsigned long long *errf, uint64_t *bits, uint64_t slice, int *d_hmeta,
-                     const std::vector<uint64_t> &hoff, const std::vector<int> &meta) {
+                     const std::vector<uint64_t> &hoff, const std::vector<int> &meta, unsigned long long *scnt) {
     WideArgs wa;
     wa.gram = c->gram.p;
     wa.binom = c->d_binom64.p;
@@ -2145,14 +2287,32 @@ int score_wide_layer(ulg_ctx *c, int L, int ph, hipStream_t st, const uint64_t *
         ws = c->d_stats.p;
         ULG_HIP(c, hipMemsetAsync(ws, 0, 32, st));
     }
+    // long walks move to the LDS kernel (reduced walks with hi-cover tables only)
+    const uint64_t budget = (wa.hoff && wa.reduced && q <= kStragQMax && c->wide_lds) ? kStragBudget : 0;
+    uint64_t *sq = queue + 3 * qn;  // straggler queue after this launch's entries (the queue has room)
+    if (budget) ULG_HIP(c, hipMemsetAsync(scnt, 0, 8, st));
     for (uint64_t base = 0; base < qn; base += per) {
         const uint64_t k = std::min<uint64_t>(per, qn - base);
         ULG_HIP(c, hipMemsetAsync(bits, 0, (size_t)(k * wpl * 8), st));
         prof_begin_s(c, ph == 0 ? "walk_wide_var0" : "walk_wide_rest", st);
         hipLaunchKernelGGL(wf, dim3((unsigned)((k + 63) / 64)), dim3(64), 0, st, wa, base, base + k, bits, wpl, errf,
-                           ws);
+                           ws, budget, sq, scnt);
         prof_end_s(c, st);
         ULG_HIP(c, hipGetLastError());
+    }
+    if (budget) {
+        unsigned long long sn = 0;
+        ULG_HIP(c, hipMemcpyAsync(&sn, scnt, 8, hipMemcpyDeviceToHost, st));
+        ULG_HIP(c, hipStreamSynchronize(st));
+        if (sn > 0) {
+            const size_t lds = (size_t)4 * ((size_t)1 << q) / 8 + kStragState;
+            const auto kf = ph == 0 ? walk_wide_lds_kernel<0> : walk_wide_lds_kernel<1>;
+            ULG_HIP(c, hipFuncSetAttribute((const void *)kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            prof_begin_s(c, "walk_wide_lds", st);
+            hipLaunchKernelGGL(kf, dim3((unsigned)sn), dim3(64), lds, st, wa, sq);
+            prof_end_s(c, st);
+            ULG_HIP(c, hipGetLastError());
+        }
     }
     if (wstat) {
         unsigned long long h[4];
@@ -2358,7 +2518,7 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
         for (int L = 1; L <= kmax; ++L)
             for (int ph = 0; ph < 2; ++ph) {
                 const uint64_t cnt = h_wk[(size_t)g * (G > 1 ? wstride : 0) + ((size_t)L * 2 + ph) * (nv + 1) + nv];
-                if (L > kMaxL) wqwords = std::max<uint64_t>(wqwords, 3 * cnt);
+                if (L > kMaxL) wqwords = std::max<uint64_t>(wqwords, 6 * cnt);  // entries + straggler copies
                 else if (variant & 16) qwords = std::max<uint64_t>(qwords, cnt * (uint64_t)(1 + 2 * bits_words(L)));
             }
     // queue counters per (group, layer, phase), then the wide walks' error flag
@@ -2376,7 +2536,7 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     if (kmax > kMaxL) {
         const uint64_t wpl_max = kmax + 1 <= 6 ? 1ull : (1ull << (kmax + 1 - 6));
         wslice = std::max<uint64_t>(kWideBitsWords / (uint64_t)G, wpl_max);
-        if ((rc = ensure(c, c->d_wbits, (size_t)(G * wslice)))) return rc;
+        if ((rc = ensure(c, c->d_wbits, (size_t)(G * wslice))) || (rc = ensure(c, c->d_scount, (size_t)G))) return rc;
         // hi-cover tables for the variables that reach a wide layer
         if (c->wide_prune) {
             hoff.assign(nv, ~0ull);
@@ -2452,7 +2612,7 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
                                                wslice,
                                                hoff.empty() ? nullptr
                                                             : c->d_hmeta.p + (size_t)g * (nv + (size_t)(nv + 1) * 8),
-                                               hoff, meta)))
+                                               hoff, meta, c->d_scount.p + g)))
                         return rc;
                     continue;
                 }

@@ -79,6 +79,7 @@ struct ulg_ctx {
     int sweep_table = 1;
     int wide_prune = 1;            // wide walks: skip absent nodes whose subsets hold no key >= -ts
     int wide_reduced = 1;          // wide walks: skip the recursion's no-op re-tests
+    int wide_lds = 1;              // wide walks: long ones replayed with their bitsets in LDS
     int score_xcd = 1;             // scoring kernels: contiguous runs of sets per XCD
     int sweep_xcd = 1;             // GPU sweep launches: contiguous runs of nodes per XCD           // GPU search: successor costs in the sweep's (layer, colex) order
     ulg::DevBuf<float> table;
@@ -117,6 +118,7 @@ struct ulg_ctx {
     uint64_t hmax_half = 0;         // entries of each half of d_hmax
     ulg::DevBuf<uint64_t> d_hoff;   // [nv] table offsets, ~0 = no table
     ulg::DevBuf<int> d_hmeta;       // per stream group: launch variables and tile / block prefixes
+    ulg::DevBuf<unsigned long long> d_scount;  // per stream group: long wide walks handed to the LDS kernel
     std::map<std::string, std::vector<double>> prof_ms;
 };
 
