@@ -126,3 +126,42 @@ def test_wide_hicover_prune_identical_lists(ulg_ctx):
         assert np.array_equal(out[0][0], o[0])
         assert np.array_equal(out[0][1], o[1])
         assert out[0][2].tobytes() == o[2].tobytes()
+
+
+@pytest.mark.timeout(400)
+def test_c1_hepatitis_reference_defaults_lambda_half(ulg_ctx):
+    """Config C1 at the reference's defaults: lambda 0.5 (score_main.cpp:214)
+    and -p 19 on data/hepatitis.clean.csv.  The walks are far deeper than at
+    lambda 2 (the GPU takes about 75 s; the oracle's literal recursion does
+    not finish the 19 layers in hours), so tests/golden/c1_hepatitis_default.json
+    holds the oracle run with -p K: every layer <= K of the GPU's -p 19 lists
+    must equal it (a layer's stored sets depend only on the layers below)."""
+    path = os.path.join(GOLDEN, "c1_hepatitis_default.json")
+    if not os.path.exists(path):
+        pytest.fail("tests/golden/c1_hepatitis_default.json missing: run tests/golden/make_c1_default_fixture.py")
+    with open(path) as f:
+        fx = json.load(f)
+    X = load_csv_ascii(os.path.join(GOLDEN, fx["csv"]))
+    n = X.shape[1]
+    assert (X.shape[0], n) == (fx["N"], fx["n"])
+    ulg_ctx.load(X, fx["lambda"])
+    offs, sets, scores = ulg_ctx.score_all(list(range(n)), [(1 << n) - 1] * n, fx["max_parents_run"])
+    K = fx["layers_checked"]
+    deeper = 0
+    for v in range(n):
+        d = fx["per_variable"][v]
+        s = sets[offs[v]:offs[v + 1]]
+        sc = scores[offs[v]:offs[v + 1]]
+        pc = np.bitwise_count(s.astype(np.uint64))
+        assert np.all(np.diff(pc) >= 0), v
+        low = int(np.searchsorted(pc, K, side="right"))
+        deeper += len(s) - low
+        s, sc = s[:low], sc[:low]
+        assert len(s) == d["count"], f"variable {v}: {len(s)} stored in layers <= {K} vs oracle {d['count']}"
+        assert hashlib.sha256(np.ascontiguousarray(s, dtype=np.uint64).tobytes()).hexdigest() == d["sets_sha256"], v
+        tot = float(sc.astype(np.float64).sum())
+        assert abs(tot - d["score_sum"]) <= REL_TOL * max(abs(d["score_sum"]), 1.0), (v, tot, d["score_sum"])
+        for idx, (ps, pscore) in zip(np.unique(np.linspace(0, len(s) - 1, 64).astype(np.int64)), d["samples"]):
+            assert int(s[idx]) == ps
+            assert abs(float(sc[idx]) - pscore) <= REL_TOL * max(abs(pscore), 1.0), (v, ps, float(sc[idx]), pscore)
+    assert deeper > 0  # layers above K stored sets too (checked only through the GPU's own walk forms)
