@@ -244,6 +244,7 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
     int64_t nexp = 0;
     static const bool prof = std::getenv("ULG_EXACT_PROF") != nullptr;
     uint64_t c_pop = 0, c_succ = 0, t0 = 0, t1 = 0;
+    uint64_t pop_hist[64][2] = {};  // pop cycles by log2(heap length)
     int64_t n_push = 0, n_upd = 0, n_succ = 0;
     while (open.len > 0) {
         if (deadline && (nexp & 4095) == 0 && Clock::now() > *deadline) {
@@ -251,8 +252,15 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
             break;
         }
         if (prof) t0 = __rdtsc();
+        const int64_t hl = open.len;
         const uint32_t ui = open.pop();
-        if (prof) { t1 = __rdtsc(); c_pop += t1 - t0; }
+        if (prof) {
+            t1 = __rdtsc();
+            c_pop += t1 - t0;
+            const int b = 63 - __builtin_clzll((uint64_t)hl | 1ull);
+            pop_hist[b][0] += t1 - t0;
+            pop_hist[b][1] += 1;
+        }
         ++nexp;
         if (ui == goal_slot) { goal = ui; break; }
         DenseRec &U = recs[ui];
@@ -301,6 +309,11 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
                      "Gcycles pop=%.3f succ_loop=%.3f stale_scans=%lld\n",
                      (long long)nexp, (long long)n_succ, (long long)n_push, (long long)n_upd, (long long)open.hwm,
                      c_pop * 1e-9, c_succ * 1e-9, (long long)open.scans);
+    if (prof)
+        for (int b = 0; b < 64; ++b)
+            if (pop_hist[b][1])
+                std::fprintf(stderr, "exact_prof(dense) pops with heap 2^%d: %llu, %.0f cycles each\n", b,
+                             (unsigned long long)pop_hist[b][1], (double)pop_hist[b][0] / (double)pop_hist[b][1]);
     *expanded += nexp;
     if (open.hang) *hang = true;
     if (goal < 0) return ULG_OK;
