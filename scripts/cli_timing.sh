@@ -21,6 +21,6 @@ for c in c2:${CK2:-4} c3:${CK3:-6}; do
   ls -la /tmp/$name.pss >> $OUT/${name}_score.log
   timeout -k 10 300 $B/astar /tmp/$name.pss -n /tmp/${name}_net --mode ${MODE:-exact} > $OUT/${name}_astar.log 2>&1 || exit $?
   t2=$(date +%s.%N)
-  echo "$name wall: score $(echo "$t1 - $t0" | bc) s, astar $(echo "$t2 - $t1" | bc) s"
+  python3 -c "print('$name wall: score %.3f s, astar %.3f s' % ($t1 - $t0, $t2 - $t1))"
   cat $OUT/${name}_score.log $OUT/${name}_astar.log
 done
