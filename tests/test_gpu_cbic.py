@@ -243,3 +243,48 @@ def test_walk_forms_identical_c3(ulg_ctx, monkeypatch):
     for k in ("1", "1w2"):
         for a, b in zip(res["4"], res[k]):
             assert a.tobytes() == b.tobytes(), k
+
+
+def test_score_graph_replay_identical_and_profiled(ulg_ctx):
+    """ulg_set_option("score_graph"): the scoring launch sequence is captured
+    into a hipGraph on the first call and replayed on the next ones with the
+    same variables, limits and buffers.  The lists are identical with and
+    without it, across replays, after a reload with other data and another
+    lambda (same shapes: the graph replays with the new Gram matrix and the
+    recapture picks up the new lambda), and a call with other variables
+    recaptures.  With profiling on the calls run unrolled (HIP events time
+    every kernel)."""
+    n, N, k = 20, 10000, 4
+    outs = []
+    try:
+        for graph in (0, 1, 1, 1):
+            ulg_ctx.set_option("score_graph", graph)
+            X, _ = synth.gaussian_sem(n, N, 9200)
+            ulg_ctx.load(X, 2.0)
+            outs.append(ulg_ctx.score_all(list(range(n)), [(1 << n) - 1] * n, k))
+        # other data, other lambda, then a variable subset (recapture)
+        res = {}
+        for graph in (0, 1):
+            ulg_ctx.set_option("score_graph", graph)
+            X2, _ = synth.gaussian_sem(n, N, 9201)
+            ulg_ctx.load(X2, 1.0)
+            a = ulg_ctx.score_all(list(range(n)), [(1 << n) - 1] * n, k)
+            b = ulg_ctx.score_all([3, 7, 11], [(1 << n) - 1] * 3, k)
+            res[graph] = (a, b)
+        ulg_ctx.set_option("score_graph", 1)
+        ulg_ctx.profile(True)
+        ulg_ctx.profile_select(["score_layer_4_rest"])
+        ulg_ctx.profile_reset()
+        for _ in range(3):
+            ulg_ctx.score(list(range(n)), [(1 << n) - 1] * n, k)
+        p = ulg_ctx.profile_get("score_layer_4_rest")
+    finally:
+        ulg_ctx.profile(False)
+        ulg_ctx.profile_select(None)
+        ulg_ctx.set_option("score_graph", 1)
+    for o in outs[1:]:
+        for x, y in zip(outs[0], o):
+            assert np.asarray(x).tobytes() == np.asarray(y).tobytes()
+    for x, y in zip(res[0][0] + res[0][1], res[1][0] + res[1][1]):
+        assert np.asarray(x).tobytes() == np.asarray(y).tobytes()
+    assert p is not None and p["count"] == 3 and p["avg_ms"] > 0

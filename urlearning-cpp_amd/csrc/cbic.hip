@@ -2191,139 +2191,193 @@ const char *kLayerNames[2][kMaxL + 1] = {
 // the queue length) the walks, in chunks whose checked bitsets fit the budget.
 // `bits` is this stream group's own slice of c->d_wbits (`slice` words): the
 // groups' walks run concurrently on their own streams.
-int score_wide_layer(ulg_ctx *c, int L, int ph, hipStream_t st, const uint64_t *d_work, const uint64_t *h_work,
-                     uint64_t cnt, int nv, int S, int kmax, uint64_t *queue, unsigned long long *qc,
-                     unsigned long long *errf, uint64_t *bits, uint64_t slice, int *d_hmeta,
-                     const std::vector<uint64_t> &hoff, const std::vector<int> &meta, unsigned long long *scnt) {
+// One wide layer phase for every stream group, in stages so the groups stay
+// concurrent: every group's scoring launch; the queue lengths (one D2H each
+// into pinned memory, then the syncs -- the launches already overlap); every
+// group's hi-cover tables and walks; the long-walk counts; the LDS replays.
+// `bits` is each group's own slice of c->d_wbits (`slice` words).
+struct WideGroup {
+    hipStream_t st;
+    const uint64_t *d_work, *h_work;
+    uint64_t cnt;
+    uint64_t *queue;
+    unsigned long long *qc, *scnt;
+    uint64_t *bits;
+    int *d_hmeta;
     WideArgs wa;
-    wa.gram = c->gram.p;
-    wa.binom = c->d_binom64.p;
-    wa.cand = c->d_cand.p;
-    wa.meta = c->d_meta.p;
-    wa.tbl_off = c->d_tbl_off.p;
-    wa.work = d_work;
-    wa.table = c->table.p;
-    wa.queue = queue;
-    wa.qcount = qc;
-    wa.hmax = nullptr;
-    wa.pval = nullptr;
-    wa.hoff = nullptr;
-    wa.reduced = c->wide_reduced;
-    wa.N = (double)c->N;
-    wa.lambda = c->lambda;
-    wa.n = c->n;
-    wa.nv = nv;
-    wa.S = S;
-    wa.L = L;
-    const uint64_t blocks = (cnt + kBlock - 1) / kBlock;
-    const WideFn sf = wide_fn(L, ph);
-    const int lds = c->n * c->n * 8;
-    if (lds > 64 * 1024) ULG_HIP(c, hipFuncSetAttribute((const void *)sf, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    prof_begin_s(c, ph == 0 ? "score_wide_var0" : "score_wide_rest", st);
-    hipLaunchKernelGGL(sf, dim3((unsigned)blocks), dim3(kBlock), (size_t)lds, st, wa);
-    prof_end_s(c, st);
-    ULG_HIP(c, hipGetLastError());
-    unsigned long long qn = 0;
-    ULG_HIP(c, hipMemcpyAsync(&qn, qc, 8, hipMemcpyDeviceToHost, st));
-    ULG_HIP(c, hipStreamSynchronize(st));
-    if (qn == 0) return ULG_OK;
-    if (d_hmeta) {
-        // hi-cover tables of this launch's variables: [lvars][tile prefix][one
-        // block prefix per strided pass], one upload
-        std::vector<int> lv;
-        for (int i = 0; i < nv; ++i)
-            if (h_work[i + 1] > h_work[i] && hoff[i] != ~0ull) lv.push_back(i);
-        const int nl = (int)lv.size();
-        if (nl > 0) {
-            int maxm = 0;
-            for (int vi : lv) maxm = std::max(maxm, meta[vi * 4 + 1]);
-            const int passes = maxm > kHiTileBits ? (maxm - kHiTileBits + kHiGroup - 1) / kHiGroup : 0;
-            std::vector<int> hm((size_t)nl + (size_t)(nl + 1) * (1 + passes), 0);
-            for (int i = 0; i < nl; ++i) hm[i] = lv[i];
-            int *tp = hm.data() + nl;
-            for (int i = 0; i < nl; ++i) {
-                const int m = meta[lv[i] * 4 + 1];
-                tp[i + 1] = tp[i] + (m <= kHiTileBits ? 1 : 1 << (m - kHiTileBits));
-            }
-            for (int p = 0; p < passes; ++p) {
-                int *bp = tp + (size_t)(nl + 1) * (1 + p);
-                const int bit_lo = kHiTileBits + p * kHiGroup;
+    std::vector<int> hm;  // hi-cover launch metadata (kept until its copy ran)
+    uint64_t qn = 0;
+};
+
+int score_wide_groups(ulg_ctx *c, int L, int ph, std::vector<WideGroup> &gs, int nv, int S, int kmax,
+                      unsigned long long *errf, uint64_t slice, const std::vector<uint64_t> &hoff,
+                      const std::vector<int> &meta) {
+    const int ng = (int)gs.size();
+    const int q = ph == 0 ? L : L + 1;
+    if ((int)c->wide_host.size() < 2 * ng) {
+        if (c->wide_pinned) (void)hipHostFree(c->wide_pinned);
+        c->wide_pinned = nullptr;
+        ULG_HIP(c, hipHostMalloc((void **)&c->wide_pinned, sizeof(unsigned long long) * 2 * (size_t)ng,
+                                 hipHostMallocDefault));
+        c->wide_host.assign(2 * ng, 0);
+    }
+    unsigned long long *pin = c->wide_pinned;
+    // 1. scoring launches
+    for (int gi = 0; gi < ng; ++gi) {
+        WideGroup &G = gs[gi];
+        WideArgs &wa = G.wa;
+        wa.gram = c->gram.p;
+        wa.binom = c->d_binom64.p;
+        wa.cand = c->d_cand.p;
+        wa.meta = c->d_meta.p;
+        wa.tbl_off = c->d_tbl_off.p;
+        wa.work = G.d_work;
+        wa.table = c->table.p;
+        wa.queue = G.queue;
+        wa.qcount = G.qc;
+        wa.hmax = nullptr;
+        wa.pval = nullptr;
+        wa.hoff = nullptr;
+        wa.reduced = c->wide_reduced;
+        wa.N = (double)c->N;
+        wa.lambda = c->lambda;
+        wa.n = c->n;
+        wa.nv = nv;
+        wa.S = S;
+        wa.L = L;
+        const uint64_t blocks = (G.cnt + kBlock - 1) / kBlock;
+        const WideFn sf = wide_fn(L, ph);
+        const int lds = c->n * c->n * 8;
+        if (lds > 64 * 1024)
+            ULG_HIP(c, hipFuncSetAttribute((const void *)sf, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        prof_begin_s(c, ph == 0 ? "score_wide_var0" : "score_wide_rest", G.st);
+        hipLaunchKernelGGL(sf, dim3((unsigned)blocks), dim3(kBlock), (size_t)lds, G.st, wa);
+        prof_end_s(c, G.st);
+        ULG_HIP(c, hipGetLastError());
+        ULG_HIP(c, hipMemcpyAsync(pin + gi, G.qc, 8, hipMemcpyDeviceToHost, G.st));
+    }
+    for (int gi = 0; gi < ng; ++gi) {
+        ULG_HIP(c, hipStreamSynchronize(gs[gi].st));
+        gs[gi].qn = pin[gi];
+    }
+    // 2. hi-cover tables and walks
+    static const bool wstat = std::getenv("ULG_WALK_STATS") != nullptr;  // diagnostics: synchronises
+    const WideWalkFn wf = wide_walk_fn(L, ph);
+    const uint64_t wpl = q <= 6 ? 1ull : (1ull << (q - 6));
+    std::vector<uint64_t> budget(ng, 0);
+    for (int gi = 0; gi < ng; ++gi) {
+        WideGroup &G = gs[gi];
+        if (G.qn == 0) continue;
+        hipStream_t st = G.st;
+        WideArgs &wa = G.wa;
+        if (G.d_hmeta) {
+            // hi-cover tables of this launch's variables: [lvars][tile prefix][one
+            // block prefix per strided pass], one upload
+            std::vector<int> lv;
+            for (int i = 0; i < nv; ++i)
+                if (G.h_work[i + 1] > G.h_work[i] && hoff[i] != ~0ull) lv.push_back(i);
+            const int nl = (int)lv.size();
+            if (nl > 0) {
+                int maxm = 0;
+                for (int vi : lv) maxm = std::max(maxm, meta[vi * 4 + 1]);
+                const int passes = maxm > kHiTileBits ? (maxm - kHiTileBits + kHiGroup - 1) / kHiGroup : 0;
+                std::vector<int> &hm = G.hm;
+                hm.assign((size_t)nl + (size_t)(nl + 1) * (1 + passes), 0);
+                for (int i = 0; i < nl; ++i) hm[i] = lv[i];
+                int *tp = hm.data() + nl;
                 for (int i = 0; i < nl; ++i) {
                     const int m = meta[lv[i] * 4 + 1];
-                    const int G = std::min(kHiGroup, m - bit_lo);
-                    bp[i + 1] = bp[i] + (G > 0 ? (int)(((1ull << (m - G)) + 255) / 256) : 0);
+                    tp[i + 1] = tp[i] + (m <= kHiTileBits ? 1 : 1 << (m - kHiTileBits));
                 }
+                for (int pp = 0; pp < passes; ++pp) {
+                    int *bp = tp + (size_t)(nl + 1) * (1 + pp);
+                    const int bit_lo = kHiTileBits + pp * kHiGroup;
+                    for (int i = 0; i < nl; ++i) {
+                        const int m = meta[lv[i] * 4 + 1];
+                        const int Gb = std::min(kHiGroup, m - bit_lo);
+                        bp[i + 1] = bp[i] + (Gb > 0 ? (int)(((1ull << (m - Gb)) + 255) / 256) : 0);
+                    }
+                }
+                ULG_HIP(c, hipMemcpyAsync(G.d_hmeta, hm.data(), hm.size() * 4, hipMemcpyHostToDevice, st));
+                HiArgs ha{G.d_hmeta, G.d_hmeta + nl, nl, c->d_meta.p, c->d_tbl_off.p, c->table.p, c->d_binom64.p,
+                          c->d_hmax.p, c->d_hmax.p + c->hmax_half, c->d_hoff.p, S, L, kmax, 0};
+                prof_begin_s(c, "wide_hicover", st);
+                if (ph == 0) hikey_tile_kernel<0><<<tp[nl], 1024, 0, st>>>(ha);
+                else hikey_tile_kernel<1><<<tp[nl], 1024, 0, st>>>(ha);
+                for (int pp = 0; pp < passes; ++pp) {
+                    ha.prefix = G.d_hmeta + nl + (size_t)(nl + 1) * (1 + pp);
+                    ha.bit_lo = kHiTileBits + pp * kHiGroup;
+                    const int nb = tp[(size_t)(nl + 1) * (1 + pp) + nl];
+                    if (nb > 0) hikey_strided_kernel<<<nb, 256, 0, st>>>(ha);
+                }
+                prof_end_s(c, st);
+                ULG_HIP(c, hipGetLastError());
+                wa.hmax = c->d_hmax.p;
+                wa.pval = c->d_hmax.p + c->hmax_half;
+                wa.hoff = c->d_hoff.p;
             }
-            ULG_HIP(c, hipMemcpyAsync(d_hmeta, hm.data(), hm.size() * 4, hipMemcpyHostToDevice, st));
-            HiArgs ha{d_hmeta, d_hmeta + nl, nl, c->d_meta.p, c->d_tbl_off.p, c->table.p, c->d_binom64.p,
-                      c->d_hmax.p, c->d_hmax.p + c->hmax_half, c->d_hoff.p, S, L, kmax, 0};
-            prof_begin_s(c, "wide_hicover", st);
-            if (ph == 0) hikey_tile_kernel<0><<<tp[nl], 1024, 0, st>>>(ha);
-            else hikey_tile_kernel<1><<<tp[nl], 1024, 0, st>>>(ha);
-            for (int p = 0; p < passes; ++p) {
-                ha.prefix = d_hmeta + nl + (size_t)(nl + 1) * (1 + p);
-                ha.bit_lo = kHiTileBits + p * kHiGroup;
-                const int nb = tp[(size_t)(nl + 1) * (1 + p) + nl];
-                if (nb > 0) hikey_strided_kernel<<<nb, 256, 0, st>>>(ha);
-            }
+        }
+        // checked bitset: 2^q bits per walking set, q = L (P holds variable 0) or L + 1
+        const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(G.qn, slice / wpl));  // slice >= wpl
+        unsigned long long *ws = nullptr;
+        if (wstat) {
+            int rc2;
+            if ((rc2 = ensure(c, c->d_stats, 16))) return rc2;
+            ws = c->d_stats.p;
+            ULG_HIP(c, hipStreamSynchronize(st));
+            ULG_HIP(c, hipMemsetAsync(ws, 0, 32, st));
+        }
+        // long walks move to the LDS kernel (reduced walks with hi-cover tables only)
+        budget[gi] = (wa.hoff && wa.reduced && q <= kStragQMax && c->wide_lds) ? kStragBudget : 0;
+        uint64_t *sq = G.queue + 3 * G.qn;  // straggler queue after this launch's entries (the queue has room)
+        if (budget[gi]) ULG_HIP(c, hipMemsetAsync(G.scnt, 0, 8, st));
+        for (uint64_t base = 0; base < G.qn; base += per) {
+            const uint64_t k = std::min<uint64_t>(per, G.qn - base);
+            ULG_HIP(c, hipMemsetAsync(G.bits, 0, (size_t)(k * wpl * 8), st));
+            prof_begin_s(c, ph == 0 ? "walk_wide_var0" : "walk_wide_rest", st);
+            hipLaunchKernelGGL(wf, dim3((unsigned)((k + 63) / 64)), dim3(64), 0, st, wa, base, base + k, G.bits, wpl,
+                               errf, ws, budget[gi], sq, G.scnt);
             prof_end_s(c, st);
             ULG_HIP(c, hipGetLastError());
-            ULG_HIP(c, hipStreamSynchronize(st));  // hm must outlive its copy
-            wa.hmax = c->d_hmax.p;
-            wa.pval = c->d_hmax.p + c->hmax_half;
-            wa.hoff = c->d_hoff.p;
+        }
+        if (budget[gi]) ULG_HIP(c, hipMemcpyAsync(pin + ng + gi, G.scnt, 8, hipMemcpyDeviceToHost, st));
+        if (wstat) {
+            unsigned long long h[4];
+            ULG_HIP(c, hipMemcpyAsync(h, ws, 32, hipMemcpyDeviceToHost, st));
+            ULG_HIP(c, hipStreamSynchronize(st));
+            std::fprintf(stderr, "walk_stats L=%d phase=%d queued=%llu walks=%llu steps=%llu max=%llu over2^20=%llu\n",
+                         L, ph, (unsigned long long)G.qn, h[0], h[1], h[2], h[3]);
         }
     }
-    // checked bitset: 2^q bits per walking set, q = L (P holds variable 0) or L + 1
-    const int q = ph == 0 ? L : L + 1;
-    const uint64_t wpl = q <= 6 ? 1ull : (1ull << (q - 6));
-    const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(qn, slice / wpl));  // slice >= wpl
-    const WideWalkFn wf = wide_walk_fn(L, ph);
-    static const bool wstat = std::getenv("ULG_WALK_STATS") != nullptr;  // diagnostics: synchronises
-    unsigned long long *ws = nullptr;
-    if (wstat) {
-        int rc2;
-        if ((rc2 = ensure(c, c->d_stats, 16))) return rc2;
-        ws = c->d_stats.p;
-        ULG_HIP(c, hipMemsetAsync(ws, 0, 32, st));
-    }
-    // long walks move to the LDS kernel (reduced walks with hi-cover tables only)
-    const uint64_t budget = (wa.hoff && wa.reduced && q <= kStragQMax && c->wide_lds) ? kStragBudget : 0;
-    uint64_t *sq = queue + 3 * qn;  // straggler queue after this launch's entries (the queue has room)
-    if (budget) ULG_HIP(c, hipMemsetAsync(scnt, 0, 8, st));
-    for (uint64_t base = 0; base < qn; base += per) {
-        const uint64_t k = std::min<uint64_t>(per, qn - base);
-        ULG_HIP(c, hipMemsetAsync(bits, 0, (size_t)(k * wpl * 8), st));
-        prof_begin_s(c, ph == 0 ? "walk_wide_var0" : "walk_wide_rest", st);
-        hipLaunchKernelGGL(wf, dim3((unsigned)((k + 63) / 64)), dim3(64), 0, st, wa, base, base + k, bits, wpl, errf,
-                           ws, budget, sq, scnt);
-        prof_end_s(c, st);
+    // 3. the long walks, replayed in LDS
+    for (int gi = 0; gi < ng; ++gi) {
+        WideGroup &G = gs[gi];
+        if (G.qn == 0 || !budget[gi]) continue;
+        ULG_HIP(c, hipStreamSynchronize(G.st));
+        const unsigned long long sn = pin[ng + gi];
+        if (sn == 0) continue;
+        const size_t lds = (size_t)4 * ((size_t)1 << q) / 8 + kStragState;
+        const auto kf = ph == 0 ? walk_wide_lds_kernel<0> : walk_wide_lds_kernel<1>;
+        ULG_HIP(c, hipFuncSetAttribute((const void *)kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        prof_begin_s(c, "walk_wide_lds", G.st);
+        hipLaunchKernelGGL(kf, dim3((unsigned)sn), dim3(64), lds, G.st, G.wa, G.queue + 3 * G.qn);
+        prof_end_s(c, G.st);
         ULG_HIP(c, hipGetLastError());
     }
-    if (budget) {
-        unsigned long long sn = 0;
-        ULG_HIP(c, hipMemcpyAsync(&sn, scnt, 8, hipMemcpyDeviceToHost, st));
-        ULG_HIP(c, hipStreamSynchronize(st));
-        if (sn > 0) {
-            const size_t lds = (size_t)4 * ((size_t)1 << q) / 8 + kStragState;
-            const auto kf = ph == 0 ? walk_wide_lds_kernel<0> : walk_wide_lds_kernel<1>;
-            ULG_HIP(c, hipFuncSetAttribute((const void *)kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            prof_begin_s(c, "walk_wide_lds", st);
-            hipLaunchKernelGGL(kf, dim3((unsigned)sn), dim3(64), lds, st, wa, sq);
-            prof_end_s(c, st);
-            ULG_HIP(c, hipGetLastError());
-        }
-    }
-    if (wstat) {
-        unsigned long long h[4];
-        ULG_HIP(c, hipMemcpyAsync(h, ws, 32, hipMemcpyDeviceToHost, st));
-        ULG_HIP(c, hipStreamSynchronize(st));
-        std::fprintf(stderr, "walk_stats L=%d phase=%d queued=%llu walks=%llu steps=%llu max=%llu over2^20=%llu\n", L, ph,
-                     qn, h[0], h[1], h[2], h[3]);
-    }
+    // the hi-cover metadata vectors must outlive their copies
+    for (int gi = 0; gi < ng; ++gi)
+        if (!gs[gi].hm.empty()) ULG_HIP(c, hipStreamSynchronize(gs[gi].st));
     return ULG_OK;
 }
 
+}  // namespace
+
+namespace {
+uint64_t dbits(double x) {
+    uint64_t u;
+    std::memcpy(&u, &x, 8);
+    return u;
+}
 }  // namespace
 
 extern "C" {
@@ -2566,6 +2620,42 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     const auto t_call = std::chrono::steady_clock::now();
     c->out_of_time = 0;
     int done_L = kmax;
+    const int64_t nb = (int64_t)((total_slots + kSlotsPerBlock - 1) / kSlotsPerBlock);
+    if ((rc = ensure(c, c->d_blk, (size_t)nb + 1))) return rc;
+    // The launch sequence from here to set_total_kernel has no host sync when
+    // every layer is unrolled and no budget / diagnostic is on, and it is the
+    // same on every call with the same variables, limits and buffers: it is
+    // captured once into a hipGraph (all stream groups, the fork and join
+    // events, the profiling events) and replayed, which removes the host
+    // launch path of ~40 kernels per call (score_graph, default on).
+    const bool use_graph =
+        c->score_graph && !c->prof && kmax <= kMaxL && c->time_limit_ms == 0 && !wck && !(variant & 8);
+    std::vector<uint64_t> gkey;
+    if (use_graph) {
+        gkey.assign({(uint64_t)nv, (uint64_t)max_parents, (uint64_t)variant, (uint64_t)G, (uint64_t)Ls,
+                     (uint64_t)c->score_xcd, (uint64_t)n, (uint64_t)c->N, dbits(c->lambda), (uint64_t)c->prof,
+                     (uint64_t)(uintptr_t)c->table.p, (uint64_t)(uintptr_t)c->d_work.p,
+                     (uint64_t)(uintptr_t)c->d_workg.p, (uint64_t)(uintptr_t)c->d_queue.p,
+                     (uint64_t)(uintptr_t)c->d_qcount.p, (uint64_t)(uintptr_t)c->d_cand.p,
+                     (uint64_t)(uintptr_t)c->d_meta.p, (uint64_t)(uintptr_t)c->d_tbl_off.p,
+                     (uint64_t)(uintptr_t)c->out_sets.p, (uint64_t)(uintptr_t)c->out_scores.p,
+                     (uint64_t)(uintptr_t)c->out_offsets.p, (uint64_t)(uintptr_t)c->d_blk.p,
+                     (uint64_t)(uintptr_t)c->gram.p, (uint64_t)(uintptr_t)c->d_binom.p,
+                     (uint64_t)(uintptr_t)c->d_binom64.p, (uint64_t)total_slots});
+        for (int i = 0; i < nv; ++i) gkey.push_back((uint64_t)vars[i]);
+        for (int i = 0; i < nv; ++i) gkey.push_back(candidates[i]);
+        for (const std::string &nm : c->prof_only) gkey.push_back(std::hash<std::string>{}(nm));
+        if (c->gexec && gkey == c->gkey) {
+            c->completed_layer = kmax;
+            ULG_HIP(c, hipGraphLaunch(c->gexec, c->stream));
+            for (const ProfRec &r : c->gprof) c->pending.push_back(r);
+            goto launched;
+        }
+        graph_reset(c);
+        ULG_HIP(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed));
+    }
+    {
+    const size_t pend0 = c->pending.size();
     for (int L = 1; L <= kmax; ++L) {
         for (int ph = 0; ph < 2; ++ph) {
             if (L <= Ls) {
@@ -2593,6 +2683,7 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
                 for (int g = 1; g < G; ++g) ULG_HIP(c, hipStreamWaitEvent(gst[g], c->sync_events[0], 0));
                 forked = true;
             }
+            std::vector<WideGroup> wide;  // a wide layer: every group's part, staged together
             for (int g = 0; g < G; ++g) {
                 const size_t wo = (size_t)g * (G > 1 ? wstride : 0) + ((size_t)L * 2 + ph) * (nv + 1);
                 const uint64_t cnt = h_wk[wo + nv];
@@ -2605,15 +2696,17 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
                 const uint64_t blocks = (cnt + kBlock - 1) / kBlock;
                 if (blocks > 0x7fffffffull) return set_err(c, ULG_ERR_UNSUPPORTED, "ulg_cbic_score: layer too large");
                 if (L > kMaxL) {
-                    if ((rc = score_wide_layer(c, L, ph, st, d_wk + wo, h_wk.data() + wo, cnt, nv, S, kmax,
-                                               c->d_wqueue.p + g * wqwords,
-                                               c->d_qcount.p + (size_t)g * 2 * (kmax + 1) + (L * 2 + ph),
-                                               c->d_qcount.p + nqc - 1, c->d_wbits.p + (size_t)g * wslice,
-                                               wslice,
-                                               hoff.empty() ? nullptr
-                                                            : c->d_hmeta.p + (size_t)g * (nv + (size_t)(nv + 1) * 8),
-                                               hoff, meta, c->d_scount.p + g)))
-                        return rc;
+                    WideGroup wg;
+                    wg.st = st;
+                    wg.d_work = d_wk + wo;
+                    wg.h_work = h_wk.data() + wo;
+                    wg.cnt = cnt;
+                    wg.queue = c->d_wqueue.p + g * wqwords;
+                    wg.qc = c->d_qcount.p + (size_t)g * 2 * (kmax + 1) + (L * 2 + ph);
+                    wg.scnt = c->d_scount.p + g;
+                    wg.bits = c->d_wbits.p + (size_t)g * wslice;
+                    wg.d_hmeta = hoff.empty() ? nullptr : c->d_hmeta.p + (size_t)g * (nv + (size_t)(nv + 1) * 8);
+                    wide.push_back(std::move(wg));
                     continue;
                 }
                 const LdsLayout lay = lds_layout(n, nv, S, L, variant);
@@ -2706,6 +2799,9 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
                     }
                 }
             }
+            if (!wide.empty() &&
+                (rc = score_wide_groups(c, L, ph, wide, nv, S, kmax, c->d_qcount.p + nqc - 1, wslice, hoff, meta)))
+                return rc;
         }
         if (c->time_limit_ms > 0 && L < kmax) {
             for (int g = 0; g < (forked ? G : 1); ++g) ULG_HIP(c, hipStreamSynchronize(gst[g]));
@@ -2736,8 +2832,6 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     }
     c->completed_layer = done_L;
     // compaction
-    const int64_t nb = (int64_t)((total_slots + kSlotsPerBlock - 1) / kSlotsPerBlock);
-    if ((rc = ensure(c, c->d_blk, (size_t)nb + 1))) return rc;
     prof_begin(c, "count_stored");
     count_kernel<<<(unsigned)nb, kBlock, 0, c->stream>>>(c->table.p, total_slots, c->d_blk.p);
     prof_end(c);
@@ -2763,6 +2857,21 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     prof_end(c);
     set_total_kernel<<<1, 1, 0, c->stream>>>(c->d_blk.p, nb, nv, c->out_offsets.p);
     ULG_HIP(c, hipGetLastError());
+    if (use_graph) {
+        hipGraph_t graph = nullptr;
+        ULG_HIP(c, hipStreamEndCapture(c->stream, &graph));
+        c->graph = graph;
+        ULG_HIP(c, hipGraphInstantiate(&c->gexec, graph, nullptr, nullptr, 0));
+        c->gkey = gkey;
+        // the profiling events recorded inside the graph belong to it now
+        c->gprof.assign(c->pending.begin() + (std::ptrdiff_t)pend0, c->pending.end());
+        for (ProfRec &r : c->gprof) r.graph = true;
+        c->pending.resize(pend0);
+        ULG_HIP(c, hipGraphLaunch(c->gexec, c->stream));
+        for (const ProfRec &r : c->gprof) c->pending.push_back(r);
+    }
+    }
+launched:
     uint64_t stored = 0;
     unsigned long long wide_err = 0;
     ULG_HIP(c, hipMemcpyAsync(&stored, c->d_blk.p + nb, 8, hipMemcpyDeviceToHost, c->stream));

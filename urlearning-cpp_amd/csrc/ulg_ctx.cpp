@@ -74,10 +74,26 @@ void prof_collect(ulg_ctx *c) {
         float ms = 0.f;
         if (hipEventSynchronize(r.stop) == hipSuccess && hipEventElapsedTime(&ms, r.start, r.stop) == hipSuccess)
             c->prof_ms[r.name].push_back(ms);
+        if (r.graph) continue;  // the graph records these again on every replay
         c->event_pool.push_back(r.start);
         c->event_pool.push_back(r.stop);
     }
     c->pending.clear();
+}
+
+void graph_reset(ulg_ctx *c) {
+    (void)hipStreamSynchronize(c->stream);
+    prof_collect(c);
+    if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
+    if (c->graph) (void)hipGraphDestroy(c->graph);
+    c->gexec = nullptr;
+    c->graph = nullptr;
+    c->gkey.clear();
+    for (const ProfRec &r : c->gprof) {
+        c->event_pool.push_back(r.start);
+        c->event_pool.push_back(r.stop);
+    }
+    c->gprof.clear();
 }
 
 }  // namespace ulg
@@ -122,7 +138,9 @@ void ulg_destroy(ulg_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    prof_collect(c);
+    graph_reset(c);
+    if (c->wide_pinned) (void)hipHostFree(c->wide_pinned);
+    c->wide_pinned = nullptr;
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
     c->event_pool.clear();
     for (hipStream_t s : c->aux_streams) (void)hipStreamDestroy(s);
@@ -178,6 +196,12 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
     if (std::strcmp(name, "sweep_xcd") == 0) {
         if (value < 0 || value > 1) return set_err(c, ULG_ERR_ARG, "sweep_xcd must be 0 or 1");
         c->sweep_xcd = (int)value;
+        return ULG_OK;
+    }
+    if (std::strcmp(name, "score_graph") == 0) {
+        if (value < 0 || value > 1) return set_err(c, ULG_ERR_ARG, "score_graph must be 0 or 1");
+        c->score_graph = (int)value;
+        if (!value) graph_reset(c);
         return ULG_OK;
     }
     if (std::strcmp(name, "score_xcd") == 0) {

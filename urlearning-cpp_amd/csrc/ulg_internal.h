@@ -33,6 +33,7 @@ struct PssState;
 struct ProfRec {
     std::string name;
     hipEvent_t start, stop;
+    bool graph = false;  // recorded by a captured graph (its events stay with the graph)
 };
 
 // Host copy of what was last uploaded into a device buffer: repeated calls
@@ -81,6 +82,11 @@ struct ulg_ctx {
     int wide_reduced = 1;          // wide walks: skip the recursion's no-op re-tests
     int wide_lds = 1;              // wide walks: long ones replayed with their bitsets in LDS
     int score_xcd = 1;             // scoring kernels: contiguous runs of sets per XCD
+    int score_graph = 1;           // scoring call: replay the captured launch sequence
+    hipGraph_t graph = nullptr;    // the captured scoring launches, its instance, its key
+    hipGraphExec_t gexec = nullptr;
+    std::vector<uint64_t> gkey;
+    std::vector<ulg::ProfRec> gprof;  // profiling events inside the graph
     int sweep_xcd = 1;             // GPU sweep launches: contiguous runs of nodes per XCD           // GPU search: successor costs in the sweep's (layer, colex) order
     ulg::DevBuf<float> table;
     ulg::DevBuf<uint64_t> d_tbl_off, d_work, d_blk;
@@ -119,6 +125,8 @@ struct ulg_ctx {
     ulg::DevBuf<uint64_t> d_hoff;   // [nv] table offsets, ~0 = no table
     ulg::DevBuf<int> d_hmeta;       // per stream group: launch variables and tile / block prefixes
     ulg::DevBuf<unsigned long long> d_scount;  // per stream group: long wide walks handed to the LDS kernel
+    unsigned long long *wide_pinned = nullptr;  // pinned queue / long-walk counts of the wide stages
+    std::vector<unsigned long long> wide_host;
     std::map<std::string, std::vector<double>> prof_ms;
 };
 
@@ -175,6 +183,7 @@ void prof_end(ulg_ctx *c);
 void prof_begin_s(ulg_ctx *c, const char *name, hipStream_t stream);
 void prof_end_s(ulg_ctx *c, hipStream_t stream);
 void prof_collect(ulg_ctx *c);  // after a stream sync
+void graph_reset(ulg_ctx *c);   // drop the captured scoring graph (cbic.hip)
 void pss_release(ulg_ctx *c);    // pss.hip
 
 // binomial table C(a, b), a < 64, b < kBinomK, clamped to uint32
