@@ -68,6 +68,25 @@ def test_wide_layers_hepatitis_prefix_match_oracle(ulg_ctx, oracle_built, lam):
     _compare_lists(*o, *g, variables, ctx=f"hepatitis[:, :13] lam={lam}")
 
 
+@pytest.mark.parametrize("lam", [0.5, 2.0])
+def test_wide_lds_replay_every_walk_hepatitis_prefix_match_oracle(ulg_ctx, oracle_built, lam):
+    """wide_lds = 2 sends every wide walk to walk_wide_lds_kernel (the mask-frame
+    replay with skip / hi bitsets), not only the long ones: its lists must
+    equal the oracle's on the walk-heavy hepatitis prefix."""
+    X = load_csv_ascii(os.path.join(GOLDEN, "hepatitis.clean.csv"))[:, :13]
+    n = X.shape[1]
+    variables = list(range(n))
+    cands = [(1 << n) - 1] * n
+    ulg_ctx.load(X, lam)
+    try:
+        ulg_ctx.set_option("wide_lds", 2)
+        g = ulg_ctx.score_all(variables, cands, n - 1)
+    finally:
+        ulg_ctx.set_option("wide_lds", 1)
+    o = _oracle_lists(oracle_built, X, lam, variables, cands, n - 1)
+    _compare_lists(*o, *g, variables, ctx=f"hepatitis[:, :13] lam={lam} wide_lds=2")
+
+
 def test_c1_hepatitis_default_parent_limit_matches_digest(ulg_ctx):
     """Config C1 (BASELINE.json configs[0]) on the GPU: all 20 variables, full
     skeleton, -p default n - 1 = 19, against the oracle's digest."""
@@ -98,8 +117,8 @@ def test_c1_hepatitis_default_parent_limit_matches_digest(ulg_ctx):
 def test_wide_hicover_prune_identical_lists(ulg_ctx):
     """ulg_set_option("wide_prune"): the walks skip absent nodes below which no
     present key reaches -ts; "wide_reduced": they skip the recursion's no-op
-    re-tests; "wide_lds": walks over 2^13 steps are replayed with their bitsets
-    in LDS.  The stored lists with and without either are identical bit for
+    re-tests; "wide_lds": walks over 2^13 steps (2: over 1 step, so every
+    walk) are replayed by walk_wide_lds_kernel.  The stored lists with and without either are identical bit for
     bit, on C4's (n=30, N=100k, MMPC, -p = n-1) variables
     whose unpruned walks finish in well under a second each."""
     import ulg
@@ -112,7 +131,7 @@ def test_wide_hicover_prune_identical_lists(ulg_ctx):
     assert all(9 <= bin(cands[v] & ~(1 << v)).count("1") <= 12 for v in vs)
     out = []
     try:
-        for prune, reduced, lds in ((0, 0, 0), (1, 0, 0), (0, 1, 0), (1, 1, 0), (1, 1, 1)):
+        for prune, reduced, lds in ((0, 0, 0), (1, 0, 0), (0, 1, 0), (1, 1, 0), (1, 1, 1), (1, 1, 2)):
             ulg_ctx.set_option("wide_prune", prune)
             ulg_ctx.set_option("wide_reduced", reduced)
             ulg_ctx.set_option("wide_lds", lds)
@@ -165,3 +184,15 @@ def test_c1_hepatitis_reference_defaults_lambda_half(ulg_ctx):
             assert int(s[idx]) == ps
             assert abs(float(sc[idx]) - pscore) <= REL_TOL * max(abs(pscore), 1.0), (v, ps, float(sc[idx]), pscore)
     assert deeper > 0  # layers above K stored sets too (checked only through the GPU's own walk forms)
+    # all 19 layers against the direct walk form (walk_wide_kernel, no LDS
+    # replay), whose digest tests/golden/c1_hepatitis_default_walk_digest.json holds
+    with open(os.path.join(GOLDEN, "c1_hepatitis_default_walk_digest.json")) as f:
+        wd = json.load(f)
+    assert wd["lambda"] == fx["lambda"] and wd["max_parents_run"] == fx["max_parents_run"]
+    for v in range(n):
+        d = wd["per_variable"][v]
+        s = np.ascontiguousarray(sets[offs[v]:offs[v + 1]], dtype=np.uint64)
+        sc = np.ascontiguousarray(scores[offs[v]:offs[v + 1]])
+        assert len(s) == d["count"], v
+        assert hashlib.sha256(s.tobytes()).hexdigest() == d["sets_sha256"], v
+        assert hashlib.sha256(sc.tobytes()).hexdigest() == d["scores_sha256"], v

@@ -1646,30 +1646,52 @@ WideWalkFn wide_walk_fn(int L, int phase) {
 
 // ---- long wide walks in LDS -----------------------------------------------
 // A wide walk is one lane's sequential DFS; the few long ones set a layer's
-// time (C4: 0.6 M steps for one set at L = 17), and in walk_wide_kernel every
-// step waits on scratch memory and global bitsets (~1 us).  Walks over
-// kStragBudget steps (only where q = |local bits| <= kStragQMax and the
-// hi-cover tables exist) are re-queued and replayed here from the start, one
-// workgroup per set: the 64 lanes first lay out, over the 2^q local subsets,
-// bitsets of `present`, `hi` (present and >= -ts) and `cover` (some key >= -ts
-// among its subsets and variable 0) from pval / hmax, then lane 0 runs the
-// same reduced walk with `checked`, those bitsets and its frame stack in LDS.
-constexpr int kStragQMax = 18;                 // 4 bitsets of 2^18 bits = 128 KiB of LDS
-constexpr uint64_t kStragBudget = 1ull << 13;  // steps before a walk moves here
-constexpr int kStragState = 32 * 4 + 7 * 32 + 32 * 33 / 2 + 16;  // Ts, 6 x u8 frames, pvs, lc
+// time (C1 at the reference's default lambda 0.5: single walks of 5-19 M
+// steps at L = 18, 19), and in walk_wide_kernel every step waits on scratch
+// memory and global bitsets (~1 us).  Walks over kStragBudget steps (only
+// where q = |local bits| <= kStragQMax and the hi-cover tables exist) are
+// re-queued and replayed here from the start, one workgroup per set.
+//
+// Fill: the workgroup lays out, over the 2^q local subsets, two bitsets from
+// pval / hmax: `skip` (present below -ts, or absent with no key >= -ts among
+// its subsets and variable 0: a test of it changes nothing but `checked`,
+// which it would never consult again) and `hi` (present and >= -ts: the walk
+// stops there).  A test is then: skip bit set (or checked) -> next; hi bit set
+// -> dominated; otherwise expand.  `checked` merges into `skip`: checked nodes
+// are expanded ones, never hi, and the empty set starts checked.
+//
+// Walk (lane 0): the reduced walk of walk_wide_kernel with every parent-vector
+// list held as a bit mask.  A list is its real entries in increasing local-bit
+// order followed by zero padding (the root list is P's bits; an expansion of
+// T2 = T ^ {x} appends the caller's entries != x in order, so order is kept,
+// and zeros appended from the padding read like padding), so a frame is: node
+// N, removed entry x, the caller's list (remaining mask `rem`, remaining zeros
+// `zr`), the appended mask B, the call count js, and whether the current call
+// still owes its position-1 test (call 1 tests positions 0 and 1, call j >= 2
+// position j - 1 = the entry it appended).  N is checked after each call of
+// its expansion returns (BIC_OLS.cpp:234 recursion).  Wave 0 runs
+// the walk with its lanes reading a node's q neighbour bits at once, so a
+// test is a register bit test; frames are 32 B in LDS, pushed per expansion.
+constexpr int kStragQMax = 20;                 // skip bitset 2^20 bits = 128 KiB of LDS
+constexpr int kStragHiLdsQ = 19;               // hi bitset in LDS up to here, else in global scratch
+constexpr uint64_t kStragBudget = 1ull << 13;  // steps in walk_wide_kernel before a walk moves here
+constexpr int kStragThreads = 256;             // fill threads; lane 0 walks
+constexpr int kStragDepth = 24;
+constexpr int kStragState = kStragDepth * 32 + 32;  // frames (2 x 16 B), lc
+constexpr uint64_t kStragIterCap = 1ull << 32;
 
-template <int PHASE>
-__global__ void __launch_bounds__(64) walk_wide_lds_kernel(WideArgs a, const uint64_t *sq) {
+template <int PHASE, bool HI_LDS>
+__global__ void __launch_bounds__(kStragThreads) walk_wide_lds_kernel(WideArgs a, const uint64_t *sq,
+                                                                      uint64_t *hig, unsigned long long *err,
+                                                                      unsigned long long *wstats) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int L = a.L;
     const int q = PHASE == 0 ? L : L + 1;
     const uint32_t nw = (1u << q) >> 6;
-    uint64_t *chk = reinterpret_cast<uint64_t *>(smem);
-    uint64_t *pres = chk + nw, *hib = pres + nw, *cov = hib + nw;
-    uint32_t *Ts = reinterpret_cast<uint32_t *>(cov + nw);
-    uint8_t *idxs = reinterpret_cast<uint8_t *>(Ts + 32);
-    uint8_t *is = idxs + 32, *js = is + 32, *us = js + 32, *inner = us + 32, *ends = inner + 32, *lc = ends + 32;
-    uint8_t *pvs = lc + 32;
+    uint64_t *skip = reinterpret_cast<uint64_t *>(smem);
+    uint64_t *hib = HI_LDS ? skip + nw : hig + (uint64_t)blockIdx.x * nw;
+    uint4 *frames = reinterpret_cast<uint4 *>(skip + (HI_LDS ? 2 * nw : nw));
+    uint8_t *lc = reinterpret_cast<uint8_t *>(frames + kStragDepth);
     const uint64_t *e = sq + 3 * (uint64_t)blockIdx.x;
     const uint64_t slot = e[0], cm = e[1];
     const int vi = (int)(uint32_t)e[2];
@@ -1678,6 +1700,7 @@ __global__ void __launch_bounds__(64) walk_wide_lds_kernel(WideArgs a, const uin
     const bool z = a.meta[vi * 4 + 2] != 0;
     const uint64_t zb = z ? 1ull : 0ull;
     const uint64_t ho = a.hoff[vi];
+    const uint64_t tk0 = wstats ? wall_clock64() : 0;
     if (threadIdx.x == 0) {
         uint64_t rem = cm;
         const int first = PHASE == 0 ? 0 : 1;
@@ -1688,92 +1711,199 @@ __global__ void __launch_bounds__(64) walk_wide_lds_kernel(WideArgs a, const uin
         }
     }
     __syncthreads();
-    for (uint32_t w = threadIdx.x; w < nw; w += 64) {
-        uint64_t pw = 0, hw = 0, cw = 0;
+    for (uint32_t w = threadIdx.x; w < nw; w += kStragThreads) {
+        uint64_t sw = 0, hw = 0;
+        uint64_t Xw = 0;  // compact mask of the word's high local bits
+        for (uint32_t y = (w << 6); y; y &= y - 1) Xw |= 1ull << lc[__builtin_ctz(y)];
         for (int b = 0; b < 64; ++b) {
             const uint32_t t = (w << 6) | (uint32_t)b;
-            uint64_t X = (t & 1u) ? zb : 0ull;  // local bit 0 = variable 0
-            for (uint32_t y = t & ~1u; y; y &= y - 1) X |= 1ull << lc[__builtin_ctz(y)];
+            uint64_t X = Xw | ((t & 1u) ? zb : 0ull);  // local bit 0 = variable 0
+            for (uint32_t y = (uint32_t)b & ~1u; y; y &= y - 1) X |= 1ull << lc[__builtin_ctz(y)];
+            bool pres = false, hi = false;
             if (!(PHASE == 1 && (t & 1u) && !z)) {
                 const float val = a.pval[ho + X];
                 if (fbits(val) != kAbsentBits) {
-                    pw |= 1ull << b;
-                    if (val >= thr) hw |= 1ull << b;
+                    pres = true;
+                    hi = val >= thr;
                 }
             }
-            if (a.hmax[ho + (X | zb)] >= thr) cw |= 1ull << b;
+            const bool sk = t == 0 || (pres ? !hi : !(a.hmax[ho + (X | zb)] >= thr));
+            if (sk) sw |= 1ull << b;
+            if (hi && t != 0) hw |= 1ull << b;
         }
-        pres[w] = pw;
+        skip[w] = sw;
         hib[w] = hw;
-        cov[w] = cw;
-        chk[w] = 0;
     }
     __syncthreads();
-    if (threadIdx.x != 0) return;
+    if (threadIdx.x >= 64) return;
+    // wave 0 walks, every lane in step (the walk state is wave-uniform); the
+    // lanes only split up to read a node's neighbour bits: bit l of sm / hm is
+    // the skip / hi bit of N ^ {l}.  Within one expansion only its children's
+    // subtrees change `skip` (N's own mark is not a neighbour of N), so sm is
+    // re-read after each child returns and every test is a register bit test.
+    const int lane = threadIdx.x;
+    const uint64_t tk1 = wstats ? wall_clock64() : 0;
     auto bit = [](const uint64_t *v, uint32_t t) -> bool { return (v[t >> 6] >> (t & 63)) & 1ull; };
-    chk[0] |= 1ull;  // checked.insert(empty_set)
-    for (int i = 0; i < L; ++i) pvs[i] = (uint8_t)(i + (PHASE == 0 ? 0 : 1));
-    int d = 0;
-    Ts[0] = PHASE == 0 ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
-    idxs[0] = 0;
-    ends[0] = (uint8_t)L;
-    inner[0] = 0;
-    bool dom = false;
+    auto rfl = [](uint32_t v) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+    // lanes >= q read a valid word too, so both loads issue back to back
+    const uint32_t lbit = 1u << (lane < q ? lane : 0);
+    auto nbr = [&](uint32_t Nn, uint32_t &sm_, uint32_t &hm_) {
+        const uint32_t t = Nn ^ lbit;
+        const uint64_t sw = skip[t >> 6], hw = hib[t >> 6];
+        sm_ = (uint32_t)__ballot((int)(((sw >> (t & 63)) & 1ull) | (lane >= q)));
+        hm_ = (uint32_t)__ballot((int)(((hw >> (t & 63)) & 1ull) & (lane < q)));
+    };
+    uint4 *fext = reinterpret_cast<uint4 *>(lc + 32);  // per frame: hm, sm
+    const uint32_t P = PHASE == 0 ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
+    uint32_t N = P, rem = P, B = 0, sm, hm;
+    nbr(N, sm, hm);
+    int x = 31, zr = 0, js = 0, d = 0, mS = L;
+    bool pend = false, incall = false, dom = false;
+    uint64_t it = 0;
     while (true) {
-        const int mm = L - d;
-        const int po = d * L - d * (d - 1) / 2;
-        if (!inner[d]) {
-            if (idxs[d] == ends[d]) {
-                if (d == 0) break;
-                --d;
-                const uint32_t c = Ts[d + 1];
-                chk[c >> 6] |= 1ull << (c & 63);
-                continue;
+        if (++it > kStragIterCap) {
+            if (lane == 0) atomicOr(err, 1ull);
+            break;
+        }
+        int y;
+        if (pend) {  // call 1's position-1 test: the zero padding, variable 0
+            pend = false;
+            y = 0;
+        } else {
+            if (incall) {  // the call returned: checked.insert(N)
+                if (lane == 0) atomicOr(&skip[N >> 6], 1ull << (N & 63));
+                incall = false;
             }
-            const uint8_t u = pvs[po + idxs[d]];
-            const uint32_t T2 = Ts[d] ^ (1u << u);
-            if (bit(chk, T2)) {
-                ++idxs[d];
-                continue;
-            }
-            if (bit(pres, T2)) {
-                if (bit(hib, T2)) {
-                    dom = true;
-                    break;
+            // Next test that is not a no-op.  A test whose node has its skip
+            // bit set changes nothing, so after call 1 (N is checked from then
+            // on) a run of such calls only appends its entries to B.
+            const uint32_t xb = x < 32 ? 1u << x : 0u;
+            const uint32_t cand = rem & ~xb;  // real entries that make calls
+            bool found = false;
+            if (d == 0) {  // the root call: P's entries, no appends
+                const uint32_t ev = rem & ~sm;
+                if (ev) {
+                    y = __builtin_ctz(ev);
+                    rem &= ~((2u << y) - 1u);
+                    found = true;
                 }
-                ++idxs[d];
+            } else if (js == 0) {  // call 1, with its position-1 test
+                if (cand) {
+                    y = __builtin_ctz(cand);
+                    rem &= ~((2u << y) - 1u);
+                    B |= 1u << y;
+                    found = true;
+                } else if (zr && x != 0) {  // the first entry is padding
+                    --zr;
+                    y = 0;
+                    found = true;
+                }
+                if (found) {
+                    js = 1;
+                    incall = true;
+                    pend = mS - 1 >= 2;
+                }
+            } else {
+                const uint32_t ev = cand & ~sm;
+                if (ev) {
+                    y = __builtin_ctz(ev);
+                    const uint32_t run = cand & ((2u << y) - 1u);  // skipped calls + this one
+                    B |= run;
+                    js += __popc(run);
+                    rem &= ~((2u << y) - 1u);
+                    incall = true;
+                    found = true;
+                } else {
+                    B |= cand;  // the rest of the real entries: no-op calls
+                    js += __popc(cand);
+                    rem = 0;
+                    if (zr && x != 0) {  // padding entries: each a call testing N ^ {0}
+                        if (sm & 1u) {
+                            js += zr;
+                            zr = 0;
+                        } else {
+                            --zr;
+                            ++js;
+                            y = 0;
+                            incall = true;
+                            found = true;
+                        }
+                    }
+                }
+            }
+            if (!found) {  // the expansion (or the root call) is done
+                if (d == 0) break;
+                // Back in the caller's frame, whose neighbour bits the subtree of
+                // N = caller ^ {x} changed only at N itself (marked iff it made
+                // a call) when x != 0: x never re-enters a list below it, so
+                // every node of the subtree differs from the caller in bit x.
+                // Variable 0 re-enters as padding: then read them again.
+                const int cx = x;
+                const bool cmarked = js > 0;
+                --d;
+                const uint4 f = frames[d];
+                const uint4 g = fext[d];
+                N = rfl(f.x);
+                rem = rfl(f.y);
+                B = rfl(f.z);
+                const uint32_t w = rfl(f.w);
+                hm = rfl(g.x);
+                sm = rfl(g.y);
+                x = (int)(w & 31u);
+                zr = (int)((w >> 5) & 31u);
+                js = (int)((w >> 10) & 31u);
+                pend = (w >> 15) & 1u;
+                incall = (w >> 16) & 1u;
+                mS = d == 0 ? L : L - d + 1;
+                if (cx != 0) {
+                    if (cmarked) sm |= 1u << cx;
+                } else {
+                    uint32_t h2;
+                    nbr(N, sm, h2);
+                }
                 continue;
             }
-            if (!bit(cov, T2)) {
-                chk[T2 >> 6] |= 1ull << (T2 & 63);
-                ++idxs[d];
-                continue;
-            }
-            inner[d] = 1;
-            is[d] = 0;
-            js[d] = 0;
-            us[d] = u;
-            for (int k = 0; k < mm - 1; ++k) pvs[po + mm + k] = 0;
-            continue;
         }
-        if (is[d] == mm) {
-            inner[d] = 0;
-            ++idxs[d];
-            continue;
+        if ((sm >> y) & 1u) continue;
+        if ((hm >> y) & 1u) {
+            dom = true;
+            break;
         }
-        const uint8_t pi = pvs[po + is[d]];
-        ++is[d];
-        if (pi == us[d]) continue;
-        pvs[po + mm + js[d]] = pi;
-        ++js[d];
-        Ts[d + 1] = Ts[d] ^ (1u << us[d]);
-        const int j = js[d];
-        idxs[d + 1] = (uint8_t)(j == 1 ? 0 : j - 1);
-        ends[d + 1] = (uint8_t)(j == 1 ? (mm - 1 < 2 ? mm - 1 : 2) : j);
-        inner[d + 1] = 0;
+        // expand N ^ {y} with the current call's list (root: P's bits; else B_j)
+        const uint32_t Sc = d == 0 ? P : B;
+        const int mc = d == 0 ? L : mS - 1;
+        if (d + 1 >= kStragDepth || mc < __popc(Sc)) {  // cannot happen: the list holds its entries
+            if (lane == 0) atomicOr(err, 1ull);
+            break;
+        }
+        if (lane == 0) {
+            frames[d] = make_uint4(N, rem, B,
+                                   (uint32_t)x | ((uint32_t)zr << 5) | ((uint32_t)js << 10) |
+                                       ((uint32_t)pend << 15) | ((uint32_t)incall << 16));
+            fext[d] = make_uint4(hm, sm, 0u, 0u);
+        }
         ++d;
+        N ^= 1u << y;
+        x = y;
+        rem = Sc;
+        zr = mc - __popc(Sc);
+        B = 0;
+        js = 0;
+        pend = false;
+        incall = false;
+        mS = mc;
+        nbr(N, sm, hm);
     }
+    if (lane != 0) return;
     a.table[slot] = dom ? absent_f() : -ts;
+    if (wstats) {  // ULG_WALK_STATS: replays, iterations, max iterations, max fill / walk ticks
+        const uint64_t tk2 = wall_clock64();
+        atomicAdd(&wstats[4], 1ull);
+        atomicAdd(&wstats[5], (unsigned long long)it);
+        atomicMax(&wstats[6], (unsigned long long)it);
+        atomicMax(&wstats[7], (unsigned long long)(tk1 - tk0));
+        atomicMax(&wstats[8], (unsigned long long)(tk2 - tk1));
+    }
 }
 
 // ---- hi-cover tables for the wide walks ---------------------------------
@@ -2325,12 +2455,15 @@ int score_wide_groups(ulg_ctx *c, int L, int ph, std::vector<WideGroup> &gs, int
             if ((rc2 = ensure(c, c->d_stats, 16))) return rc2;
             ws = c->d_stats.p;
             ULG_HIP(c, hipStreamSynchronize(st));
-            ULG_HIP(c, hipMemsetAsync(ws, 0, 32, st));
+            ULG_HIP(c, hipMemsetAsync(ws, 0, 64, st));
         }
         // long walks move to the LDS kernel (reduced walks with hi-cover tables only)
-        budget[gi] = (wa.hoff && wa.reduced && q <= kStragQMax && c->wide_lds) ? kStragBudget : 0;
+        budget[gi] = (wa.hoff && wa.reduced && q <= kStragQMax && c->wide_lds)
+                         ? (c->wide_lds == 2 ? 1 : kStragBudget)
+                         : 0;
         uint64_t *sq = G.queue + 3 * G.qn;  // straggler queue after this launch's entries (the queue has room)
         if (budget[gi]) ULG_HIP(c, hipMemsetAsync(G.scnt, 0, 8, st));
+        const auto tw0 = std::chrono::steady_clock::now();
         for (uint64_t base = 0; base < G.qn; base += per) {
             const uint64_t k = std::min<uint64_t>(per, G.qn - base);
             ULG_HIP(c, hipMemsetAsync(G.bits, 0, (size_t)(k * wpl * 8), st));
@@ -2345,8 +2478,11 @@ int score_wide_groups(ulg_ctx *c, int L, int ph, std::vector<WideGroup> &gs, int
             unsigned long long h[4];
             ULG_HIP(c, hipMemcpyAsync(h, ws, 32, hipMemcpyDeviceToHost, st));
             ULG_HIP(c, hipStreamSynchronize(st));
-            std::fprintf(stderr, "walk_stats L=%d phase=%d queued=%llu walks=%llu steps=%llu max=%llu over2^20=%llu\n",
-                         L, ph, (unsigned long long)G.qn, h[0], h[1], h[2], h[3]);
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw0).count();
+            std::fprintf(stderr,
+                         "walk_stats L=%d phase=%d queued=%llu walks=%llu steps=%llu max=%llu over2^20=%llu "
+                         "launch_ms=%.1f\n",
+                         L, ph, (unsigned long long)G.qn, h[0], h[1], h[2], h[3], ms);
         }
     }
     // 3. the long walks, replayed in LDS
@@ -2356,13 +2492,37 @@ int score_wide_groups(ulg_ctx *c, int L, int ph, std::vector<WideGroup> &gs, int
         ULG_HIP(c, hipStreamSynchronize(G.st));
         const unsigned long long sn = pin[ng + gi];
         if (sn == 0) continue;
-        const size_t lds = (size_t)4 * ((size_t)1 << q) / 8 + kStragState;
-        const auto kf = ph == 0 ? walk_wide_lds_kernel<0> : walk_wide_lds_kernel<1>;
+        // skip bitset in LDS; the hi bitset too up to q = kStragHiLdsQ, else in
+        // this group's checked-bitset slice (free once its walks are done)
+        const bool hl = q <= kStragHiLdsQ;
+        const uint64_t nw = ((uint64_t)1 << q) >> 6;
+        const size_t lds = (size_t)(hl ? 2 : 1) * nw * 8 + kStragState;
+        using LdsFn = void (*)(WideArgs, const uint64_t *, uint64_t *, unsigned long long *, unsigned long long *);
+        const LdsFn kf = ph == 0 ? (hl ? walk_wide_lds_kernel<0, true> : walk_wide_lds_kernel<0, false>)
+                                 : (hl ? walk_wide_lds_kernel<1, true> : walk_wide_lds_kernel<1, false>);
         ULG_HIP(c, hipFuncSetAttribute((const void *)kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        prof_begin_s(c, "walk_wide_lds", G.st);
-        hipLaunchKernelGGL(kf, dim3((unsigned)sn), dim3(64), lds, G.st, G.wa, G.queue + 3 * G.qn);
-        prof_end_s(c, G.st);
-        ULG_HIP(c, hipGetLastError());
+        const uint64_t per = hl ? sn : std::max<uint64_t>(1, slice / nw);
+        unsigned long long *ws = wstat ? c->d_stats.p : nullptr;
+        if (wstat) ULG_HIP(c, hipMemsetAsync(ws, 0, 128, G.st));
+        const auto tl0 = std::chrono::steady_clock::now();
+        for (uint64_t base = 0; base < sn; base += per) {
+            const uint64_t k = std::min<uint64_t>(per, sn - base);
+            prof_begin_s(c, "walk_wide_lds", G.st);
+            hipLaunchKernelGGL(kf, dim3((unsigned)k), dim3(kStragThreads), lds, G.st, G.wa,
+                               G.queue + 3 * (G.qn + base), G.bits, errf, ws);
+            prof_end_s(c, G.st);
+            ULG_HIP(c, hipGetLastError());
+        }
+        if (wstat) {
+            unsigned long long h[16];
+            ULG_HIP(c, hipMemcpyAsync(h, ws, 128, hipMemcpyDeviceToHost, G.st));
+            ULG_HIP(c, hipStreamSynchronize(G.st));
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tl0).count();
+            std::fprintf(stderr,
+                         "walk_lds_stats L=%d phase=%d q=%d replays=%llu iters=%llu max=%llu fill_max_us=%.1f "
+                         "walk_max_us=%.1f launch_ms=%.1f\n",
+                         L, ph, q, h[4], h[5], h[6], h[7] / 100.0, h[8] / 100.0, ms);
+        }
     }
     // the hi-cover metadata vectors must outlive their copies
     for (int gi = 0; gi < ng; ++gi)

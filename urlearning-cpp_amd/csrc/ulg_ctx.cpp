@@ -210,7 +210,7 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         return ULG_OK;
     }
     if (std::strcmp(name, "wide_lds") == 0) {
-        if (value < 0 || value > 1) return set_err(c, ULG_ERR_ARG, "wide_lds must be 0 or 1");
+        if (value < 0 || value > 2) return set_err(c, ULG_ERR_ARG, "wide_lds must be 0, 1 or 2");
         c->wide_lds = (int)value;
         return ULG_OK;
     }
