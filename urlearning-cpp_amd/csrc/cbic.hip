@@ -1675,7 +1675,8 @@ WideWalkFn wide_walk_fn(int L, int phase) {
 constexpr int kStragQMax = 20;                 // skip bitset 2^20 bits = 128 KiB of LDS
 constexpr int kStragHiLdsQ = 19;               // hi bitset in LDS up to here, else in global scratch
 constexpr uint64_t kStragBudget = 1ull << 13;  // steps in walk_wide_kernel before a walk moves here
-constexpr int kStragThreads = 256;             // fill threads; lane 0 walks
+constexpr int kStragThreads = 256;             // fill threads (64 when many walks share the GPU); wave 0 walks
+constexpr uint64_t kStragWide = 4096;          // replays per launch from which blocks are one wave
 constexpr int kStragDepth = 24;
 constexpr int kStragState = kStragDepth * 32 + 32;  // frames (2 x 16 B), lc
 constexpr uint64_t kStragIterCap = 1ull << 32;
@@ -1711,7 +1712,7 @@ __global__ void __launch_bounds__(kStragThreads) walk_wide_lds_kernel(WideArgs a
         }
     }
     __syncthreads();
-    for (uint32_t w = threadIdx.x; w < nw; w += kStragThreads) {
+    for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) {
         uint64_t sw = 0, hw = 0;
         uint64_t Xw = 0;  // compact mask of the word's high local bits
         for (uint32_t y = (w << 6); y; y &= y - 1) Xw |= 1ull << lc[__builtin_ctz(y)];
@@ -2508,7 +2509,10 @@ int score_wide_groups(ulg_ctx *c, int L, int ph, std::vector<WideGroup> &gs, int
         for (uint64_t base = 0; base < sn; base += per) {
             const uint64_t k = std::min<uint64_t>(per, sn - base);
             prof_begin_s(c, "walk_wide_lds", G.st);
-            hipLaunchKernelGGL(kf, dim3((unsigned)k), dim3(kStragThreads), lds, G.st, G.wa,
+            // many short replays: one wave per block, so more walks run at once
+            // (the walk is one wave's; waves 1-3 only speed up the fill)
+            const unsigned th = sn >= kStragWide ? 64u : (unsigned)kStragThreads;
+            hipLaunchKernelGGL(kf, dim3((unsigned)k), dim3(th), lds, G.st, G.wa,
                                G.queue + 3 * (G.qn + base), G.bits, errf, ws);
             prof_end_s(c, G.st);
             ULG_HIP(c, hipGetLastError());
