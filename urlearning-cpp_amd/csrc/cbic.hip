@@ -1744,7 +1744,6 @@ __global__ void __launch_bounds__(kStragThreads) walk_wide_lds_kernel(WideArgs a
     // re-read after each child returns and every test is a register bit test.
     const int lane = threadIdx.x;
     const uint64_t tk1 = wstats ? wall_clock64() : 0;
-    auto bit = [](const uint64_t *v, uint32_t t) -> bool { return (v[t >> 6] >> (t & 63)) & 1ull; };
     auto rfl = [](uint32_t v) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
     // lanes >= q read a valid word too, so both loads issue back to back
     const uint32_t lbit = 1u << (lane < q ? lane : 0);

@@ -202,6 +202,7 @@ struct DEnt {
 
 struct DenseHeap {
     DEnt *a = nullptr;  // buffer (grows to at most 2^m + 1 entries; never shrinks)
+    bool pf5 = false;   // pop: prefetch five levels ahead as well as four
     int64_t len = 0, hwm = 0;
     DenseRec *recs = nullptr;
     bool hang = false;
@@ -251,6 +252,15 @@ struct DenseHeap {
             if (g4 + 15 < n) {
                 __builtin_prefetch(&a[g4]);
                 __builtin_prefetch(&a[g4 + 15]);
+            }
+            if (pf5) {  // and five levels ahead: 32 entries, 256 B
+                const int64_t g5 = 32 * second + 31;
+                if (g5 + 31 < n) {
+                    __builtin_prefetch(&a[g5]);
+                    __builtin_prefetch(&a[g5 + 8]);
+                    __builtin_prefetch(&a[g5 + 16]);
+                    __builtin_prefetch(&a[g5 + 31]);
+                }
             }
             second = 2 * (second + 1);
             second -= (int64_t)cns(a[second], a[second - 1]);
