@@ -294,7 +294,7 @@ int ulg_sweep_shard_end(ulg_ctx *ctx, uint64_t *vpar, int *order, float *goal_co
  * below which no present key reaches -ts (hi-cover tables per variable);
  * "wide_reduced" (0/1, default 1): they skip the recursion's re-tests that
  * cannot change its state (each expanded node costs O(m) tests, not O(m^2));
- * "wide_lds" (0/1/2, default 1): walks longer than 2^13 steps are replayed by
+ * "wide_lds" (0/1/2, default 1): walks longer than 2^6 steps are replayed by
  * one workgroup each with their skip / hi bitsets in LDS (2^q <= 2^20 local
  * subsets; the hi bitset in HBM above 2^19); 2 replays every walk that way.
  * All variants compute identical results; the knob exists for A/B timing. */

@@ -117,7 +117,7 @@ def test_c1_hepatitis_default_parent_limit_matches_digest(ulg_ctx):
 def test_wide_hicover_prune_identical_lists(ulg_ctx):
     """ulg_set_option("wide_prune"): the walks skip absent nodes below which no
     present key reaches -ts; "wide_reduced": they skip the recursion's no-op
-    re-tests; "wide_lds": walks over 2^13 steps (2: over 1 step, so every
+    re-tests; "wide_lds": walks over 2^6 steps (2: over 1 step, so every
     walk) are replayed by walk_wide_lds_kernel.  The stored lists with and without either are identical bit for
     bit, on C4's (n=30, N=100k, MMPC, -p = n-1) variables
     whose unpruned walks finish in well under a second each."""

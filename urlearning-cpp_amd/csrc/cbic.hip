@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "search_internal.h"
@@ -1674,7 +1675,13 @@ WideWalkFn wide_walk_fn(int L, int phase) {
 // test is a register bit test; frames are 32 B in LDS, pushed per expansion.
 constexpr int kStragQMax = 20;                 // skip bitset 2^20 bits = 128 KiB of LDS
 constexpr int kStragHiLdsQ = 19;               // hi bitset in LDS up to here, else in global scratch
-constexpr uint64_t kStragBudget = 1ull << 13;  // steps in walk_wide_kernel before a walk moves here
+constexpr uint64_t kStragBudget = 1ull << 6;  // steps in walk_wide_kernel before a walk moves here (2^13 -> 2^6: C4 0.82 -> 0.24 s, C1 10.0 -> 9.4 s)
+// ULG_STRAG_BUDGET=<log2 steps> overrides it (A/B timing only: results are the same)
+inline uint64_t strag_budget() {
+    static const uint64_t b = std::getenv("ULG_STRAG_BUDGET") ? 1ull << std::atoi(std::getenv("ULG_STRAG_BUDGET"))
+                                                              : kStragBudget;
+    return b;
+}
 constexpr int kStragThreads = 256;             // fill threads (64 when many walks share the GPU); wave 0 walks
 constexpr uint64_t kStragWide = 4096;          // replays per launch from which blocks are one wave
 constexpr int kStragDepth = 24;
@@ -2459,7 +2466,7 @@ int score_wide_groups(ulg_ctx *c, int L, int ph, std::vector<WideGroup> &gs, int
         }
         // long walks move to the LDS kernel (reduced walks with hi-cover tables only)
         budget[gi] = (wa.hoff && wa.reduced && q <= kStragQMax && c->wide_lds)
-                         ? (c->wide_lds == 2 ? 1 : kStragBudget)
+                         ? (c->wide_lds == 2 ? 1 : strag_budget())
                          : 0;
         uint64_t *sq = G.queue + 3 * G.qn;  // straggler queue after this launch's entries (the queue has room)
         if (budget[gi]) ULG_HIP(c, hipMemsetAsync(G.scnt, 0, 8, st));
