@@ -210,32 +210,96 @@ __global__ void __launch_bounds__(kB) sweep_w_kernel(SearchDev d, const uint64_t
 // The same slices when every v_j's lattice is exactly over comp \ {v_j}
 // (D_v = the rest of the component, the tables' scope covers it): then slice
 // entry (j, p, r) is lattice entry i of v_j with popcount(i) = p and colex
-// rank r, so each thread reads one lattice entry in order (coalesced) and
-// writes it to its slice; a wave's 64 consecutive i land in 7 contiguous
-// runs (one per popcount of their low 6 bits).
-constexpr int kScatterPer = 16;
-__global__ void __launch_bounds__(kB) sweep_w_scatter_kernel(const uint32_t *table, const uint64_t *tb_off,
-                                                             const uint64_t *gbinom, const uint64_t *loffm1,
-                                                             const int *comp_vars, const int *jlist, int m,
-                                                             uint64_t half, float *w) {
+// rank r.  A block takes 2^kTileBits consecutive entries i (one high part H,
+// every low part): colex rank = rank of the low part + a term of H and the
+// low popcount k only, so the tile's entries land in kTileBits + 1
+// contiguous runs of the slice, one per k, C(kTileBits, k) long.  The block
+// reads the tile in order, permutes it in LDS into run order and writes the
+// runs out contiguously (the previous form wrote each wave's 64 entries as 7
+// runs of 1..20 floats: 2.6 ms for C3's 1.68 GB of slices).
+constexpr int kTileBits = 12;
+// the permutation of a full tile, the same for every tile: entry e (the low
+// part) goes to run popcount(e) at its colex rank; run_of[r] = the run of
+// run-order position r
+struct TilePerm {
+    uint16_t dst[1 << kTileBits];
+    uint8_t run_of[1 << kTileBits];
+};
+constexpr TilePerm make_tile_perm() {
+    TilePerm t{};
+    uint32_t C[kTileBits + 1][kTileBits + 2] = {};
+    for (int a = 0; a <= kTileBits; ++a) {
+        C[a][0] = 1;
+        for (int b = 1; b <= a; ++b) C[a][b] = C[a - 1][b - 1] + (b <= a - 1 ? C[a - 1][b] : 0);
+    }
+    uint32_t roff[kTileBits + 2] = {};
+    for (int k = 0; k <= kTileBits; ++k) roff[k + 1] = roff[k] + C[kTileBits][k];
+    for (uint32_t e = 0; e < (1u << kTileBits); ++e) {
+        uint32_t rank = 0;
+        int tt = 0;
+        for (int b = 0; b < kTileBits; ++b)
+            if ((e >> b) & 1u) {
+                ++tt;
+                rank += C[b][tt];
+            }
+        t.dst[e] = (uint16_t)(roff[tt] + rank);
+    }
+    for (int k = 0; k <= kTileBits; ++k)
+        for (uint32_t r = roff[k]; r < roff[k + 1]; ++r) t.run_of[r] = (uint8_t)k;
+    return t;
+}
+__constant__ TilePerm kTilePerm = make_tile_perm();
+
+__global__ void __launch_bounds__(kB) sweep_w_tile_kernel(const uint32_t *table, const uint64_t *tb_off,
+                                                          const uint64_t *gbinom, const uint64_t *loffm1,
+                                                          const int *comp_vars, const int *jlist, int m,
+                                                          uint64_t half, float *w) {
     __shared__ uint32_t binom[33 * 33];
     __shared__ uint32_t lo[kMaxM + 1];
+    __shared__ float tile[1 << kTileBits];
+    __shared__ uint32_t roff[kTileBits + 2];
+    __shared__ uint32_t rbase[kTileBits + 1];
     for (int e = threadIdx.x; e < m * 33; e += kB) binom[e] = (uint32_t)gbinom[e];
     for (int i = threadIdx.x; i <= m; i += kB) lo[i] = (uint32_t)loffm1[i];
     __syncthreads();
+    const int lb = m - 1 < kTileBits ? m - 1 : kTileBits;
+    const uint32_t tn = 1u << lb;
+    const uint64_t H = (uint64_t)blockIdx.x << lb;  // the tile's high part
     const int j = jlist ? jlist[blockIdx.y] : (int)blockIdx.y;
     const uint32_t *tv = table + tb_off[comp_vars[j]];
     float *wj = w + (uint64_t)blockIdx.y * half;
-    // kScatterPer entries per thread, kB apart (each pass is one coalesced
-    // sweep of the block's range): the LDS preload is paid once per block
-    const uint64_t base = (uint64_t)blockIdx.x * kB * kScatterPer;
-    for (int k = 0; k < kScatterPer; ++k) {
-        const uint64_t i = base + (uint64_t)k * kB + threadIdx.x;
-        if (i >= half) return;
+    if (threadIdx.x <= (unsigned)lb) {
+        const int k = (int)threadIdx.x;  // low popcount
+        uint32_t o = 0;
+        for (int kk = 0; kk < k; ++kk) o += binom[lb * 33 + kk];
+        roff[k] = o;
+        if (k == lb) roff[lb + 1] = tn;
+        uint32_t rank = 0;
+        int t = k;
+        for (uint64_t x = H; x; x &= x - 1) rank += binom[__builtin_ctzll(x) * 33 + (++t)];
+        rbase[k] = lo[t] + rank;  // t = k + popcount(H): the slice's layer
+    }
+    __syncthreads();
+    if (lb == kTileBits) {
+        for (uint32_t e = threadIdx.x; e < tn; e += kB) tile[kTilePerm.dst[e]] = ord_cost(tv[H + e]);
+        __syncthreads();
+        for (uint32_t e = threadIdx.x; e < tn; e += kB) {
+            const int k = kTilePerm.run_of[e];
+            wj[rbase[k] + (e - roff[k])] = tile[e];
+        }
+        return;
+    }
+    for (uint32_t e = threadIdx.x; e < tn; e += kB) {  // a component of <= kTileBits + 1 variables
         uint32_t rank = 0;
         int t = 0;
-        for (uint64_t x = i; x; x &= x - 1) rank += binom[__builtin_ctzll(x) * 33 + (++t)];
-        wj[lo[t] + rank] = ord_cost(tv[i]);
+        for (uint32_t x = e; x; x &= x - 1) rank += binom[__builtin_ctz(x) * 33 + (++t)];
+        tile[roff[t] + rank] = ord_cost(tv[H + e]);
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < tn; e += kB) {
+        int k = 0;
+        while (roff[k + 1] <= e) ++k;
+        wj[rbase[k] + (e - roff[k])] = tile[e];
     }
 }
 
@@ -575,10 +639,9 @@ int astar_gpu(ulg_ctx *c, const uint64_t *edges, uint64_t *vpar, int *order, flo
                 if (e == hipSuccess) {
                     prof_begin(c, "search_sweep_w");
                     if (sweep_scatter_ok(s, comp))
-                        sweep_w_scatter_kernel<<<dim3((unsigned)((half + kB * kScatterPer - 1) / (kB * kScatterPer)),
-                                                      (unsigned)m), kB, 0,
-                                                 c->stream>>>(s.d_table.p, s.d_tb_off.p, d_bn.p, d_lo.p, d_cv.p,
-                                                              nullptr, m, half, s.d_sweep_w.p);
+                        sweep_w_tile_kernel<<<dim3((unsigned)(half >> std::min(m - 1, kTileBits)), (unsigned)m), kB, 0,
+                                              c->stream>>>(s.d_table.p, s.d_tb_off.p, d_bn.p, d_lo.p, d_cv.p, nullptr,
+                                                           m, half, s.d_sweep_w.p);
                     else
                         sweep_w_kernel<<<dim3((unsigned)((half + kB - 1) / kB), (unsigned)m), kB, 0, c->stream>>>(
                             dv, d_bn.p, d_lo.p, d_cv.p, m, half, s.d_sweep_w.p, nullptr);
@@ -714,9 +777,9 @@ int sweep_shard_begin(ulg_ctx *c, uint64_t own, int64_t *max_nodes) {
             if (s.support[v] != (all & ~(1ull << v))) scatter = false;
         }
         if (scatter)
-            sweep_w_scatter_kernel<<<dim3((unsigned)((half + kB * kScatterPer - 1) / (kB * kScatterPer)), (unsigned)nown),
-                                     kB, 0, c->stream>>>(
-                s.d_table.p, s.d_tb_off.p, s.shard_bn.p, d_lo.p, s.shard_cv.p, d_jl.p, m, half, s.d_sweep_w.p);
+            sweep_w_tile_kernel<<<dim3((unsigned)(half >> std::min(m - 1, kTileBits)), (unsigned)nown), kB, 0,
+                                  c->stream>>>(s.d_table.p, s.d_tb_off.p, s.shard_bn.p, d_lo.p, s.shard_cv.p, d_jl.p, m,
+                                               half, s.d_sweep_w.p);
         else
             sweep_w_kernel<<<dim3((unsigned)((half + kB - 1) / kB), (unsigned)nown), kB, 0, c->stream>>>(
                 s.dev(), s.shard_bn.p, d_lo.p, s.shard_cv.p, m, half, s.d_sweep_w.p, d_jl.p);
