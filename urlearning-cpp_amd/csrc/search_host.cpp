@@ -225,7 +225,8 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
     open.a = static_cast<DEnt *>(heapmem.p) + 1;
     // pop: prefetch 5 levels ahead too (C3: 17.6 -> 16.8 s on the box's EPYC
     // 9575F; ULG_EXACT_PF=0 turns it off).  Prefetching the entries of the
-    // coming decrease-keys was measured slower (18.3 s) and is not done.
+    // coming decrease-keys (18.3 s), or the likely next pop's row and
+    // successor records (18.6 s), was measured slower and is not done.
     static const int pfmode = std::getenv("ULG_EXACT_PF") ? std::atoi(std::getenv("ULG_EXACT_PF")) : 2;
     open.pf5 = (pfmode & 2) != 0;
 
