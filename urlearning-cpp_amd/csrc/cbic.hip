@@ -546,8 +546,16 @@ __device__ __forceinline__ BS make_bits(uint64_t *lds_base) {
 // PHASE 0: sets containing variable 0; 1: the rest.  V = variant bits (see
 // ulg_set_option "score_variant"), compile-time so each form gets its own
 // register allocation.
+#ifndef ULG_SCORE_WPE
+#define ULG_SCORE_WPE 0  // A/B builds: minimum waves per SIMD asked of the scoring kernel's register budget
+#endif
+#if ULG_SCORE_WPE > 0
+#define ULG_SCORE_ATTR __attribute__((amdgpu_waves_per_eu(ULG_SCORE_WPE)))
+#else
+#define ULG_SCORE_ATTR
+#endif
 template <int L, int PHASE, int V>
-__global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
+__global__ void __launch_bounds__(kBlock) ULG_SCORE_ATTR score_layer_kernel(ScoreArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const LdsLayout lay = lds_layout(a.n, a.nv, a.S, L, V);
     double *g = reinterpret_cast<double *>(smem + lay.gram);

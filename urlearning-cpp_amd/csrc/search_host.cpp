@@ -227,7 +227,11 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
     // 9575F; ULG_EXACT_PF=0 turns it off).  Prefetching the entries of the
     // coming decrease-keys (18.3 s), or the likely next pop's row and
     // successor records (18.6 s), was measured slower and is not done.
-    static const int pfmode = std::getenv("ULG_EXACT_PF") ? std::atoi(std::getenv("ULG_EXACT_PF")) : 2;
+    // Bit 2 (default on): the heap top's successor records and cost row are
+    // prefetched before its pop, so they arrive while the pop descends the
+    // heap (C3 16.9 -> 14.0 s, 2 alternating A/B runs); bit 3 adds the coming
+    // decrease-keys' heap entries after the pop (measured no better).
+    static const int pfmode = std::getenv("ULG_EXACT_PF") ? std::atoi(std::getenv("ULG_EXACT_PF")) : 6;
     open.pf5 = (pfmode & 2) != 0;
 
     // slot bit of each variable, and its column in the row table
@@ -259,6 +263,17 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
         }
         if (prof) t0 = __rdtsc();
         const int64_t hl = open.len;
+        if (pfmode & 4) {
+            // the node about to be popped is already known (the heap top):
+            // its successor records and cost row are fetched while the pop
+            // descends the heap, instead of after it
+            const uint32_t top = open.a[0].slot();
+            const uint64_t tv = g_have_bmi2 ? pdep_bmi2(top, scope) : pdep64(top, scope);
+            const float *trow = rows + (uint64_t)top * (uint64_t)nl;
+            __builtin_prefetch(trow);
+            __builtin_prefetch(trow + nl - 1);
+            for (uint64_t x = the_scc & ~tv; x; x &= x - 1) __builtin_prefetch(&recs[top | sbit[__builtin_ctzll(x)]], 1);
+        }
         const uint32_t ui = open.pop();
         if (prof) {
             t1 = __rdtsc();
@@ -281,9 +296,19 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
                 if ((variables & edges[leaf]) == 0) leaves &= ~(1ull << leaf);
             }
         const float *row = rows + (uint64_t)ui * (uint64_t)nl;
-        __builtin_prefetch(row);
-        __builtin_prefetch(row + nl - 1);
-        for (uint64_t x = leaves; x; x &= x - 1) __builtin_prefetch(&recs[ui | sbit[__builtin_ctzll(x)]], 1);
+        if (!(pfmode & 4)) {
+            __builtin_prefetch(row);
+            __builtin_prefetch(row + nl - 1);
+            for (uint64_t x = leaves; x; x &= x - 1) __builtin_prefetch(&recs[ui | sbit[__builtin_ctzll(x)]], 1);
+        }
+        if (pfmode & 8) {
+            // the heap entries the coming decrease-keys start from (the
+            // records are in cache by now)
+            for (uint64_t x = leaves; x; x &= x - 1) {
+                const int32_t p = recs[ui | sbit[__builtin_ctzll(x)]].pq;
+                if (p > 0) __builtin_prefetch(&open.a[p - 1], 1);
+            }
+        }
         for (uint64_t x = leaves; x; x &= x - 1) {
             const int leaf = __builtin_ctzll(x);
             const uint32_t si = ui | sbit[leaf];

@@ -154,6 +154,94 @@ void astar_cluster(const HostTables &T, uint64_t cluster, ClusterRun &R) {
     }
 }
 
+// astar_cluster over dense node homes: recs[pext(S, cluster)] (16 B) and
+// 8-byte heap entries (DenseHeap, the same heap algorithms and comparator as
+// Heap), so a successor is one read of a small array instead of an index
+// probe plus a node-vector read.  Re-opening (:556-576) pushes a closed
+// record back; a record's pq is 0 until its node is generated (the root is
+// never a successor, so generatedNodes' missing root changes nothing).  The
+// expansion count and the goal's leaf chain equal astar_cluster's (A/B:
+// ULG_TRIPLET_DENSE=0, tests/test_gpu_triplet.py).
+constexpr int kDenseClusterBits = 22;  // 64 MiB of records per search thread
+
+void astar_cluster_dense(const HostTables &T, uint64_t cluster, ClusterRun &R) {
+    const int m = __builtin_popcountll(cluster);
+    const uint64_t nslots = 1ull << m;
+    thread_local std::vector<DenseRec> recv;
+    thread_local std::vector<DEnt> heapv;
+    if (recv.size() < nslots) recv.resize(nslots);
+    if (heapv.size() < nslots + 2) heapv.resize(nslots + 2);
+    DenseRec *recs = recv.data();
+    std::memset(recs, 0, nslots * sizeof(DenseRec));
+    DenseHeap open;
+    open.recs = recs;
+    open.a = heapv.data() + 1;
+    uint32_t sbit[64] = {0};
+    {
+        int i = 0;
+        for (uint64_t x = cluster; x; x &= x - 1) sbit[__builtin_ctzll(x)] = 1u << i++;
+    }
+    const uint32_t goal_slot = (uint32_t)(nslots - 1);
+    const uint64_t r1 = cluster >> 1;
+    recs[0] = DenseRec{0.0f, 0.0f, 0, (uint8_t)(r1 ? __builtin_ctzll(r1) + 1 : 0), {0, 0, 0}};
+    open.push(0);
+    int64_t goal = -1, nexp = 0;
+    const float upperBound = FLT_MAX;
+    while (open.len > 0) {
+        const uint32_t ui = open.pop();
+        ++nexp;
+        if (ui == goal_slot) { goal = ui; break; }
+        DenseRec &U = recs[ui];
+        if (U.g + U.h > upperBound) break;
+        U.pq = -1;
+        const float ug = U.g;
+        const uint64_t variables = g_have_bmi2 ? pdep_bmi2(ui, cluster) : pdep64(ui, cluster);
+        const uint64_t cand = cluster & ~variables;
+        for (uint64_t x = cand; x; x &= x - 1) T.prefetch_bs(__builtin_ctzll(x), variables);
+        for (uint64_t x = cand; x; x &= x - 1) {
+            const int leaf = __builtin_ctzll(x);
+            const uint32_t si = ui | sbit[leaf];
+            DenseRec &S = recs[si];
+            // getScore(leaf, S u {leaf}) == getScore(leaf, S): leaf is never in its own sets
+            const float g = ug + T.bs(leaf, variables);
+            if (S.pq == 0) {
+                bool complete = false;
+                S.g = g;
+                S.h = T.h(variables | (1ull << leaf), &complete);
+                S.leaf = (uint8_t)leaf;
+                open.push(si);
+                continue;
+            }
+            if (g < S.g) {
+                S.leaf = (uint8_t)leaf;
+                S.g = g;
+                if (S.pq == -1) open.push(si);  // re-open
+                else open.update(si);
+            }
+        }
+    }
+    R.nexp = nexp;
+    R.hang = open.hang;
+    if (goal < 0) return;
+    // reconstructSolution (:172-224)
+    uint64_t remaining = cluster;
+    uint32_t cur = (uint32_t)goal;
+    for (int i = 0; i < m; ++i) {
+        const int leaf = recs[cur].leaf;
+        R.qv.push_back(leaf);
+        R.qs.push_back(remaining);
+        remaining ^= 1ull << leaf;
+        cur ^= sbit[leaf];
+        if (remaining == 0 || recs[cur].pq == 0) break;  // the root is not in generatedNodes
+    }
+}
+
+void search_cluster(const HostTables &T, uint64_t cluster, ClusterRun &R) {
+    static const bool dense = !std::getenv("ULG_TRIPLET_DENSE") || std::atoi(std::getenv("ULG_TRIPLET_DENSE")) != 0;
+    if (dense && __builtin_popcountll(cluster) <= kDenseClusterBits) astar_cluster_dense(T, cluster, R);
+    else astar_cluster(T, cluster, R);
+}
+
 // each leaf's best parent set among its predecessors, from the device tables
 int cluster_parents_of(Triplet &t, const ClusterRun &R, std::vector<uint64_t> &op) {
     op.assign(t.n, 0);
@@ -174,7 +262,7 @@ int cluster_astar(Triplet &t, uint64_t cluster, std::vector<uint64_t> &op) {
     HostTables T;
     host_tables(*t.s, T);
     ClusterRun R;
-    astar_cluster(T, cluster, R);
+    search_cluster(T, cluster, R);
     t.expanded += R.nexp;
     if (R.hang) t.hang = true;
     return cluster_parents_of(t, R, op);
@@ -266,7 +354,7 @@ int solve_parallel(Triplet &t, const std::vector<uint64_t> &batch) {
             T.pd = P.pd.data();
             T.groups = P.groups;
             T.pd_off = P.pd_off;
-            astar_cluster(T, batch[i], runs[i]);
+            search_cluster(T, batch[i], runs[i]);
         }
     };
     std::vector<std::thread> pool;
