@@ -162,20 +162,21 @@ void astar_cluster(const HostTables &T, uint64_t cluster, ClusterRun &R) {
 // never a successor, so generatedNodes' missing root changes nothing).  The
 // expansion count and the goal's leaf chain equal astar_cluster's (A/B:
 // ULG_TRIPLET_DENSE=0, tests/test_gpu_triplet.py).
-constexpr int kDenseClusterBits = 22;  // 64 MiB of records per search thread
+// Every cluster the driver searches qualifies (kMaxCluster): at 26 variables
+// 1 GiB of records and 0.5 GiB of heap per search thread, kept per thread.
+constexpr int kDenseClusterBits = kMaxCluster;
 
-void astar_cluster_dense(const HostTables &T, uint64_t cluster, ClusterRun &R) {
+bool astar_cluster_dense(const HostTables &T, uint64_t cluster, ClusterRun &R) {
     const int m = __builtin_popcountll(cluster);
     const uint64_t nslots = 1ull << m;
-    thread_local std::vector<DenseRec> recv;
-    thread_local std::vector<DEnt> heapv;
-    if (recv.size() < nslots) recv.resize(nslots);
-    if (heapv.size() < nslots + 2) heapv.resize(nslots + 2);
-    DenseRec *recs = recv.data();
-    std::memset(recs, 0, nslots * sizeof(DenseRec));
+    thread_local HostHuge recmem, heapmem;
+    if (!recmem.reserve(nslots * sizeof(DenseRec), false) || !heapmem.reserve((nslots + 16) * sizeof(DEnt), false))
+        return false;
+    DenseRec *recs = static_cast<DenseRec *>(recmem.p);
+    recmem.zero_prefix(nslots * sizeof(DenseRec));
     DenseHeap open;
     open.recs = recs;
-    open.a = heapv.data() + 1;
+    open.a = static_cast<DEnt *>(heapmem.p) + 1;
     uint32_t sbit[64] = {0};
     {
         int i = 0;
@@ -188,6 +189,13 @@ void astar_cluster_dense(const HostTables &T, uint64_t cluster, ClusterRun &R) {
     int64_t goal = -1, nexp = 0;
     const float upperBound = FLT_MAX;
     while (open.len > 0) {
+        {
+            // the top's successor records are fetched while the pop descends
+            // the heap (search_host.cpp's dense replay does the same)
+            const uint32_t top = open.a[0].slot();
+            const uint64_t tv = g_have_bmi2 ? pdep_bmi2(top, cluster) : pdep64(top, cluster);
+            for (uint64_t x = cluster & ~tv; x; x &= x - 1) __builtin_prefetch(&recs[top | sbit[__builtin_ctzll(x)]], 1);
+        }
         const uint32_t ui = open.pop();
         ++nexp;
         if (ui == goal_slot) { goal = ui; break; }
@@ -222,7 +230,7 @@ void astar_cluster_dense(const HostTables &T, uint64_t cluster, ClusterRun &R) {
     }
     R.nexp = nexp;
     R.hang = open.hang;
-    if (goal < 0) return;
+    if (goal < 0) return true;
     // reconstructSolution (:172-224)
     uint64_t remaining = cluster;
     uint32_t cur = (uint32_t)goal;
@@ -234,12 +242,13 @@ void astar_cluster_dense(const HostTables &T, uint64_t cluster, ClusterRun &R) {
         cur ^= sbit[leaf];
         if (remaining == 0 || recs[cur].pq == 0) break;  // the root is not in generatedNodes
     }
+    return true;
 }
 
 void search_cluster(const HostTables &T, uint64_t cluster, ClusterRun &R) {
     static const bool dense = !std::getenv("ULG_TRIPLET_DENSE") || std::atoi(std::getenv("ULG_TRIPLET_DENSE")) != 0;
-    if (dense && __builtin_popcountll(cluster) <= kDenseClusterBits) astar_cluster_dense(T, cluster, R);
-    else astar_cluster(T, cluster, R);
+    if (dense && __builtin_popcountll(cluster) <= kDenseClusterBits && astar_cluster_dense(T, cluster, R)) return;
+    astar_cluster(T, cluster, R);  // the indexed form (or the mapping failed)
 }
 
 // each leaf's best parent set among its predecessors, from the device tables
