@@ -21,6 +21,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <unordered_map>
 #include <unordered_set>
 
@@ -35,6 +38,8 @@ constexpr int kMaxCluster = 26;  // triplet_astar.cpp:840
 
 inline bool bit(uint64_t s, int i) { return (s >> i) & 1ull; }
 
+struct SearchPool;
+
 struct Triplet {
     ulg_ctx *c = nullptr;
     SearchState *s = nullptr;
@@ -48,6 +53,7 @@ struct Triplet {
         bool hang = false;
     };
     std::unordered_map<uint64_t, SpecResult> spec;  // searched ahead, not yet asked for
+    SearchPool *pool = nullptr;  // look-ahead searches on host threads (ulg_triplet_astar)
     int threads = 1;           // host threads for searches ahead (ULG_TRIPLET_THREADS)
     bool parallel_ok = false;  // device tables cover every variable; host costs ready
     int ci = -1, cj = 0, ck = 0;  // the first sweep's current triple (speculate); -1: off
@@ -81,6 +87,7 @@ struct Triplet {
 struct ClusterRun {
     int64_t nexp = 0;
     bool hang = false;
+    bool cancelled = false;  // stopped by SearchPool::shutdown (never consumed)
     std::vector<int> qv;        // leaves from the goal back to the root
     std::vector<uint64_t> qs;   // the set each leaf was added to (incl. itself)
 };
@@ -88,7 +95,7 @@ struct ClusterRun {
 // run_astar_on_one_scc of triplet_astar.cpp:285-674 with ancestors = {} and
 // the_scc = cluster: no skeleton filter, and a closed node whose g strictly
 // improves is pushed back onto the open list (:556-576).  Reads only T.
-void astar_cluster(const HostTables &T, uint64_t cluster, ClusterRun &R) {
+void astar_cluster(const HostTables &T, uint64_t cluster, ClusterRun &R, const std::atomic<bool> *cancel) {
     std::vector<Node> nodes;
     nodes.reserve(1024);
     SubsetIndex generated;
@@ -101,6 +108,10 @@ void astar_cluster(const HostTables &T, uint64_t cluster, ClusterRun &R) {
     int64_t goal = -1, nexp = 0;
     const float upperBound = FLT_MAX;
     while (!open.empty()) {
+        if (cancel && (nexp & 4095) == 0 && cancel->load(std::memory_order_relaxed)) {
+            R.cancelled = true;
+            return;
+        }
         const uint32_t ui = open.pop();
         ++nexp;
         const uint64_t variables = nodes[ui].sub;
@@ -166,7 +177,7 @@ void astar_cluster(const HostTables &T, uint64_t cluster, ClusterRun &R) {
 // 1 GiB of records and 0.5 GiB of heap per search thread, kept per thread.
 constexpr int kDenseClusterBits = kMaxCluster;
 
-bool astar_cluster_dense(const HostTables &T, uint64_t cluster, ClusterRun &R) {
+bool astar_cluster_dense(const HostTables &T, uint64_t cluster, ClusterRun &R, const std::atomic<bool> *cancel) {
     const int m = __builtin_popcountll(cluster);
     const uint64_t nslots = 1ull << m;
     thread_local HostHuge recmem, heapmem;
@@ -189,6 +200,10 @@ bool astar_cluster_dense(const HostTables &T, uint64_t cluster, ClusterRun &R) {
     int64_t goal = -1, nexp = 0;
     const float upperBound = FLT_MAX;
     while (open.len > 0) {
+        if (cancel && (nexp & 4095) == 0 && cancel->load(std::memory_order_relaxed)) {
+            R.cancelled = true;
+            return true;
+        }
         {
             // the top's successor records are fetched while the pop descends
             // the heap (search_host.cpp's dense replay does the same)
@@ -245,10 +260,10 @@ bool astar_cluster_dense(const HostTables &T, uint64_t cluster, ClusterRun &R) {
     return true;
 }
 
-void search_cluster(const HostTables &T, uint64_t cluster, ClusterRun &R) {
+void search_cluster(const HostTables &T, uint64_t cluster, ClusterRun &R, const std::atomic<bool> *cancel = nullptr) {
     static const bool dense = !std::getenv("ULG_TRIPLET_DENSE") || std::atoi(std::getenv("ULG_TRIPLET_DENSE")) != 0;
-    if (dense && __builtin_popcountll(cluster) <= kDenseClusterBits && astar_cluster_dense(T, cluster, R)) return;
-    astar_cluster(T, cluster, R);  // the indexed form (or the mapping failed)
+    if (dense && __builtin_popcountll(cluster) <= kDenseClusterBits && astar_cluster_dense(T, cluster, R, cancel)) return;
+    astar_cluster(T, cluster, R, cancel);  // the indexed form (or the mapping failed)
 }
 
 // each leaf's best parent set among its predecessors, from the device tables
@@ -382,6 +397,104 @@ int solve_parallel(Triplet &t, const std::vector<uint64_t> &batch) {
     return ULG_OK;
 }
 
+// A pool of host threads that searches clusters ahead of the driver: the
+// driver queues the cluster it needs at the front and the clusters it will
+// probably ask for next behind it, and waits only for the one it needs, while
+// the others keep running (a batch no longer waits for its slowest search).
+// A result is counted (runs, distinct, expansions) only when the driver asks
+// for its cluster, so the statistics are the sequential driver's; results
+// never asked for are dropped, and searches still running at the end are
+// cancelled.  Workers read only the host cost table and their own host PDBs.
+struct SearchPool {
+    HostTables base;
+    int pd_count = 2;
+    std::mutex mu;
+    std::condition_variable cv_work, cv_done;
+    std::deque<uint64_t> queue;
+    std::unordered_map<uint64_t, int> state;  // 1 queued, 2 running, 3 done
+    std::unordered_map<uint64_t, std::pair<ClusterRun, bool>> done;  // run, PDB built
+    std::atomic<bool> cancel{false};
+    bool stop = false;
+    std::vector<std::thread> workers;
+
+    void start(const SearchState &s, int pdc, int nthreads) {
+        host_tables(s, base);
+        pd_count = pdc;
+        for (int k = 0; k < nthreads; ++k) workers.emplace_back([this] { work(); });
+    }
+    void work() {
+        HostPdb P;
+        std::unique_lock<std::mutex> lk(mu);
+        while (true) {
+            cv_work.wait(lk, [&] { return stop || !queue.empty(); });
+            if (stop) return;
+            const uint64_t cl = queue.front();
+            queue.pop_front();
+            state[cl] = 2;
+            lk.unlock();
+            ClusterRun R;
+            const bool ok = pdb_host(base, cl, pd_count, P);
+            if (ok) {
+                HostTables T = base;
+                T.pd = P.pd.data();
+                T.groups = P.groups;
+                T.pd_off = P.pd_off;
+                search_cluster(T, cl, R, &cancel);
+            }
+            lk.lock();
+            done.emplace(cl, std::make_pair(std::move(R), ok));
+            state[cl] = 3;
+            cv_done.notify_all();
+        }
+    }
+    bool known(uint64_t cl) {
+        std::lock_guard<std::mutex> lk(mu);
+        return state.count(cl) != 0;
+    }
+    size_t pending() {
+        std::lock_guard<std::mutex> lk(mu);
+        return queue.size();
+    }
+    // queue cl (front: the driver needs it now; a queued one moves up)
+    void submit(uint64_t cl, bool front) {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = state.find(cl);
+        if (it != state.end()) {
+            if (front && it->second == 1) {
+                queue.erase(std::find(queue.begin(), queue.end(), cl));
+                queue.push_front(cl);
+            }
+            return;
+        }
+        state[cl] = 1;
+        if (front) queue.push_front(cl);
+        else queue.push_back(cl);
+        cv_work.notify_one();
+    }
+    // waits for a submitted cluster's search and hands its result over
+    void take(uint64_t cl, ClusterRun &R, bool &ok) {
+        std::unique_lock<std::mutex> lk(mu);
+        cv_done.wait(lk, [&] { return state[cl] == 3; });
+        auto it = done.find(cl);
+        R = std::move(it->second.first);
+        ok = it->second.second;
+        done.erase(it);
+        state.erase(cl);
+    }
+    void shutdown() {
+        cancel = true;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+            queue.clear();
+        }
+        cv_work.notify_all();
+        for (auto &th : workers) th.join();
+        workers.clear();
+    }
+    ~SearchPool() { shutdown(); }
+};
+
 // Up to `want` distinct clusters, not yet searched, of the triples the first
 // sweep reaches after (ci, cj, ck) on the current skeleton -- orientations may
 // still change some of them, which only leaves a result unused.
@@ -399,7 +512,7 @@ void speculate(Triplet &t, std::vector<uint64_t> &batch, size_t want) {
                 if (t.checked.count(key)) continue;
                 const uint64_t big = t.clusters[i] | t.clusters[unc[j]] | t.clusters[unc[k]];
                 if (__builtin_popcountll(big) > kMaxCluster || t.memo->count(big) || t.spec.count(big) ||
-                    !seen.insert(big).second)
+                    (t.pool && t.pool->known(big)) || !seen.insert(big).second)
                     continue;
                 batch.push_back(big);
             }
@@ -412,12 +525,28 @@ const std::vector<uint64_t> *cluster_parents(Triplet &t, uint64_t cluster) {
     if (it != t.memo->end()) return &it->second;
     static const bool trace = std::getenv("ULG_TRIPLET_TRACE") != nullptr;  // per-search progress on stderr
     const auto c0 = std::chrono::steady_clock::now();
-    if (!t.spec.count(cluster) && t.threads > 1 && t.ci >= 0 && t.parallel_ok) {
-        std::vector<uint64_t> batch{cluster};
-        speculate(t, batch, (size_t)t.threads);
-        if ((t.rc = solve_parallel(t, batch))) return nullptr;
-    }
     auto sp = t.spec.find(cluster);
+    if (sp == t.spec.end() && t.pool) {
+        t.pool->submit(cluster, true);
+        if (t.ci >= 0) {  // the first sweep: keep about two searches per thread queued
+            const size_t want = 2 * (size_t)t.threads, have = t.pool->pending();
+            std::vector<uint64_t> more;
+            if (have < want) speculate(t, more, want - have);
+            for (uint64_t m : more) t.pool->submit(m, false);
+        }
+        ClusterRun R;
+        bool ok = false;
+        t.pool->take(cluster, R, ok);
+        if (!ok) {
+            t.rc = set_err(t.c, ULG_ERR_UNSUPPORTED, "pattern-database group larger than 24 variables");
+            return nullptr;
+        }
+        Triplet::SpecResult spr;
+        spr.nexp = R.nexp;
+        spr.hang = R.hang;
+        if ((t.rc = cluster_parents_of(t, R, spr.op))) return nullptr;
+        sp = t.spec.emplace(cluster, std::move(spr)).first;
+    }
     std::vector<uint64_t> op;
     int64_t nexp;
     if (sp != t.spec.end()) {
@@ -592,6 +721,11 @@ extern "C" int ulg_triplet_astar(ulg_ctx *c, const uint64_t *edges, int pd_count
     t.memo = memo_for(s, pd_count);
     init_skeleton(t, edges);
     set_parallel(t);
+    SearchPool pool;  // its destructor cancels and joins whatever still runs
+    if (t.parallel_ok) {
+        pool.start(s, pd_count, t.threads);
+        t.pool = &pool;
+    }
     for (int i = 0; i < n && !t.rc; ++i) {
         const uint64_t pin = t.nb[i];
         std::vector<int> unc;
@@ -631,6 +765,21 @@ extern "C" int ulg_triplet_astar(ulg_ctx *c, const uint64_t *edges, int pd_count
                 if (!((t.dg(i, j) || t.dg(j, i)) && !bit(t.nb[i], j))) continue;
                 ++delta;
                 t.add_edge(i, j);
+                if (t.pool) {
+                    // the clusters this edge's triples ask for are fixed until
+                    // the next add_edge: queue them all, in asking order
+                    for (int k = 0; k < n; ++k) {
+                        if (k == i || k == j || !(bit(t.clusters[i], k) || bit(t.clusters[j], k))) continue;
+                        int a[3] = {i, j, k};
+                        std::sort(a, a + 3);
+                        const uint64_t key = ((uint64_t)a[0] << 40) + ((uint64_t)a[1] << 20) + (uint64_t)a[2];
+                        const uint64_t big = t.clusters[i] | t.clusters[j] | t.clusters[k];
+                        if (__builtin_popcountll(big) > kMaxCluster || t.checked.count(key) || t.memo->count(big) ||
+                            t.spec.count(big))
+                            continue;
+                        t.pool->submit(big, false);
+                    }
+                }
                 for (int k = 0; k < n; ++k)
                     if (k != i && k != j && (bit(t.clusters[i], k) || bit(t.clusters[j], k))) process_triple(t, i, j, k);
             }
