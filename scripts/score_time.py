@@ -15,7 +15,7 @@ ctx = ulg.Context(0)
 ctx.load(X, 2.0)
 full = [(1 << n) - 1] * n
 for _ in range(5):
-    ctx.score(list(range(n)), full, k)
+    stored, scored = ctx.score(list(range(n)), full, k)
 best = 1e9
 for rep in range(3):
     t = time.perf_counter()
@@ -23,4 +23,5 @@ for rep in range(3):
     for _ in range(K):
         ctx.score(list(range(n)), full, k)
     best = min(best, (time.perf_counter() - t) / K)
-print(f"{os.environ.get('ULG_LIB', 'default')} c3 {best * 1e3:.4f} ms per call", flush=True)
+print(f"{os.environ.get('ULG_LIB', 'default')} c3 {best * 1e3:.4f} ms per call, {stored} of {scored} stored",
+      flush=True)

@@ -444,6 +444,9 @@ __device__ __forceinline__ void best_subset_stack(uint32_t Ptop, uint32_t pvtop,
     }
 }
 
+#ifndef ULG_PRES_NB
+#define ULG_PRES_NB 0  // > 0: subsets per batch of branch-free gathers (measured no faster, r2an/r2ao)
+#endif
 // Presence of every key with a fully unrolled subset loop: the rank of each
 // subset t of the Q local bits is a compile-time sum of per-(bit, position)
 // binomials preloaded into registers.  Q = L when variable 0 is in P (local
@@ -462,6 +465,47 @@ __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi,
     uint64_t off[L + 1];
 #pragma unroll
     for (int pc = 1; pc <= L; ++pc) off[pc] = toffv[pc];
+#if ULG_PRES_NB > 0
+    // Branch-free, in batches of ULG_PRES_NB subsets: every load of a batch
+    // is issued before the first is used.  (Skipping the subsets with local
+    // bit 0 when variable 0 is no candidate with a branch serialised the
+    // gathers: one L2 round trip per subset.)  Those subsets read a valid
+    // slot instead and their bits are masked out.
+    const float *safe = table + off[1];
+#pragma clang loop unroll(full)
+    for (uint32_t t0 = 1; t0 < (1u << Q); t0 += ULG_PRES_NB) {
+        float v[ULG_PRES_NB];
+#pragma unroll
+        for (uint32_t j = 0; j < ULG_PRES_NB; ++j) {
+            const uint32_t t = t0 + j;
+            const int pc = __builtin_popcount(t);
+            if (t >= (1u << Q) || pc > L || t == Plocal) continue;
+            if (pc == L && (PHASE == 0 || !(t & 1u))) continue;
+            uint64_t rk = 0;
+            int jj = 0;
+#pragma unroll
+            for (int b = 0; b < Q; ++b)
+                if ((t >> b) & 1u) {
+                    ++jj;
+                    rk += RB[b][jj];
+                }
+            const float *p = table + off[pc] + rk;
+            if (t & 1u) p = z ? p : safe;
+            v[j] = *p;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < ULG_PRES_NB; ++j) {
+            const uint32_t t = t0 + j;
+            const int pc = __builtin_popcount(t);
+            if (t >= (1u << Q) || pc > L || t == Plocal) continue;
+            if (pc == L && (PHASE == 0 || !(t & 1u))) continue;
+            const bool ok = !(t & 1u) || z;
+            // the absent sentinel is a NaN: never >= thr
+            present.w[t >> 6] |= (uint64_t)(ok && fbits(v[j]) != kAbsentBits) << (t & 63);
+            hi.w[t >> 6] |= (uint64_t)(ok && v[j] >= thr) << (t & 63);
+        }
+    }
+#else
 #pragma clang loop unroll(full)
     for (uint32_t t = 1; t < (1u << Q); ++t) {
         const int pc = __builtin_popcount(t);
@@ -480,6 +524,7 @@ __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi,
         if (fbits(val) != kAbsentBits) present.set(t);
         if (val >= thr) hi.set(t);  // the absent sentinel is a NaN: never >= thr
     }
+#endif
 }
 
 struct ScoreArgs {
