@@ -454,6 +454,10 @@ __device__ __forceinline__ void best_subset_stack(uint32_t Ptop, uint32_t pvtop,
 template <int L, int PHASE, int Q, int W>
 __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi, float thr, const uint32_t *binom,
                                                   uint64_t cpack, bool z, const float *table, const uint64_t *toffv) {
+#ifdef ULG_PROBE_NOPRES
+    // timing probe only (wrong lists, scripts/r2ap.sh): the scorer's floor without the gathers and walks
+    return;
+#endif
     constexpr uint32_t Plocal = (Q == L) ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
     uint32_t RB[Q][L + 1];
 #pragma unroll
