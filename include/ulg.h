@@ -112,6 +112,19 @@ int ulg_cbic_score_vars(ulg_ctx *ctx, const int *vars, int nv,
                         uint64_t *sets, float *scores, int64_t *offsets,
                         int64_t cap);
 
+/* Per-call counterpart of ScoringFunction::calculateScore(variable, parents,
+ * cache) (scoring_function.h:16-23, BIC_OLS.cpp:174-276): for each pair
+ * (vars[i], parents[i]) the value it returns, -float(the_score) with
+ * the_score = N ln(RSS/N) + lambda ln(N) |P| (calculateScoreAndBeta,
+ * BIC_OLS.cpp:277-388; no parents -> -0.0f), batched on the device from the
+ * loaded Gram matrix with the layer scorer's Cholesky, so a stored set's value
+ * equals what ulg_cbic_score stored for it.  The variable's own bit is
+ * ignored (parent_vec skips it).  The cache insertion rule (store iff the
+ * value is < 0 and no subset dominates) stays with ulg_cbic_score, which
+ * applies it layer by layer.  At most 31 parents per set. */
+int ulg_cbic_score_sets(ulg_ctx *ctx, int64_t count, const int *vars,
+                        const uint64_t *parents, float *neg_scores);
+
 /* The .pss "%f" + atof round trip the A* input goes through
  * (score_main.cpp:191, score_cache.cpp:151), computed exactly on the
  * device: cost = float(-1 * strtod(printf("%f", score))). */

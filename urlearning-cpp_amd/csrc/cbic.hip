@@ -2227,6 +2227,70 @@ __global__ void quantize_kernel(const float *in, float *out, int64_t count) {
     if (i < count) out[i] = quantize_score(in[i]);
 }
 
+// ScoringFunction::calculateScore's return value for arbitrary (variable,
+// parent set) pairs (BIC_OLS.cpp:174-276 via calculateScoreAndBeta, :277-388):
+// -float(N ln(RSS/N) + lambda ln(N) |P|), 0 parents -> -0.0f (BIC_OLS.cpp:
+// 300-303).  One lane per pair, parents in ascending order (parent_vec), the
+// Cholesky in the layer kernels' operation order, so a stored set's value is
+// the one ulg_cbic_score stored for it.
+__global__ void __launch_bounds__(kBlock) score_sets_kernel(const double *gram, const uint64_t *pairs, int64_t count,
+                                                            int n, double N, double lambda, float *out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double *g = reinterpret_cast<double *>(smem);
+    for (int i = threadIdx.x; i < n * n; i += kBlock) g[i] = gram[i];
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= count) return;
+    const int v = (int)pairs[2 * i];
+    const uint64_t P = pairs[2 * i + 1] & ~(1ull << v);
+    const int L = __builtin_popcountll(P);
+    if (L == 0) {
+        out[i] = -0.0f;
+        return;
+    }
+    int gv[kWideMax];
+    {
+        uint64_t rem = P;
+        for (int j = 0; j < L; ++j) {
+            gv[j] = __builtin_ctzll(rem);
+            rem &= rem - 1;
+        }
+    }
+    double Lm[kWideMax * (kWideMax + 1) / 2];
+    double y[kWideMax];
+    for (int r = 0; r < L; ++r) {
+        for (int j = 0; j <= r; ++j) Lm[r * (r + 1) / 2 + j] = g[gv[r] * n + gv[j]];
+        y[r] = g[gv[r] * n + v];
+    }
+    const double cvv = g[v * n + v];
+    for (int j = 0; j < L; ++j) {
+        const int rj = j * (j + 1) / 2;
+        double s = Lm[rj + j];
+        for (int k = 0; k < j; ++k) s -= Lm[rj + k] * Lm[rj + k];
+        const double d = sqrt(s);
+        Lm[rj + j] = d;
+        const double inv = 1.0 / d;
+        for (int r = j + 1; r < L; ++r) {
+            const int rr = r * (r + 1) / 2;
+            double t = Lm[rr + j];
+            for (int k = 0; k < j; ++k) t -= Lm[rr + k] * Lm[rj + k];
+            Lm[rr + j] = t * inv;
+        }
+    }
+    double yy = 0.0;
+    for (int r = 0; r < L; ++r) {
+        const int rr = r * (r + 1) / 2;
+        double t = y[r];
+        for (int k = 0; k < r; ++k) t -= Lm[rr + k] * y[k];
+        t = t / Lm[rr + r];
+        y[r] = t;
+        yy += t * t;
+    }
+    const double rss = cvv - yy;
+    const double the_score = N * log(rss / N) + lambda * log(N) * (double)L - 0.0;  // BIC_OLS.cpp:366
+    out[i] = -(float)the_score;
+}
+
 using KernelFn = void (*)(ScoreArgs);
 template <int L, int V>
 KernelFn pick_phase(int phase) {
@@ -3143,6 +3207,35 @@ int ulg_cbic_score_vars(ulg_ctx *c, const int *vars, int nv, const uint64_t *can
     if (rc) return rc;
     if (stored > cap) return set_err(c, ULG_ERR_ARG, "ulg_cbic_score_vars: output capacity too small");
     return ulg_cbic_fetch(c, sets, scores, offsets, 0);
+}
+
+int ulg_cbic_score_sets(ulg_ctx *c, int64_t count, const int *vars, const uint64_t *parents, float *neg_scores) {
+    if (!c || count < 0 || (count > 0 && (!vars || !parents || !neg_scores))) return ULG_ERR_ARG;
+    if (!c->loaded) return set_err(c, ULG_ERR_STATE, "ulg_cbic_score_sets: call ulg_cbic_load first");
+    if (count == 0) return ULG_OK;
+    const int n = c->n;
+    const uint64_t allmask = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+    std::vector<uint64_t> pairs((size_t)count * 2);
+    for (int64_t i = 0; i < count; ++i) {
+        if (vars[i] < 0 || vars[i] >= n) return set_err(c, ULG_ERR_ARG, "ulg_cbic_score_sets: variable out of range");
+        if (parents[i] & ~allmask) return set_err(c, ULG_ERR_ARG, "ulg_cbic_score_sets: parent bit >= n");
+        if (__builtin_popcountll(parents[i] & ~(1ull << vars[i])) > kWideMax)
+            return set_err(c, ULG_ERR_UNSUPPORTED, "ulg_cbic_score_sets: more than ULG_MAX_PARENTS_GPU (31) parents");
+        pairs[2 * i] = (uint64_t)vars[i];
+        pairs[2 * i + 1] = parents[i];
+    }
+    ULG_HIP(c, hipSetDevice(c->device));
+    int rc;
+    if ((rc = ensure(c, c->d_sets_in, (size_t)count * 2)) || (rc = ensure(c, c->qbuf_out, (size_t)count))) return rc;
+    ULG_HIP(c, hipMemcpyAsync(c->d_sets_in.p, pairs.data(), (size_t)count * 16, hipMemcpyHostToDevice, c->stream));
+    prof_begin(c, "score_sets");
+    score_sets_kernel<<<(unsigned)((count + kBlock - 1) / kBlock), kBlock, (size_t)n * n * 8, c->stream>>>(
+        c->gram.p, c->d_sets_in.p, count, n, c->N, c->lambda, c->qbuf_out.p);
+    prof_end(c);
+    ULG_HIP(c, hipMemcpyAsync(neg_scores, c->qbuf_out.p, (size_t)count * 4, hipMemcpyDeviceToHost, c->stream));
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    return ULG_OK;
 }
 
 int ulg_quantize_costs(ulg_ctx *c, const float *scores, float *costs, int64_t count) {

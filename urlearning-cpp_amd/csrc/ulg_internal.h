@@ -106,6 +106,7 @@ struct ulg_ctx {
     ulg::DevBuf<int64_t> out_offsets;
 
     ulg::DevBuf<float> qbuf_in, qbuf_out;
+    ulg::DevBuf<uint64_t> d_sets_in;              // ulg_cbic_score_sets: (variable, parent mask) pairs
 
     // ---- search side (best-score tables, pattern database, A*) ----
     ulg::SearchState *search = nullptr;

@@ -41,6 +41,7 @@ def lib():
         L.ulg_cbic_score.argtypes = [P, P, I, P, I, C.POINTER(I64), C.POINTER(I64)]
         L.ulg_cbic_fetch.argtypes = [P, P, P, P, I]
         L.ulg_cbic_score_vars.argtypes = [P, P, I, P, I, P, P, P, I64]
+        L.ulg_cbic_score_sets.argtypes = [P, I64, P, P, P]
         L.ulg_quantize_costs.argtypes = [P, P, P, I64]
         L.ulg_search_load.argtypes = [P, I, P, P, P]
         L.ulg_search_from_scores.argtypes = [P]
@@ -158,6 +159,16 @@ class Context:
     def score_all(self, variables, candidates, max_parents: int):
         st, _ = self.score(variables, candidates, max_parents)
         return self.fetch(st)
+
+    def score_sets(self, variables, parents) -> np.ndarray:
+        """ScoringFunction::calculateScore's value per (variable, parent mask) pair (ulg_cbic_score_sets)."""
+        v = np.ascontiguousarray(variables, dtype=np.int32)
+        p = np.ascontiguousarray(parents, dtype=np.uint64)
+        if v.shape != p.shape:
+            raise ValueError("score_sets: variables and parents differ in length")
+        out = np.empty(max(len(v), 1), dtype=np.float32)
+        self._check(lib().ulg_cbic_score_sets(self._h, len(v), _ptr(v), _ptr(p), _ptr(out)), "ulg_cbic_score_sets")
+        return out[:len(v)]
 
     def quantize(self, scores: np.ndarray) -> np.ndarray:
         s = np.ascontiguousarray(scores, dtype=np.float32)
