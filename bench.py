@@ -73,7 +73,8 @@ def cpu_baseline(cfg, X, target_s=15.0):
     import oracle
     oracle.build()
     n, k, lam = cfg["n"], cfg["k"], cfg["lam"]
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1))
+    # T = nproc: the CPUs this process may run on
+    threads = max(1, len(os.sched_getaffinity(0)))
     nvars = min(n, threads)
     variables = list(range(nvars))
     cands = [(1 << n) - 1] * n
@@ -87,6 +88,7 @@ def cpu_baseline(cfg, X, target_s=15.0):
     c = oracle.score_sample(ds, lam, variables, cands, k, frac, threads)
     dt = time.perf_counter() - t0
     return {"value": c / dt, "unit": "parent-set scores/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
+            "cpu_quota": cpu_quota(),
             "sample": f"CPU oracle (C restatement, per-set OLS over all N rows) on {nvars} of {n} variables, "
                       f"first {frac:.4f} of every layer 1..{k} in Gosper order: {c} parent sets in {dt:.2f} s "
                       f"on {threads} threads"}
@@ -173,14 +175,16 @@ def search_roofline(cfg, n, pull, reps):
 
 
 def search_metrics(ctx, cfg, variables, cands, rank, ws, reps=3, edges=None, skel_note="full skeleton",
-                   loaded=False):
+                   loaded=False, lists=None):
     """Order-graph search side: GPU best-score tables + pattern database +
     the GPU layer-synchronous search at the bench config (time to the optimal
     order cost; it settles every lattice node, so its rate is lattice nodes/s,
     not A* expansions), then the exact-order A* (the reference's pop order,
-    bit-exact DAG; true A* expansions/s) and the CPU oracle's A* on config C2
-    (rank 0, N=1 only).  loaded: the lists are already in the search state
-    (ulg_search_load_scores after the exchange)."""
+    bit-exact DAG; true A* expansions/s) and a bounded sample of the CPU
+    oracle's A* at the same config (rank 0, N=1 only; exact_astar_legs).
+    loaded: the lists are already in the search state (ulg_search_load_scores
+    after the exchange); lists: the same lists on the host (offsets, sets,
+    scores) for the CPU leg."""
     import time as _t
     n, k = cfg["n"], cfg["k"]
     full = [(1 << n) - 1] * n
@@ -188,7 +192,9 @@ def search_metrics(ctx, cfg, variables, cands, rank, ws, reps=3, edges=None, ske
     out = {}
     tables_ms = tables_again_ms = None
     if not loaded:
-        ctx.score(list(range(n)), full if edges is None else ulg.candidates_from_edges(edges, n), k)
+        stored, _ = ctx.score(list(range(n)), full if edges is None else ulg.candidates_from_edges(edges, n), k)
+        if lists is None and rank == 0 and ws == 1:
+            lists = ctx.fetch(stored)
         t0 = _t.perf_counter()
         ctx.search_from_scores()
         tables_ms = 1e3 * (_t.perf_counter() - t0)
@@ -226,34 +232,80 @@ def search_metrics(ctx, cfg, variables, cands, rank, ws, reps=3, edges=None, ske
                                  "%d later calls" % (reps - 1)}
     if edges is None and pull is not None:
         out["gpu_search"]["roofline"] = search_roofline(cfg, n, pull, reps)
-    if rank == 0 and ws == 1:
-        c2 = CONFIGS["c2"]
-        n2, N2, k2 = c2["n"], c2["N"], c2["k"]
-        X2, _ = synth.gaussian_sem(n2, N2, 9200)
-        full2 = [(1 << n2) - 1] * n2
-        ctx.load(X2, c2["lam"])
-        ctx.score(list(range(n2)), full2, k2)
-        ctx.search_from_scores()
-        ts = _t.perf_counter()
-        e = ctx.astar(edges=full2, mode=0, net_text=False)
-        dt = _t.perf_counter() - ts
-        out["exact"] = {"config": f"C2 (n={n2}, N={N2}, k={k2}), full skeleton", "expansions": e["expanded"],
-                        "ms": 1e3 * dt, "expansions_per_s": e["expanded"] / dt, "goal_cost": e["cost"],
-                        "note": "reference pop order replayed on the host over GPU-built O(1) tables (incl. table D2H)"}
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle
-        offs, sets, scores = ctx.fetch(ctx.score(list(range(n2)), full2, k2)[0])
-        costs = ctx.quantize(scores)
-        srch = oracle.Search(n2, offs, sets, costs)
-        ts = _t.perf_counter()
-        r = srch.astar(edges=full2)
-        dt = _t.perf_counter() - ts
-        out["cpu_baseline"] = {"value": r["expanded"] / dt, "unit": "A* expansions/s", "cores": 1, "kind": "port",
-                               "cpu": cpu_model(),
-                               "sample": f"CPU oracle A* (sorted-list scans, reference heap) on C2: "
-                                         f"{r['expanded']} expansions in {dt:.2f} s",
-                               "same_dag_as_exact": [int(x) for x in r["vpar"]] == [int(x) for x in e["vpar"]]}
+    if rank == 0 and ws == 1 and lists is not None:
+        out.update(exact_astar_legs(ctx, cfg, skel, lists))
     return out
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def exact_astar_legs(ctx, cfg, skel, lists, oracle_budget_s=15.0):
+    """The headline's A* half at the bench config: the exact-order A*
+    (run_astar_on_one_scc, astar_main.cpp:266-459: the reference's heap and
+    pop order replayed on the host over the GPU-built O(1) tables) from the
+    root push to the goal pop, reported as expansions/s, with its netFile
+    checked against the oracle command lines' (tests/golden/<config>_oracle.json
+    when the config has one); then the CPU oracle's A* (sorted-list scans,
+    reference heap, one thread like the reference) on the same lists for a
+    bounded wall-clock budget (its -r watchdog), reported as expansions/s over
+    that sample with the open-list size it reached."""
+    import time as _t
+    n = cfg["n"]
+    out = {}
+    ts = _t.perf_counter()
+    e = ctx.astar(edges=skel, mode=0, net_text=True)
+    dt = _t.perf_counter() - ts
+    fx = os.path.join(GOLDEN, f"{cfg['id']}_oracle.json")
+    same = None
+    if os.path.exists(fx):
+        ref = json.load(open(fx))
+        same = (e["net_text"] == ref["net_file"] and e["expanded"] == ref["expanded"]
+                and np.float32(e["cost"]).tobytes() == np.float32(ref["goal_cost"]).tobytes())
+    out["exact"] = {"config": f"{cfg['id'].upper()} (n={n}, N={cfg['N']}, k={cfg['k']}), "
+                              + ("full skeleton" if skel == [(1 << n) - 1] * n else "skeleton"),
+                    "expansions": e["expanded"], "ms": 1e3 * dt, "expansions_per_s": e["expanded"] / dt,
+                    "goal_cost": e["cost"],
+                    "same_netfile_cost_expansions_as_oracle_fixture": same,
+                    "oracle_fixture": os.path.relpath(fx, ROOT) if os.path.exists(fx) else None,
+                    "note": "reference pop order replayed on the host over GPU-built O(1) tables; the time "
+                            "includes the successor-cost rows' build and copy (first call)"}
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    offs, sets, scores = lists
+    costs = ctx.quantize(scores)
+    srch = oracle.Search(n, offs, sets, costs)
+    ts = _t.perf_counter()
+    srch.pdb_build(2)
+    pdb_s = _t.perf_counter() - ts
+    ts = _t.perf_counter()
+    r = srch.astar(edges=skel, time_limit_s=oracle_budget_s)
+    dt = _t.perf_counter() - ts
+    full_run = None
+    if os.path.exists(fx):
+        ref = json.load(open(fx))
+        full_run = (f"the oracle's full run of this config (make_c3_fixture.py, build container's CPU): "
+                    f"{ref['expanded']} expansions in {ref['oracle_astar_seconds']:.0f} s = "
+                    f"{ref['expanded'] / ref['oracle_astar_seconds']:.0f} expansions/s")
+    out["cpu_baseline"] = {
+        "value": r["expanded"] / dt, "unit": "A* expansions/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
+        "sample": f"CPU oracle A* (sorted-list getScore scans, hashed generatedNodes, reference heap) on the "
+                  f"{cfg['id'].upper()} lists, stopped by its -r watchdog after {dt:.1f} s: {r['expanded']} "
+                  f"expansions, open list {r['open_list']} nodes "
+                  f"({'goal reached' if not r['out_of_time'] else 'goal not reached'}); PDB build "
+                  f"{pdb_s:.2f} s outside the timed region",
+        "full_run": full_run,
+        "expansions_reached_fraction_of_exact": r["expanded"] / max(e["expanded"], 1)}
+    return out
+
+
+def cpu_quota():
+    """The cgroup CPU bandwidth limit (cpu.max), which can be far below nproc:
+    threads beyond it time-share."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_model():
@@ -485,6 +537,7 @@ def sharded_search(ctx, cfg, ex, variables, cands, rows, skel_note, rank, ws, di
     search (replicas).  Ranks must agree on the lists (digest) and
     the goal cost."""
     n = cfg["n"]
+    host_lists = None
     if ex is not None:
         stored, _ = ctx.score(variables, cands, cfg["k"])
         ex.fill(ctx, stored)
@@ -500,6 +553,7 @@ def sharded_search(ctx, cfg, ex, variables, cands, rows, skel_note, rank, ws, di
     else:
         stored, _ = ctx.score(variables, cands, cfg["k"])
         offs, sets, scores = ctx.fetch(stored)
+        host_lists = (offs, sets, scores)
         t0 = t1 = time.perf_counter()
 
         def load():
@@ -510,7 +564,8 @@ def sharded_search(ctx, cfg, ex, variables, cands, rows, skel_note, rank, ws, di
     tb = time.perf_counter()
     load()  # again, with the tables already allocated (3.4 GB at C3)
     tc = time.perf_counter()
-    out = search_metrics(ctx, cfg, variables, cands, rank, ws, edges=rows, skel_note=skel_note, loaded=True)
+    out = search_metrics(ctx, cfg, variables, cands, rank, ws, edges=rows, skel_note=skel_note, loaded=True,
+                         lists=host_lists)
     out["gpu_search"].update(assemble_ms=1e3 * (t1 - t0), tables_ms=1e3 * (tb - ta), tables_rebuild_ms=1e3 * (tc - tb))
     out["lists_sha256"] = digest
     if dist and ws > 1 and rows is None:

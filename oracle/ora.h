@@ -114,6 +114,11 @@ typedef struct ora_search ora_search;
 ora_search *ora_search_create(int n, const int64_t *offsets,
                               const ora_varset *sets, const float *costs);
 void ora_search_free(ora_search *s);
+/* wall-clock budget of ora_astar / ora_astar_scc (the reference's -r
+ * watchdog); 0 = none.  ora_search_out_of_time: the last search stopped on it */
+void ora_search_set_time_limit(ora_search *s, double seconds);
+int ora_search_out_of_time(const ora_search *s);
+int64_t ora_search_last_open(const ora_search *s);
 /* SparseParentList::getScore (sparse_parent_list.cpp:44-55): first entry
  * whose set is a subset of S; FLT_MAX if none.  *parents gets that set. */
 float ora_bestscore(ora_search *s, int v, ora_varset S, ora_varset *parents);

@@ -20,6 +20,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 typedef struct { vs_t set; float cost; int64_t idx; } spl_entry;
 
@@ -44,7 +45,22 @@ struct ora_search {
     int pd_count;
     vs_t ancestors, scc;
     pdb_group *groups;
+    double time_limit_s; /* -r (astar_main.cpp:135-138,696-706): 0 = none */
+    int out_of_time;
+    int64_t last_open; /* open-list size when the last search ended */
 };
+
+static double now_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+/* the -r watchdog: the search loop ends (outOfTime, astar_main.cpp:266)
+ * once the budget is spent; the expansions so far are still reported */
+void ora_search_set_time_limit(ora_search *s, double seconds) { s->time_limit_s = seconds; }
+int ora_search_out_of_time(const ora_search *s) { return s->out_of_time; }
+int64_t ora_search_last_open(const ora_search *s) { return s->last_open; }
 
 static int cmp_spl(const void *a, const void *b) {
     const spl_entry *x = (const spl_entry *)a, *y = (const spl_entry *)b;
@@ -437,7 +453,13 @@ static int run_astar_one(ora_search *s, const vs_t *edges, int skeleton_good,
     const vs_t allVariables = ancestors | the_scc;
     const float upperBound = FLT_MAX;
     int64_t nodesExpanded = 0;
+    const double t_end = s->time_limit_s > 0 ? now_s() + s->time_limit_s : 0.0;
+    s->out_of_time = 0;
     while (open.size > 0) {
+        if (t_end > 0 && (nodesExpanded & 1023) == 0 && now_s() > t_end) {
+            s->out_of_time = 1;
+            break;
+        }
         node_t *u = hp_pop(&open);
         nodesExpanded++;
         const vs_t variables = u->sub;
@@ -477,6 +499,7 @@ static int run_astar_one(ora_search *s, const vs_t *edges, int skeleton_good,
         }
     }
     *expanded += nodesExpanded;
+    s->last_open = open.size;
     if (open.hang) *hang = 1;
     int ok = 0;
     if (goal) {

@@ -59,6 +59,10 @@ def lib():
         L.ora_search_create.argtypes = [I, P, P, P]
         L.ora_search_create.restype = P
         L.ora_search_free.argtypes = [P]
+        L.ora_search_set_time_limit.argtypes = [P, D]
+        L.ora_search_out_of_time.argtypes = [P]
+        L.ora_search_last_open.argtypes = [P]
+        L.ora_search_last_open.restype = I64
         L.ora_bestscore.argtypes = [P, I, U64, C.POINTER(U64)]
         L.ora_bestscore.restype = F
         L.ora_pdb_build.argtypes = [P, I, U64, U64]
@@ -213,8 +217,11 @@ class Search:
         k = lib().ora_pdb_groups(self.h, _p(g), 64)
         return [int(x) for x in g[:k]]
 
-    def astar(self, edges=None, pd_count=2, ancestors=None, scc=None):
+    def astar(self, edges=None, pd_count=2, ancestors=None, scc=None, time_limit_s=0.0):
+        """time_limit_s > 0: the reference's -r watchdog; the result's
+        out_of_time says the search stopped on it (expanded = pops so far)."""
         n = self.n
+        lib().ora_search_set_time_limit(self.h, float(time_limit_s))
         vpar = np.zeros(n, dtype=np.uint64)
         order = np.zeros(n, dtype=np.int32)
         cost = C.c_float()
@@ -231,7 +238,8 @@ class Search:
                                      int(scc) if scc is not None else (1 << n) - 1, _p(vpar), _p(order),
                                      C.byref(cost), C.byref(exp), buf, len(buf))
         return {"rc": rc, "vpar": vpar, "order": order, "cost": cost.value, "expanded": exp.value,
-                "net_text": buf.value.decode()}
+                "net_text": buf.value.decode(), "out_of_time": bool(lib().ora_search_out_of_time(self.h)),
+                "open_list": lib().ora_search_last_open(self.h)}
 
 
 def triplet(search, edges=None, pd_count=2):

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Generate tests/golden/c3_oracle.json: the CPU oracle's command-line path
 at BASELINE config C3 (n=25, N=10k, k=6, lambda=2, full skeleton, seeded
-synthetic data synth.gaussian_sem(25, 10000, 9200)).
+synthetic data synth.gaussian_sem(25, 10000, 9200)); with --config c2 the
+same for C2 (n=20, N=10k, k=4) into tests/golden/c2_oracle.json, which
+__graft_entry__.smoke() checks.
 
   ref_score c3.csv c3.pss -f cBIC --lambda 2 -p 6 -t T   (score_main.cpp)
   ref_astar c3.pss -n c3_net                             (astar_main.cpp)
@@ -11,7 +13,7 @@ parent sets (sorted uint64 masks), the sum of the printed scores, and the
 oracle's netFile / netFile.csv text with the goal cost and the expansion
 count.  tests/test_gpu_c3_dag.py checks the GPU pipeline against it.
 Runs in this container only (it needs oracle/build/ and a few minutes of
-CPU): python tests/golden/make_c3_fixture.py [workdir] [threads]
+CPU): python tests/golden/make_c3_fixture.py [--config c2|c3] [workdir] [threads]
 """
 import hashlib
 import json
@@ -25,7 +27,7 @@ sys.path.insert(0, os.path.join(ROOT, "urlearning-cpp_amd"))
 import numpy as np  # noqa: E402
 import synth  # noqa: E402
 
-N_VARS, N_ROWS, K, LAM, SEED = 25, 10000, 6, 2.0, 9200
+CONFIGS = {"c3": (25, 10000, 6, 2.0, 9200), "c2": (20, 10000, 4, 2.0, 9200)}
 
 
 def pss_sets(path):
@@ -60,12 +62,17 @@ def sets_digest(masks):
 
 
 def main():
-    work = sys.argv[1] if len(sys.argv) > 1 else "/tmp/c3ref"
-    threads = sys.argv[2] if len(sys.argv) > 2 else str(os.cpu_count() or 8)
+    argv = sys.argv[1:]
+    cfg = "c3"
+    if argv[:1] == ["--config"]:
+        cfg, argv = argv[1], argv[2:]
+    N_VARS, N_ROWS, K, LAM, SEED = CONFIGS[cfg]
+    work = argv[0] if len(argv) > 0 else f"/tmp/{cfg}ref"
+    threads = argv[1] if len(argv) > 1 else str(os.cpu_count() or 8)
     os.makedirs(work, exist_ok=True)
-    csv = os.path.join(work, "c3.csv")
-    pss = os.path.join(work, "c3_ref.pss")
-    net = os.path.join(work, "c3_ref_net")
+    csv = os.path.join(work, f"{cfg}.csv")
+    pss = os.path.join(work, f"{cfg}_ref.pss")
+    net = os.path.join(work, f"{cfg}_ref_net")
     if not os.path.exists(net):
         X, _ = synth.gaussian_sem(N_VARS, N_ROWS, SEED)
         synth.write_csv(csv, X)
@@ -79,14 +86,15 @@ def main():
     expanded = int(re.search(r"Nodes expanded: (\d+)", log).group(1))
     ref_time = float(re.search(r"ref_astar: time=(\S+)s", log).group(1))
     per_var = pss_sets(pss)
-    res = {"config": "C3: n=25, N=10000, k=6, lambda=2, full skeleton, synth.gaussian_sem(25, 10000, 9200)",
+    res = {"config": f"{cfg.upper()}: n={N_VARS}, N={N_ROWS}, k={K}, lambda={LAM:g}, full skeleton, "
+                     f"synth.gaussian_sem({N_VARS}, {N_ROWS}, {SEED})",
            "generator": "tests/golden/make_c3_fixture.py (oracle/build/ref_score -t T, ref_astar)",
            "stored_per_variable": [len(m) for m, _ in per_var],
            "sets_sha256_per_variable": [sets_digest(m) for m, _ in per_var],
            "printed_score_sum_per_variable": [s for _, s in per_var],
            "goal_cost": cost, "expanded": expanded, "oracle_astar_seconds": ref_time,
            "net_file": open(net).read(), "net_csv": open(net + ".csv").read()}
-    out = os.path.join(ROOT, "tests", "golden", "c3_oracle.json")
+    out = os.path.join(ROOT, "tests", "golden", f"{cfg}_oracle.json")
     json.dump(res, open(out, "w"), indent=1)
     print(f"wrote {out}: {sum(res['stored_per_variable'])} stored sets, cost {cost}, {expanded} expansions")
 
