@@ -312,8 +312,8 @@ int ulg_sweep_shard_end(ulg_ctx *ctx, uint64_t *vpar, int *order, float *goal_co
  * subsets; the hi bitset in HBM above 2^19); 2 replays every walk that way.
  * All variants compute identical results; the knob exists for A/B timing. */
 int ulg_set_option(ulg_ctx *ctx, const char *name, int64_t value);
-/* Read-back of per-call state: "out_of_time" (1 if the last ulg_cbic_score or
- * ulg_astar* ran out of time_limit_ms), "highest_completed_layer" (the
+/* Read-back of per-call state: "out_of_time" (1 if the last ulg_cbic_score,
+ * ulg_astar* or ulg_triplet_astar ran out of time_limit_ms), "highest_completed_layer" (the
  * reference's ScoreCalculator::highestCompletedLayer of the last scoring call,
  * score_calculator.h:45). */
 int ulg_get_info(ulg_ctx *ctx, const char *name, int64_t *value);

@@ -185,10 +185,11 @@ def test_cli_c1_hepatitis_default_parent_limit(tmp_path):
     os.remove(pss)
 
 
-def test_triplet_cli_rejects_running_time():
-    """triplet_astar's watchdog (triplet_astar.cpp:141,355) would end every
-    later A* of the driver without a goal -- a clock-dependent MEC -- so -r > 0
-    is refused loudly instead of being ignored."""
-    r = subprocess.run([os.path.join(PKG, "bin", "triplet_astar"), "x.pss", "-r", "5"], capture_output=True,
+def test_triplet_cli_accepts_running_time():
+    """triplet_astar -r is the reference's flag (triplet_astar.cpp:1647,
+    1674-1681): accepted and announced as the reference does, before the
+    score file is read."""
+    r = subprocess.run([os.path.join(PKG, "bin", "triplet_astar"), "missing.pss", "-r", "5"], capture_output=True,
                        text=True, timeout=60)
-    assert r.returncode == 2 and "not supported" in r.stderr
+    assert "Maximum running time: 5" in r.stdout
+    assert r.returncode == 1 and "not supported" not in r.stderr

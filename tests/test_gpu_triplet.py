@@ -218,3 +218,38 @@ def test_triplet_look_ahead_threads_equal_sequential(ulg_ctx, oracle_built, monk
     for r in res.values():
         assert r["mec"].tolist() == ref["mec"].tolist()
         assert (r["runs"], r["distinct"], r["expanded"]) == (ref["runs"], ref["distinct"], ref["expanded"])
+
+
+def test_triplet_running_time_budget(ulg_ctx):
+    """triplet_astar -r (triplet_astar.cpp:1674-1681): once the watchdog has
+    fired every A* of the driver ends without a goal (:139-142,355,657-662),
+    so process_triple sees the empty optimal-parents vectors of :855 and
+    orients nothing -- memoised clusters included, which the reference would
+    search again.  A budget spent before the first search leaves only the
+    isolated orphan edges (:1166-1178); a generous one changes nothing."""
+    n = 14
+    X, W = synth.gaussian_sem(n, 3000, 9412)
+    rows = [r & ~(1 << i) for i, r in enumerate(synth.true_skeleton_edges(W, 0.1, 9412))]
+    ulg_ctx.load(X, 2.0)
+    ulg_ctx.score(list(range(n)), ulg.candidates_from_edges(rows, n), 4)
+    ulg_ctx.search_from_scores()
+    full = ulg_ctx.triplet(edges=rows)
+    assert ulg_ctx.info("out_of_time") == 0
+    try:
+        ulg_ctx.set_option("time_limit_ms", 600000)
+        same = ulg_ctx.triplet(edges=rows)
+        assert ulg_ctx.info("out_of_time") == 0 and same["mec"].tolist() == full["mec"].tolist()
+        ulg_ctx.set_option("time_limit_ms", 1)
+        import time
+        time.sleep(0.01)
+        cut = ulg_ctx.triplet(edges=rows)
+        assert ulg_ctx.info("out_of_time") == 1
+        assert cut["distinct"] == 0 and cut["expanded"] == 0 and cut["runs"] > 0
+        mec = cut["mec"]
+        assert (mec == mec.T).all(), "only undirected orphan edges survive"
+        for i in range(n):
+            for j in range(n):
+                if mec[i, j]:
+                    assert (rows[i] >> j) & 1 and bin(rows[i]).count("1") == 1 and bin(rows[j]).count("1") == 1
+    finally:
+        ulg_ctx.set_option("time_limit_ms", 0)

@@ -61,6 +61,18 @@ struct Triplet {
     int num_v_structures = 0;
     bool hang = false;
     int rc = ULG_OK;
+    // the -r watchdog (triplet_astar.cpp:139-142,355,1674-1681): once the
+    // budget is spent every A* ends without a goal ("No solution found",
+    // :657-662), so process_triple sees the empty op of :855 -- also for
+    // clusters solved before, which the reference would search again
+    bool timed = false;
+    std::chrono::steady_clock::time_point deadline;
+    const std::vector<uint64_t> *no_solution() {
+        static const std::vector<uint64_t> none(64, 0);
+        c->out_of_time = 1;
+        return &none;
+    }
+    bool past_deadline() const { return timed && std::chrono::steady_clock::now() > deadline; }
 
     bool dg(int a, int b) const { return bit(out[a], b); }
     void set(int a, int b, bool v) {
@@ -521,6 +533,7 @@ void speculate(Triplet &t, std::vector<uint64_t> &batch, size_t want) {
 
 const std::vector<uint64_t> *cluster_parents(Triplet &t, uint64_t cluster) {
     ++t.runs;
+    if (t.past_deadline()) return t.no_solution();
     auto it = t.memo->find(cluster);
     if (it != t.memo->end()) return &it->second;
     static const bool trace = std::getenv("ULG_TRIPLET_TRACE") != nullptr;  // per-search progress on stderr
@@ -564,6 +577,9 @@ const std::vector<uint64_t> *cluster_parents(Triplet &t, uint64_t cluster) {
         std::fprintf(stderr, "triplet: cluster %016llx (%d variables): %lld expansions in %.3f s\n",
                      (unsigned long long)cluster, __builtin_popcountll(cluster), (long long)nexp,
                      std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count());
+    // a search the budget ran out during: the reference's loop stopped
+    // without a goal (its result is not kept)
+    if (t.past_deadline()) return t.no_solution();
     ++t.distinct;
     return &t.memo->emplace(cluster, std::move(op)).first->second;
 }
@@ -719,6 +735,11 @@ extern "C" int ulg_triplet_astar(ulg_ctx *c, const uint64_t *edges, int pd_count
     t.n = n;
     t.pd_count = pd_count;
     t.memo = memo_for(s, pd_count);
+    c->out_of_time = 0;
+    if (c->time_limit_ms > 0) {
+        t.timed = true;
+        t.deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(c->time_limit_ms);
+    }
     init_skeleton(t, edges);
     set_parallel(t);
     SearchPool pool;  // its destructor cancels and joins whatever still runs
