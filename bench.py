@@ -483,10 +483,15 @@ def main():
             c = time.perf_counter()
             ts_score.append(b - a)
             ts_ex.append(c - b)
+        stored_bytes = sum(ex.counts) * (ex.w + 4)
         split = {"score_ms": 1e3 * float(np.median(ts_score)), "exchange_ms": 1e3 * float(np.median(ts_ex)),
                  "exchange_bytes_per_rank": ex.block, "exchange_bytes_total": ex.block * ws,
-                 "block_capacity_sets": ex.cap,
-                 "note": "medians of synchronised steps after the timed region (rank-local clocks)"}
+                 "block_capacity_sets": ex.cap, "a_priori_capacity_sets": ex.bound,
+                 "stored_sets_total": sum(ex.counts), "stored_bytes_total": stored_bytes,
+                 "exchange_over_stored_bytes": ex.block * ws / max(stored_bytes, 1), "regathers": ex.regathers,
+                 "note": "medians of synchronised steps after the timed region (rank-local clocks); blocks "
+                         "sized by the learned capacity (the largest rank's stored count + 2% + 256 sets; the "
+                         "first exchange used the a-priori bound)"}
 
     search = None
     if args.mode == "shard" and not args.no_search:

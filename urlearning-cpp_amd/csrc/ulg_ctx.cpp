@@ -1,4 +1,5 @@
 // ulg_ctx.cpp -- context lifecycle, errors, profiling for libulg.so.
+#include <mutex>
 #include <cstdio>
 #include <cstring>
 
@@ -7,7 +8,11 @@
 namespace ulg {
 
 int set_err(ulg_ctx *c, int code, const std::string &msg) {
-    if (c) c->err = msg;
+    if (c) {
+        // the wide scoring layers run one host thread per stream group
+        std::lock_guard<std::mutex> lk(c->mu);
+        c->err = msg;
+    }
     return code;
 }
 
@@ -45,9 +50,14 @@ uint64_t binom64(int a, int b) {
 void prof_begin(ulg_ctx *c, const char *name) { prof_begin_s(c, name, c->stream); }
 void prof_end(ulg_ctx *c) { prof_end_s(c, c->stream); }
 
+// The record a thread's prof_end_s closes: its own last prof_begin_s (the
+// wide scoring layers drive their stream groups from several host threads).
+thread_local int64_t t_prof_rec = -1;
+
 void prof_begin_s(ulg_ctx *c, const char *name, hipStream_t stream) {
-    c->prof_skip = !c->prof || (!c->prof_only.empty() && !c->prof_only.count(name));
-    if (c->prof_skip) return;
+    t_prof_rec = -1;
+    if (!c->prof || (!c->prof_only.empty() && !c->prof_only.count(name))) return;
+    std::lock_guard<std::mutex> lk(c->mu);
     ProfRec r;
     r.name = name;
     // events come from a per-context pool: creating two per kernel costs more
@@ -61,12 +71,15 @@ void prof_begin_s(ulg_ctx *c, const char *name, hipStream_t stream) {
         }
     }
     (void)hipEventRecord(r.start, stream);
+    t_prof_rec = (int64_t)c->pending.size();
     c->pending.push_back(r);
 }
 
 void prof_end_s(ulg_ctx *c, hipStream_t stream) {
-    if (c->prof_skip || c->pending.empty()) return;
-    (void)hipEventRecord(c->pending.back().stop, stream);
+    if (t_prof_rec < 0) return;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (t_prof_rec < (int64_t)c->pending.size()) (void)hipEventRecord(c->pending[(size_t)t_prof_rec].stop, stream);
+    t_prof_rec = -1;
 }
 
 void prof_collect(ulg_ctx *c) {

@@ -1,6 +1,7 @@
 // ulg_internal.h -- shared host-side state of the MI355X URLearning path.
 #pragma once
 
+#include <mutex>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -118,7 +119,7 @@ struct ulg_ctx {
     bool prof = false;
     std::vector<ulg::ProfRec> pending;
     std::set<std::string> prof_only;  // ulg_profile_select: time only these kernels
-    bool prof_skip = false;
+    std::mutex mu;  // err / pending: the wide scoring layers use one host thread per stream group
     std::vector<hipEvent_t> event_pool;
     ulg::Mirror mir_tbl_off, mir_work, mir_cand, mir_meta, mir_workg, mir_hoff;
     ulg::DevBuf<float> d_hmax;      // wide walks: hi-cover tables (subset max of the present keys), then the present keys

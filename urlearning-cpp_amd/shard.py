@@ -10,9 +10,11 @@ first.  `ListExchange` then runs the ONE collective of the data path: an
 all-gather (RCCL over xGMI on MI355X; gloo in the CPU tests) of fixed-size
 per-rank blocks.  A block holds the rank's local offsets followed by its
 stored sets and scores, written straight from the scorer's device buffers
-(ulg_cbic_fetch with device pointers).  Block capacity is the a-priori bound
-"every scored set is stored", which every rank computes from (candidates, k),
-so no count exchange precedes the data.  After the gather every rank holds
+(ulg_cbic_fetch with device pointers).  The first exchange sizes the blocks
+by the a-priori bound "every scored set is stored", which every rank
+computes from (candidates, k), so no count exchange precedes the data; the
+headers carry the counts, and later exchanges use the learned capacity
+(ListExchange).  After the gather every rank holds
 every variable's list in variable order, ready for ulg_search_load_scores
 (local best-score tables + search) or a .pss writer.
 
@@ -116,24 +118,42 @@ class ListExchange:
       [0, hdr)                   int64 local offsets[nv_r + 1] (ulg_cbic_fetch)
       [hdr, hdr + w cap)         stored sets: uint32 when n <= 32 (w = 4), else uint64 (w = 8)
       [hdr + w cap, + 4 cap)     float32 scores
-    cap = max over ranks of sum_{v in rank} var_weight (every scored set
-    stored), so a rank's lists always fit and no counts travel first.  With
-    n <= 32 a set is its low 32 bits, so the block carries 8 B per set
-    instead of 12 (a third less on the wire); the sets are fetched into a
-    staging buffer and narrowed on the device."""
+    With n <= 32 a set is its low 32 bits, so the block carries 8 B per set
+    instead of 12; the sets are fetched into a staging buffer and narrowed on
+    the device.
 
-    def __init__(self, n: int, parts, candidates, k: int, rank: int, device="cuda", comm_device=None):
+    Capacity.  The first exchange uses the a-priori bound "every scored set
+    stored" (max over ranks of sum_{v in rank} var_weight), which needs no
+    count exchange.  Every block's header carries its rank's stored count, so
+    after each gather every rank knows every count and the next exchanges use
+    a learned capacity: the largest count plus `slack` (at C3 the stored lists
+    are a third of the scored sets, so the blocks shrink about 3x).  A rank
+    whose lists outgrow the capacity sends its header only; every rank sees
+    that in the gathered headers, all grow the capacity to the largest count
+    and gather once more (a second collective only then)."""
+
+    def __init__(self, n: int, parts, candidates, k: int, rank: int, device="cuda", comm_device=None,
+                 learn=True, slack=0.02):
         self.n, self.parts, self.rank, self.ws = n, parts, rank, len(parts)
         self.mine = parts[rank]
         bounds = [sum(var_weight(n, v, candidates[v], k) for v in p) for p in parts]
-        self.cap = max(max(bounds), 1)
+        self.bound = max(max(bounds), 1)  # the a-priori capacity
+        self.learn, self.slack = learn, slack
         maxnv = max(len(p) for p in parts)
         self.narrow = n <= 32
         self.w = 4 if self.narrow else 8
         self.hdr = 16 * ((8 * (maxnv + 1) + 15) // 16)
-        self.block = 16 * ((self.hdr + (self.w + 4) * self.cap + 15) // 16)
         self.device = torch.device(device)
         self.comm_device = torch.device(comm_device) if comm_device is not None else self.device
+        self.regathers = 0  # exchanges that had to grow the capacity and gather again
+        self.counts = None  # every rank's stored count at the last gather
+        self._src = None
+        self._next = None  # learned capacity, adopted by the next fill
+        self._resize(self.bound)
+
+    def _resize(self, cap: int):
+        self.cap = max(int(cap), 1)
+        self.block = 16 * ((self.hdr + (self.w + 4) * self.cap + 15) // 16)
         self.buf = torch.zeros(self.block, dtype=torch.uint8, device=self.device)
         self.out = torch.empty(self.ws * self.block, dtype=torch.uint8, device=self.comm_device)
         base = self.buf.data_ptr()
@@ -152,44 +172,85 @@ class ListExchange:
             return raw.view(torch.int64)
         return raw.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
 
+    def _write(self):
+        """Fill the send block from the remembered source (header only when
+        the lists do not fit)."""
+        kind, a, b = self._src
+        if kind == "ctx":
+            ctx, stored = a, b
+            if stored <= self.cap:
+                ctx.fetch_device(self.sets_ptr, self.scores_ptr, self.offs_ptr)
+                if self.narrow:
+                    # low 32 bits of each set (little endian), on the device
+                    lo = self.stage.view(torch.int32).view(-1, 2)[:, 0]
+                    self.buf[self.hdr:self.hdr + 4 * self.cap].view(torch.int32).copy_(lo)
+            else:  # header only: the offsets, through buffers that hold the lists
+                tmp_sets = torch.empty(max(stored, 1), dtype=torch.int64, device=self.device)
+                tmp_scores = torch.empty(max(stored, 1), dtype=torch.float32, device=self.device)
+                ctx.fetch_device(tmp_sets.data_ptr(), tmp_scores.data_ptr(), self.offs_ptr)
+            return
+        offsets, sets, scores = a
+        cnt = int(offsets[-1])
+        b = np.zeros(self.block, dtype=np.uint8)
+        b[:8 * len(offsets)] = offsets.view(np.uint8)
+        if cnt <= self.cap:
+            st = np.asarray(sets[:cnt], dtype=np.uint64)
+            if self.narrow:
+                if cnt and int(st.max()) >> 32:
+                    raise RuntimeError("shard: a set above bit 31 with n <= 32")
+                st = st.astype(np.uint32)
+            b[self.hdr:self.hdr + self.w * cnt] = st.view(np.uint8)
+            o = self.hdr + self.w * self.cap
+            b[o:o + 4 * cnt] = np.asarray(scores[:cnt], dtype=np.float32).view(np.uint8)
+        self.buf.copy_(torch.from_numpy(b))
+
+    def _adopt(self):
+        # the learned capacity replaces the blocks (the previous gather's
+        # output is no longer needed once the next fill starts)
+        if self._next is not None and self._next < self.cap:
+            self._resize(self._next)
+        self._next = None
+
     def fill(self, ctx, stored: int):
         """Write this rank's lists (the last ctx.score over self.mine) into
         the send block, straight from the scorer's device buffers."""
-        if stored > self.cap:
-            raise RuntimeError(f"shard block overflow: {stored} stored > capacity {self.cap}")
-        ctx.fetch_device(self.sets_ptr, self.scores_ptr, self.offs_ptr)
-        if self.narrow:
-            # low 32 bits of each set (little endian), on the device
-            lo = self.stage.view(torch.int32).view(-1, 2)[:, 0]
-            self.buf[self.hdr:self.hdr + 4 * self.cap].view(torch.int32).copy_(lo)
+        self._adopt()
+        self._src = ("ctx", ctx, int(stored))
+        self._write()
 
     def fill_host(self, offsets, sets, scores):
         """Same from host lists (local offsets[nv_r + 1], sets, scores), e.g.
         the CPU oracle's in the gloo tests."""
+        self._adopt()
         offsets = np.asarray(offsets, dtype=np.int64)
-        cnt = int(offsets[-1])
-        if cnt > self.cap:
-            raise RuntimeError(f"shard block overflow: {cnt} stored > capacity {self.cap}")
-        b = np.zeros(self.block, dtype=np.uint8)
-        b[:8 * len(offsets)] = offsets.view(np.uint8)
-        st = np.asarray(sets[:cnt], dtype=np.uint64)
-        if self.narrow:
-            if cnt and int(st.max()) >> 32:
-                raise RuntimeError("shard: a set above bit 31 with n <= 32")
-            st = st.astype(np.uint32)
-        b[self.hdr:self.hdr + self.w * cnt] = st.view(np.uint8)
-        o = self.hdr + self.w * self.cap
-        b[o:o + 4 * cnt] = np.asarray(scores[:cnt], dtype=np.float32).view(np.uint8)
-        self.buf.copy_(torch.from_numpy(b))
+        self._src = ("host", (offsets, sets, scores), None)
+        self._write()
 
-    def allgather(self, group=None):
-        """The data-path collective: one all-gather of fixed-size blocks."""
+    def _gather(self, group):
         src = self.buf if self.comm_device == self.device else self.buf.to(self.comm_device)
         if self.comm_device.type != "cpu":
             dist.all_gather_into_tensor(self.out, src, group=group)
         else:
             parts = list(self.out.view(self.ws, self.block).unbind(0))
             dist.all_gather(parts, src, group=group)
+
+    def _read_counts(self):
+        hdr = self.out.view(self.ws, self.block)[:, :self.hdr].cpu().numpy().view(np.int64)
+        return [int(hdr[r, len(p)]) for r, p in enumerate(self.parts)]
+
+    def allgather(self, group=None):
+        """The data-path collective: one all-gather of fixed-size blocks
+        (a second one only if some rank's lists outgrew the capacity)."""
+        self._gather(group)
+        self.counts = self._read_counts()  # one small D2H of the headers
+        need = max(self.counts)
+        if need > self.cap:
+            self.regathers += 1
+            self._resize(need + int(self.slack * need) + 256)
+            self._write()
+            self._gather(group)
+            self.counts = self._read_counts()
+        self._next = need + int(self.slack * need) + 256 if self.learn else None
         return self.out
 
     def assemble(self, device=None):
