@@ -310,6 +310,15 @@ int ulg_sweep_shard_end(ulg_ctx *ctx, uint64_t *vpar, int *order, float *goal_co
  * "wide_lds" (0/1/2, default 1): walks longer than 2^6 steps are replayed by
  * one workgroup each with their skip / hi bitsets in LDS (2^q <= 2^20 local
  * subsets; the hi bitset in HBM above 2^19); 2 replays every walk that way.
+ * "wide_pool" (0/1, default 1): with score_streams > 1 the wide layers run
+ * variable by variable on score_streams host threads, largest candidate set
+ * first (0: every group's part of a layer together, the slowest group
+ * holding the next layer).
+ * "wide_host" (iterations, default 4096, 0 = never): an LDS replay still
+ * walking after that many iterations stops and is replayed from the start on
+ * a host thread over the same bitsets (one wave issues at most one
+ * instruction every 4 cycles; a host core runs the same sequential walk tens
+ * of times faster).
  * All variants compute identical results; the knob exists for A/B timing. */
 int ulg_set_option(ulg_ctx *ctx, const char *name, int64_t value);
 /* Read-back of per-call state: "out_of_time" (1 if the last ulg_cbic_score,

@@ -20,6 +20,9 @@ def main():
     n, N = 30, 100000
     X, _ = synth.gaussian_sem(n, N, 9200)
     ctx = ulg.Context(0)
+    for kv in filter(None, os.environ.get("ULG_OPTS", "").split(",")):  # A/B knobs: name=value,...
+        a, b = kv.split("=")
+        ctx.set_option(a, int(b))
     ctx.load(X, 2.0)
     rows = ctx.mmpc(0.01)
     cands = ulg.candidates_from_edges(rows, n)

@@ -147,6 +147,40 @@ def test_wide_hicover_prune_identical_lists(ulg_ctx):
         assert out[0][2].tobytes() == o[2].tobytes()
 
 
+@pytest.mark.timeout(300)
+def test_wide_pool_identical_lists_c4(ulg_ctx):
+    """ulg_set_option("wide_pool"): the wide layers variable by variable on
+    score_streams host threads (default) or every stream group's part of a
+    layer together; "wide_host": LDS replays past that many iterations
+    finish on host threads (1: every replay does, so host_walk re-decides
+    all of them; 0: none).  All 30 C4 variables (n=30, N=100k, MMPC,
+    -p = n-1; the wide layers reach 18) give bit-identical lists in every
+    combination, and the pool's repeat call too."""
+    import ulg
+    n, N = 30, 100000
+    X, _ = synth.gaussian_sem(n, N, 9200)
+    ulg_ctx.load(X, 2.0)
+    rows = ulg_ctx.mmpc(0.01)
+    cands = ulg.candidates_from_edges(rows, n)
+    vs = list(range(n))
+    out = []
+    try:
+        for pool, streams, host in ((0, 3, 0), (1, 3, 4096), (1, 3, 4096), (1, 2, 4096), (1, 3, 1), (0, 1, 64)):
+            ulg_ctx.set_option("wide_pool", pool)
+            ulg_ctx.set_option("score_streams", streams)
+            ulg_ctx.set_option("wide_host", host)
+            offs, sets, scores = ulg_ctx.score_all(vs, [cands[v] for v in vs], n - 1)
+            out.append((np.asarray(offs).copy(), np.asarray(sets).copy(), np.asarray(scores).copy()))
+    finally:
+        ulg_ctx.set_option("wide_pool", 1)
+        ulg_ctx.set_option("score_streams", 3)
+        ulg_ctx.set_option("wide_host", 4096)
+    for o in out[1:]:
+        assert np.array_equal(out[0][0], o[0])
+        assert np.array_equal(out[0][1], o[1])
+        assert out[0][2].tobytes() == o[2].tobytes()
+
+
 @pytest.mark.timeout(400)
 def test_c1_hepatitis_reference_defaults_lambda_half(ulg_ctx):
     """Config C1 at the reference's defaults: lambda 0.5 (score_main.cpp:214)

@@ -21,6 +21,8 @@
 //     rank of the set inside the variable's candidate list (= the Gosper
 //     enumeration index), holding the stored score or an absent sentinel.
 #include <cstdio>
+#include <atomic>
+#include <thread>
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -28,6 +30,7 @@
 #include <cstring>
 
 #include "search_internal.h"
+#include "host_walk.h"
 
 using namespace ulg;
 
@@ -1741,32 +1744,26 @@ inline uint64_t strag_budget() {
 }
 constexpr int kStragThreads = 256;             // fill threads (64 when many walks share the GPU); wave 0 walks
 constexpr uint64_t kStragWide = 4096;          // replays per launch from which blocks are one wave
-constexpr int kStragDepth = 24;
-constexpr int kStragState = kStragDepth * 32 + 32;  // frames (2 x 16 B), lc
-constexpr uint64_t kStragIterCap = 1ull << 32;
 
-template <int PHASE, bool HI_LDS>
-__global__ void __launch_bounds__(kStragThreads) walk_wide_lds_kernel(WideArgs a, const uint64_t *sq,
-                                                                      uint64_t *hig, unsigned long long *err,
-                                                                      unsigned long long *wstats) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// The fill of one replay (entry e of the straggler queue) into skip / hib
+// (word w at skip[w * stride], hib[w * stride]): lc (>= 32 bytes) and xlow
+// (64 words), shared by the block, receive the local-bit -> compact index
+// map and the compact masks of the 64 low-bit patterns.  Every thread of the
+// block takes words w = tid, tid + nthreads, ...
+template <int PHASE>
+__device__ __forceinline__ void strag_fill(const WideArgs &a, const uint64_t *e, uint64_t *skip, uint64_t *hib,
+                                           uint32_t stride, uint8_t *lc, uint64_t *xlow, uint32_t tid,
+                                           uint32_t nthreads) {
     const int L = a.L;
     const int q = PHASE == 0 ? L : L + 1;
     const uint32_t nw = (1u << q) >> 6;
-    uint64_t *skip = reinterpret_cast<uint64_t *>(smem);
-    uint64_t *hib = HI_LDS ? skip + nw : hig + (uint64_t)blockIdx.x * nw;
-    uint4 *frames = reinterpret_cast<uint4 *>(skip + (HI_LDS ? 2 * nw : nw));
-    uint8_t *lc = reinterpret_cast<uint8_t *>(frames + kStragDepth);
-    const uint64_t *e = sq + 3 * (uint64_t)blockIdx.x;
-    const uint64_t slot = e[0], cm = e[1];
+    const uint64_t cm = e[1];
     const int vi = (int)(uint32_t)e[2];
-    const float ts = __uint_as_float((uint32_t)(e[2] >> 32));
-    const float thr = -ts;
+    const float thr = -__uint_as_float((uint32_t)(e[2] >> 32));
     const bool z = a.meta[vi * 4 + 2] != 0;
     const uint64_t zb = z ? 1ull : 0ull;
     const uint64_t ho = a.hoff[vi];
-    const uint64_t tk0 = wstats ? wall_clock64() : 0;
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
         uint64_t rem = cm;
         const int first = PHASE == 0 ? 0 : 1;
         lc[0] = 0;
@@ -1776,14 +1773,20 @@ __global__ void __launch_bounds__(kStragThreads) walk_wide_lds_kernel(WideArgs a
         }
     }
     __syncthreads();
-    for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) {
+    if (tid < 64) {  // compact mask of local bits 1..5 of pattern tid (bit 0 = variable 0: zb)
+        uint64_t X = 0;
+        for (uint32_t y = tid & ~1u; y; y &= y - 1) X |= 1ull << lc[__builtin_ctz(y)];
+        xlow[tid] = X | ((tid & 1u) ? zb : 0ull);
+    }
+    __syncthreads();
+    for (uint32_t w = tid; w < nw; w += nthreads) {
         uint64_t sw = 0, hw = 0;
         uint64_t Xw = 0;  // compact mask of the word's high local bits
         for (uint32_t y = (w << 6); y; y &= y - 1) Xw |= 1ull << lc[__builtin_ctz(y)];
+#pragma unroll 8
         for (int b = 0; b < 64; ++b) {
             const uint32_t t = (w << 6) | (uint32_t)b;
-            uint64_t X = Xw | ((t & 1u) ? zb : 0ull);  // local bit 0 = variable 0
-            for (uint32_t y = (uint32_t)b & ~1u; y; y &= y - 1) X |= 1ull << lc[__builtin_ctz(y)];
+            const uint64_t X = Xw | xlow[b];
             bool pres = false, hi = false;
             if (!(PHASE == 1 && (t & 1u) && !z)) {
                 const float val = a.pval[ho + X];
@@ -1796,10 +1799,50 @@ __global__ void __launch_bounds__(kStragThreads) walk_wide_lds_kernel(WideArgs a
             if (sk) sw |= 1ull << b;
             if (hi && t != 0) hw |= 1ull << b;
         }
-        skip[w] = sw;
-        hib[w] = hw;
+        skip[(uint64_t)w * stride] = sw;
+        hib[(uint64_t)w * stride] = hw;
     }
     __syncthreads();
+}
+
+// The fills of the replays handed to the host (one block each, entries
+// sq[3 * idx[b]]), written to out: [b][skip nw words][hi nw words].
+template <int PHASE>
+__global__ void __launch_bounds__(256) strag_fill_global_kernel(WideArgs a, const uint64_t *sq, const uint32_t *idx,
+                                                                uint64_t *out) {
+    __shared__ uint8_t lc[64];
+    __shared__ uint64_t xlow[64];
+    const int q = PHASE == 0 ? a.L : a.L + 1;
+    const uint64_t nw = ((uint64_t)1 << q) >> 6;
+    uint64_t *o = out + (uint64_t)blockIdx.x * 2 * nw;
+    strag_fill<PHASE>(a, sq + 3 * (uint64_t)idx[blockIdx.x], o, o + nw, 1, lc, xlow, threadIdx.x, blockDim.x);
+}
+
+// host_budget > 0: a walk still running after that many iterations stops,
+// and its queue index goes to hq (count *hqc) for the host (host_walk):
+// one wave issues at most one instruction every 4 cycles, so a long
+// sequential walk runs far faster on a host core.
+template <int PHASE, bool HI_LDS>
+__global__ void __launch_bounds__(kStragThreads) walk_wide_lds_kernel(WideArgs a, const uint64_t *sq,
+                                                                      uint64_t *hig, unsigned long long *err,
+                                                                      unsigned long long *wstats, uint64_t host_budget,
+                                                                      uint32_t *hq, unsigned int *hqc, uint32_t qbase) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int L = a.L;
+    const int q = PHASE == 0 ? L : L + 1;
+    const uint32_t nw = (1u << q) >> 6;
+    // HI_LDS: skip and hi words interleaved (one 16-B read per neighbour);
+    // else skip in LDS and hi in this block's global scratch
+    constexpr uint32_t kS = HI_LDS ? 2u : 1u;
+    uint64_t *skip = reinterpret_cast<uint64_t *>(smem);
+    uint64_t *hib = HI_LDS ? skip + 1 : hig + (uint64_t)blockIdx.x * nw;
+    uint64_t *xlow = skip + (HI_LDS ? 2 * nw : nw);
+    uint8_t *lc = reinterpret_cast<uint8_t *>(xlow + 64);
+    const uint64_t *e = sq + 3 * (uint64_t)blockIdx.x;
+    const uint64_t slot = e[0];
+    const float ts = __uint_as_float((uint32_t)(e[2] >> 32));
+    const uint64_t tk0 = wstats ? wall_clock64() : 0;
+    strag_fill<PHASE>(a, e, skip, hib, kS, lc, xlow, threadIdx.x, blockDim.x);
     if (threadIdx.x >= 64) return;
     // wave 0 walks, every lane in step (the walk state is wave-uniform); the
     // lanes only split up to read a node's neighbour bits: bit l of sm / hm is
@@ -1808,16 +1851,26 @@ __global__ void __launch_bounds__(kStragThreads) walk_wide_lds_kernel(WideArgs a
     // re-read after each child returns and every test is a register bit test.
     const int lane = threadIdx.x;
     const uint64_t tk1 = wstats ? wall_clock64() : 0;
-    auto rfl = [](uint32_t v) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
     // lanes >= q read a valid word too, so both loads issue back to back
     const uint32_t lbit = 1u << (lane < q ? lane : 0);
     auto nbr = [&](uint32_t Nn, uint32_t &sm_, uint32_t &hm_) {
         const uint32_t t = Nn ^ lbit;
-        const uint64_t sw = skip[t >> 6], hw = hib[t >> 6];
+        uint64_t sw, hw;
+        if constexpr (HI_LDS) {
+            const ulonglong2 v = *reinterpret_cast<const ulonglong2 *>(skip + 2 * (t >> 6));
+            sw = v.x;
+            hw = v.y;
+        } else {
+            sw = skip[t >> 6];
+            hw = hib[t >> 6];
+        }
         sm_ = (uint32_t)__ballot((int)(((sw >> (t & 63)) & 1ull) | (lane >= q)));
         hm_ = (uint32_t)__ballot((int)(((hw >> (t & 63)) & 1ull) & (lane < q)));
     };
-    uint4 *fext = reinterpret_cast<uint4 *>(lc + 32);  // per frame: hm, sm
+    // frames in VGPR lanes: lane d of fN .. fSm holds frame d (kStragDepth <= 64)
+    uint32_t fN = 0, fRem = 0, fB = 0, fW = 0, fHm = 0, fSm = 0;
+    auto wl = [&](uint32_t v, int l, uint32_t old) -> uint32_t { return lane == l ? v : old; };
+    auto rl = [](uint32_t v, int l) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); };
     const uint32_t P = PHASE == 0 ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
     uint32_t N = P, rem = P, B = 0, sm, hm;
     nbr(N, sm, hm);
@@ -1829,13 +1882,17 @@ __global__ void __launch_bounds__(kStragThreads) walk_wide_lds_kernel(WideArgs a
             if (lane == 0) atomicOr(err, 1ull);
             break;
         }
+        if (host_budget && it > host_budget) {  // to the host, from the start
+            if (lane == 0) hq[atomicAdd(hqc, 1u)] = qbase + blockIdx.x;
+            return;
+        }
         int y;
         if (pend) {  // call 1's position-1 test: the zero padding, variable 0
             pend = false;
             y = 0;
         } else {
             if (incall) {  // the call returned: checked.insert(N)
-                if (lane == 0) atomicOr(&skip[N >> 6], 1ull << (N & 63));
+                if (lane == 0) atomicOr(&skip[(N >> 6) * kS], 1ull << (N & 63));
                 incall = false;
             }
             // Next test that is not a no-op.  A test whose node has its skip
@@ -1905,14 +1962,12 @@ __global__ void __launch_bounds__(kStragThreads) walk_wide_lds_kernel(WideArgs a
                 const int cx = x;
                 const bool cmarked = js > 0;
                 --d;
-                const uint4 f = frames[d];
-                const uint4 g = fext[d];
-                N = rfl(f.x);
-                rem = rfl(f.y);
-                B = rfl(f.z);
-                const uint32_t w = rfl(f.w);
-                hm = rfl(g.x);
-                sm = rfl(g.y);
+                N = rl(fN, d);
+                rem = rl(fRem, d);
+                B = rl(fB, d);
+                const uint32_t w = rl(fW, d);
+                hm = rl(fHm, d);
+                sm = rl(fSm, d);
                 x = (int)(w & 31u);
                 zr = (int)((w >> 5) & 31u);
                 js = (int)((w >> 10) & 31u);
@@ -1940,12 +1995,14 @@ __global__ void __launch_bounds__(kStragThreads) walk_wide_lds_kernel(WideArgs a
             if (lane == 0) atomicOr(err, 1ull);
             break;
         }
-        if (lane == 0) {
-            frames[d] = make_uint4(N, rem, B,
-                                   (uint32_t)x | ((uint32_t)zr << 5) | ((uint32_t)js << 10) |
-                                       ((uint32_t)pend << 15) | ((uint32_t)incall << 16));
-            fext[d] = make_uint4(hm, sm, 0u, 0u);
-        }
+        fN = wl(N, d, fN);
+        fRem = wl(rem, d, fRem);
+        fB = wl(B, d, fB);
+        fW = wl((uint32_t)x | ((uint32_t)zr << 5) | ((uint32_t)js << 10) | ((uint32_t)pend << 15) |
+                    ((uint32_t)incall << 16),
+                d, fW);
+        fHm = wl(hm, d, fHm);
+        fSm = wl(sm, d, fSm);
         ++d;
         N ^= 1u << y;
         x = y;
@@ -2465,21 +2522,98 @@ struct WideGroup {
     WideArgs wa;
     std::vector<int> hm;  // hi-cover launch metadata (kept until its copy ran)
     uint64_t qn = 0;
+    uint32_t *hq = nullptr;      // replays handed to the host (indices into the straggler queue)
+    unsigned int *hqc = nullptr;
 };
 
+constexpr uint64_t kHostFewReplays = 64;  // launches of at most this many replays ...
+constexpr uint64_t kHostFewBudget = 512;   // ... hand walks to the host after this many iterations
+
+// The replays walk_wide_lds_kernel handed over (more than c->wide_host
+// iterations): their fills again into the group's bitset slice, one copy
+// back, the walks on host threads, the decisions written into the table.
+int host_walks(ulg_ctx *c, WideGroup &G, int L, int ph, int q, uint64_t sn, uint64_t slice,
+               unsigned long long *errf) {
+    const auto th0 = std::chrono::steady_clock::now();
+    unsigned int cnt = 0;
+    ULG_HIP(c, hipMemcpyAsync(&cnt, G.hqc, 4, hipMemcpyDeviceToHost, G.st));
+    ULG_HIP(c, hipStreamSynchronize(G.st));
+    if (cnt == 0) return ULG_OK;
+    if (cnt > sn) return set_err(c, ULG_ERR_STATE, "ulg_cbic_score: host walk queue overflow");
+    std::vector<uint32_t> idx(cnt);
+    std::vector<uint64_t> ent((size_t)3 * sn);
+    const uint64_t *sq = G.queue + 3 * G.qn;
+    ULG_HIP(c, hipMemcpyAsync(idx.data(), G.hq, (size_t)cnt * 4, hipMemcpyDeviceToHost, G.st));
+    ULG_HIP(c, hipMemcpyAsync(ent.data(), sq, ent.size() * 8, hipMemcpyDeviceToHost, G.st));
+    ULG_HIP(c, hipStreamSynchronize(G.st));
+    const uint64_t nw = ((uint64_t)1 << q) >> 6;
+    const uint64_t per = std::max<uint64_t>(1, slice / (2 * nw));
+    std::vector<uint64_t> bits;
+    std::vector<uint32_t> vals(cnt);
+    std::vector<uint64_t> slots(cnt);
+    for (uint64_t b0 = 0; b0 < cnt; b0 += per) {
+        const uint64_t k = std::min<uint64_t>(per, cnt - b0);
+        // this chunk's queue indices (the kernel's list is on the host now)
+        ULG_HIP(c, hipMemcpyAsync(G.hq, idx.data() + b0, k * 4, hipMemcpyHostToDevice, G.st));
+        prof_begin_s(c, "walk_wide_host_fill", G.st);
+        if (ph == 0) strag_fill_global_kernel<0><<<(unsigned)k, 256, 0, G.st>>>(G.wa, sq, G.hq, G.bits);
+        else strag_fill_global_kernel<1><<<(unsigned)k, 256, 0, G.st>>>(G.wa, sq, G.hq, G.bits);
+        prof_end_s(c, G.st);
+        ULG_HIP(c, hipGetLastError());
+        bits.resize((size_t)(k * 2 * nw));
+        ULG_HIP(c, hipMemcpyAsync(bits.data(), G.bits, bits.size() * 8, hipMemcpyDeviceToHost, G.st));
+        ULG_HIP(c, hipStreamSynchronize(G.st));
+        if (const char *dd = std::getenv("ULG_DUMP_HOSTWALK")) {  // diagnostics: the bitsets of the largest ones
+            static std::atomic<int> nd{0};
+            if (q >= 15 && nd < 16) {
+                char fn[512];
+                std::snprintf(fn, sizeof fn, "%s/hostwalk_%d_L%d_p%d_q%d.bin", dd, nd++, L, ph, q);
+                if (FILE *f = std::fopen(fn, "wb")) {
+                    std::fwrite(bits.data(), 8, 2 * nw, f);
+                    std::fclose(f);
+                }
+            }
+        }
+        std::atomic<uint64_t> next{0};
+        std::atomic<bool> bad{false};
+        auto work = [&]() {
+            for (uint64_t j = next++; j < k; j = next++) {
+                bool e = false;
+                const bool dom = host_walk(L, ph, bits.data() + j * 2 * nw, bits.data() + j * 2 * nw + nw, &e);
+                if (e) bad = true;
+                const uint64_t *en = ent.data() + 3 * (uint64_t)idx[b0 + j];
+                // the stored value is -ts: flip the float's sign bit
+                vals[b0 + j] = dom ? kAbsentBits : ((uint32_t)(en[2] >> 32) ^ 0x80000000u);
+                slots[b0 + j] = en[0];
+            }
+        };
+        const unsigned nth = (unsigned)std::min<uint64_t>(k, std::min(8u, std::max(1u, std::thread::hardware_concurrency())));
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < nth; ++t) th.emplace_back(work);
+        work();
+        for (auto &t : th) t.join();
+        if (bad) {
+            const unsigned long long one = 1;
+            ULG_HIP(c, hipMemcpyAsync(errf, &one, 8, hipMemcpyHostToDevice, G.st));
+        }
+    }
+    for (unsigned j = 0; j < cnt; ++j)
+        ULG_HIP(c, hipMemcpyAsync(G.wa.table + slots[j], &vals[j], 4, hipMemcpyHostToDevice, G.st));
+    ULG_HIP(c, hipStreamSynchronize(G.st));  // vals is about to go
+    static const bool wstat = std::getenv("ULG_WALK_STATS") != nullptr;
+    if (wstat)
+        std::fprintf(stderr, "walk_host_stats L=%d phase=%d q=%d handed=%u of %llu ms=%.2f\n", L, ph, q, cnt,
+                     (unsigned long long)sn,
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count());
+    return ULG_OK;
+}
+
+// pin: 2 * gs.size() pinned words of the caller's (queue lengths, long-walk counts)
 int score_wide_groups(ulg_ctx *c, int L, int ph, std::vector<WideGroup> &gs, int nv, int S, int kmax,
                       unsigned long long *errf, uint64_t slice, const std::vector<uint64_t> &hoff,
-                      const std::vector<int> &meta) {
+                      const std::vector<int> &meta, unsigned long long *pin) {
     const int ng = (int)gs.size();
     const int q = ph == 0 ? L : L + 1;
-    if ((int)c->wide_host.size() < 2 * ng) {
-        if (c->wide_pinned) (void)hipHostFree(c->wide_pinned);
-        c->wide_pinned = nullptr;
-        ULG_HIP(c, hipHostMalloc((void **)&c->wide_pinned, sizeof(unsigned long long) * 2 * (size_t)ng,
-                                 hipHostMallocDefault));
-        c->wide_host.assign(2 * ng, 0);
-    }
-    unsigned long long *pin = c->wide_pinned;
     // 1. scoring launches
     for (int gi = 0; gi < ng; ++gi) {
         WideGroup &G = gs[gi];
@@ -2624,8 +2758,9 @@ int score_wide_groups(ulg_ctx *c, int L, int ph, std::vector<WideGroup> &gs, int
         // this group's checked-bitset slice (free once its walks are done)
         const bool hl = q <= kStragHiLdsQ;
         const uint64_t nw = ((uint64_t)1 << q) >> 6;
-        const size_t lds = (size_t)(hl ? 2 : 1) * nw * 8 + kStragState;
-        using LdsFn = void (*)(WideArgs, const uint64_t *, uint64_t *, unsigned long long *, unsigned long long *);
+        const size_t lds = (size_t)(hl ? 2 : 1) * nw * 8 + 64 * 8 + 64;  // bitsets, xlow, lc
+        using LdsFn = void (*)(WideArgs, const uint64_t *, uint64_t *, unsigned long long *, unsigned long long *,
+                               uint64_t, uint32_t *, unsigned int *, uint32_t);
         const LdsFn kf = ph == 0 ? (hl ? walk_wide_lds_kernel<0, true> : walk_wide_lds_kernel<0, false>)
                                  : (hl ? walk_wide_lds_kernel<1, true> : walk_wide_lds_kernel<1, false>);
         ULG_HIP(c, hipFuncSetAttribute((const void *)kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -2633,6 +2768,12 @@ int score_wide_groups(ulg_ctx *c, int L, int ph, std::vector<WideGroup> &gs, int
         unsigned long long *ws = wstat ? c->d_stats.p : nullptr;
         if (wstat) ULG_HIP(c, hipMemsetAsync(ws, 0, 128, G.st));
         const auto tl0 = std::chrono::steady_clock::now();
+        // walks past this many iterations finish on the host; with few
+        // replays in the launch the host takes them sooner (it runs them in
+        // parallel threads, while the GPU's launch time is its longest walk)
+        const uint64_t hbud = sn <= kHostFewReplays ? std::min<uint64_t>(c->wide_host_iters, kHostFewBudget)
+                                                    : c->wide_host_iters;
+        if (hbud) ULG_HIP(c, hipMemsetAsync(G.hqc, 0, 4, G.st));
         for (uint64_t base = 0; base < sn; base += per) {
             const uint64_t k = std::min<uint64_t>(per, sn - base);
             prof_begin_s(c, "walk_wide_lds", G.st);
@@ -2640,9 +2781,13 @@ int score_wide_groups(ulg_ctx *c, int L, int ph, std::vector<WideGroup> &gs, int
             // (the walk is one wave's; waves 1-3 only speed up the fill)
             const unsigned th = sn >= kStragWide ? 64u : (unsigned)kStragThreads;
             hipLaunchKernelGGL(kf, dim3((unsigned)k), dim3(th), lds, G.st, G.wa,
-                               G.queue + 3 * (G.qn + base), G.bits, errf, ws);
+                               G.queue + 3 * (G.qn + base), G.bits, errf, ws, hbud, G.hq, G.hqc, (uint32_t)base);
             prof_end_s(c, G.st);
             ULG_HIP(c, hipGetLastError());
+        }
+        if (hbud) {
+            int rc2;
+            if ((rc2 = host_walks(c, G, L, ph, q, sn, slice, errf))) return rc2;
         }
         if (wstat) {
             unsigned long long h[16];
@@ -2658,6 +2803,89 @@ int score_wide_groups(ulg_ctx *c, int L, int ph, std::vector<WideGroup> &gs, int
     // the hi-cover metadata vectors must outlive their copies
     for (int gi = 0; gi < ng; ++gi)
         if (!gs[gi].hm.empty()) ULG_HIP(c, hipStreamSynchronize(gs[gi].st));
+    return ULG_OK;
+}
+
+
+// The wide layers L0..kmax of every variable that reaches them, one variable
+// per task on G host threads; thread t drives stream gst[t] with stream group
+// t's queue, counter, bitset and hi-cover-metadata slices.  Results are the
+// grouped form's (a variable's decisions read only its own slabs).
+int wide_pool(ulg_ctx *c, int L0, int G, const std::vector<hipStream_t> &gst, int nv, int S, int kmax,
+              int max_parents, const std::vector<int> &mv, const std::vector<int> &meta,
+              const std::vector<uint64_t> &work, uint64_t wqwords, uint64_t wslice, const std::vector<uint64_t> &hoff,
+              size_t nqc) {
+    // every stream's earlier layers first (the slabs the wide layers read)
+    for (int g = 0; g < G; ++g) ULG_HIP(c, hipStreamSynchronize(gst[g]));
+    std::vector<int> order;
+    for (int i = 0; i < nv; ++i)
+        if (std::min(mv[i], max_parents) >= L0) order.push_back(i);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return mv[a] > mv[b]; });
+    // per-variable launch prefixes: [task][L][phase][nv + 1], only variable i counts
+    const size_t stride = (size_t)(kmax + 1) * 2 * (nv + 1);
+    std::vector<uint64_t> vw(order.size() * stride, 0);
+    for (size_t k = 0; k < order.size(); ++k) {
+        const int i = order[k];
+        for (int L = L0; L <= kmax; ++L)
+            for (int ph = 0; ph < 2; ++ph) {
+                const uint64_t *w = &work[((size_t)L * 2 + ph) * (nv + 1)];
+                uint64_t *o = &vw[k * stride + ((size_t)L * 2 + ph) * (nv + 1)];
+                const uint64_t cnt = w[i + 1] - w[i];
+                for (int j = 0; j <= nv; ++j) o[j] = j > i ? cnt : 0;
+            }
+    }
+    int rc;
+    if ((rc = upload(c, c->d_vwork, c->mir_vwork, vw))) return rc;
+    ULG_HIP(c, hipStreamSynchronize(c->stream));  // the other threads' streams read it next
+    std::atomic<size_t> next{0};
+    std::vector<int> rcs(G, ULG_OK);
+    auto run = [&](int t) {
+        if (hipSetDevice(c->device) != hipSuccess) {
+            rcs[t] = set_err(c, ULG_ERR_HIP, "hipSetDevice failed in a wide-layer thread");
+            return;
+        }
+        for (size_t k = next++; k < order.size(); k = next++) {
+            const int i = order[k];
+            const int top = std::min(mv[i], max_parents);
+            for (int L = L0; L <= top; ++L)
+                for (int ph = 0; ph < 2; ++ph) {
+                    const size_t wo = ((size_t)L * 2 + ph) * (nv + 1);
+                    const uint64_t cnt = vw[k * stride + wo + nv];
+                    if (cnt == 0) continue;
+                    WideGroup wg;
+                    wg.st = gst[t];
+                    wg.d_work = c->d_vwork.p + k * stride + wo;
+                    wg.h_work = vw.data() + k * stride + wo;
+                    wg.cnt = cnt;
+                    wg.queue = c->d_wqueue.p + t * wqwords;
+                    wg.qc = c->d_qcount.p + (size_t)t * 2 * (kmax + 1) + (L * 2 + ph);
+                    wg.scnt = c->d_scount.p + t;
+                    wg.bits = c->d_wbits.p + (size_t)t * wslice;
+                    wg.d_hmeta = hoff.empty() ? nullptr : c->d_hmeta.p + (size_t)t * (nv + (size_t)(nv + 1) * 8);
+                    wg.hq = c->d_hq.p + (size_t)t * std::max<uint64_t>(wqwords / 6, 1);
+                    wg.hqc = c->d_hqc.p + t;
+                    // this slot's counter served the previous variable's launch
+                    if (hipMemsetAsync(wg.qc, 0, 8, wg.st) != hipSuccess) {
+                        rcs[t] = set_err(c, ULG_ERR_HIP, "hipMemsetAsync failed in a wide-layer thread");
+                        return;
+                    }
+                    std::vector<WideGroup> one{std::move(wg)};
+                    const int r = score_wide_groups(c, L, ph, one, nv, S, kmax, c->d_qcount.p + nqc - 1, wslice, hoff,
+                                                    meta, c->wide_pinned + 2 * t);
+                    if (r) {
+                        rcs[t] = r;
+                        next = order.size();  // the other threads stop at their next task
+                        return;
+                    }
+                }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < G; ++t) th.emplace_back(run, t);
+    run(0);
+    for (auto &x : th) x.join();
+    for (int r : rcs)
+        if (r) return r;
     return ULG_OK;
 }
 
@@ -2881,7 +3109,10 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     if (kmax > kMaxL) {
         const uint64_t wpl_max = kmax + 1 <= 6 ? 1ull : (1ull << (kmax + 1 - 6));
         wslice = std::max<uint64_t>(kWideBitsWords / (uint64_t)G, wpl_max);
-        if ((rc = ensure(c, c->d_wbits, (size_t)(G * wslice))) || (rc = ensure(c, c->d_scount, (size_t)G))) return rc;
+        if ((rc = ensure(c, c->d_wbits, (size_t)(G * wslice))) || (rc = ensure(c, c->d_scount, (size_t)G)) ||
+            (rc = ensure(c, c->d_hq, (size_t)G * std::max<uint64_t>(wqwords / 6, 1))) ||
+            (rc = ensure(c, c->d_hqc, (size_t)G)))
+            return rc;
         // hi-cover tables for the variables that reach a wide layer
         if (c->wide_prune) {
             hoff.assign(nv, ~0ull);
@@ -2900,6 +3131,13 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
                 hoff.clear();
             }
         }
+    }
+    if (kmax > kMaxL && (int)c->wide_host.size() < 2 * G) {
+        if (c->wide_pinned) (void)hipHostFree(c->wide_pinned);
+        c->wide_pinned = nullptr;
+        ULG_HIP(c, hipHostMalloc((void **)&c->wide_pinned, sizeof(unsigned long long) * 2 * (size_t)G,
+                                 hipHostMallocDefault));
+        c->wide_host.assign(2 * G, 0);
     }
     // Small layers (L <= Ls, little work, latency-bound): one one-pass launch
     // per phase over all variables on the context stream -- no queue, no walk
@@ -2974,6 +3212,18 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
                 for (int g = 1; g < G; ++g) ULG_HIP(c, hipStreamWaitEvent(gst[g], c->sync_events[0], 0));
                 forked = true;
             }
+            if (L > kMaxL && G > 1 && c->time_limit_ms == 0 && c->wide_pool) {
+                // The wide layers variable by variable on G host threads (one
+                // stream each): a variable's layers depend only on its own
+                // lower layers, and the long LDS replays of one variable no
+                // longer hold every other variable's next layer (the grouped
+                // form waits for each layer's slowest group).  Largest
+                // candidate sets first.
+                if ((rc = wide_pool(c, L, G, gst, nv, S, kmax, max_parents, mv, meta, work, wqwords, wslice, hoff,
+                                    nqc)))
+                    return rc;
+                break;
+            }
             std::vector<WideGroup> wide;  // a wide layer: every group's part, staged together
             for (int g = 0; g < G; ++g) {
                 const size_t wo = (size_t)g * (G > 1 ? wstride : 0) + ((size_t)L * 2 + ph) * (nv + 1);
@@ -2997,6 +3247,8 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
                     wg.scnt = c->d_scount.p + g;
                     wg.bits = c->d_wbits.p + (size_t)g * wslice;
                     wg.d_hmeta = hoff.empty() ? nullptr : c->d_hmeta.p + (size_t)g * (nv + (size_t)(nv + 1) * 8);
+                    wg.hq = c->d_hq.p + (size_t)g * std::max<uint64_t>(wqwords / 6, 1);
+                    wg.hqc = c->d_hqc.p + g;
                     wide.push_back(std::move(wg));
                     continue;
                 }
@@ -3090,10 +3342,11 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
                     }
                 }
             }
-            if (!wide.empty() &&
-                (rc = score_wide_groups(c, L, ph, wide, nv, S, kmax, c->d_qcount.p + nqc - 1, wslice, hoff, meta)))
+            if (!wide.empty() && (rc = score_wide_groups(c, L, ph, wide, nv, S, kmax, c->d_qcount.p + nqc - 1, wslice,
+                                                         hoff, meta, c->wide_pinned)))
                 return rc;
         }
+        if (L > kMaxL && G > 1 && c->time_limit_ms == 0 && c->wide_pool) break;  // the pool ran every wide layer
         if (c->time_limit_ms > 0 && L < kmax) {
             for (int g = 0; g < (forked ? G : 1); ++g) ULG_HIP(c, hipStreamSynchronize(gst[g]));
             const double ms =

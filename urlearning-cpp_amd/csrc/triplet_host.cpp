@@ -599,7 +599,7 @@ std::unordered_map<uint64_t, std::vector<uint64_t>> *memo_for(SearchState &s, in
 void set_parallel(Triplet &t) {
     const char *e = std::getenv("ULG_TRIPLET_THREADS");
     const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
-    t.threads = e ? std::max(1, std::atoi(e)) : std::min(8, hw);
+    t.threads = e ? std::max(1, std::atoi(e)) : std::min(16, hw);
     const uint64_t all = (t.n >= 64) ? ~0ull : ((1ull << t.n) - 1ull);
     t.parallel_ok = t.threads > 1 && t.s->tables_ready && (t.s->scope & all) == all && t.s->table_vars == all &&
                     search_cost_table_host(t.c) == ULG_OK;
@@ -614,6 +614,25 @@ void init_skeleton(Triplet &t, const uint64_t *edges) {
         t.nb[v] = edges ? edges[v] : all;
         t.clusters[v] = t.nb[v] | (1ull << v);
     }
+}
+
+// The distinct clusters the first sweep (triplet_astar.cpp:1148-1204) asks
+// for on the current skeleton, in first-request order (<= 26 variables).
+std::vector<uint64_t> first_sweep_clusters(const Triplet &t) {
+    std::unordered_set<uint64_t> seen;
+    std::vector<uint64_t> out;
+    for (int i = 0; i < t.n; ++i) {
+        std::vector<int> unc;
+        for (int j = 0; j < t.n; ++j)
+            if (bit(t.nb[i], j)) unc.push_back(j);
+        for (size_t j = 0; j < unc.size(); ++j)
+            for (size_t q = 0; q < j; ++q) {
+                const uint64_t big = t.clusters[i] | t.clusters[unc[j]] | t.clusters[unc[q]];
+                if (__builtin_popcountll(big) > kMaxCluster || !seen.insert(big).second) continue;
+                out.push_back(big);
+            }
+    }
+    return out;
 }
 
 // process_triple (triplet_astar.cpp:811-989)
@@ -746,6 +765,19 @@ extern "C" int ulg_triplet_astar(ulg_ctx *c, const uint64_t *edges, int pd_count
     if (t.parallel_ok) {
         pool.start(s, pd_count, t.threads);
         t.pool = &pool;
+        // Every cluster the first sweep will ask for is known now (on the
+        // initial skeleton): queue them all, largest first (a cluster's A*
+        // may expand up to 2^|cluster| nodes), so the longest searches start
+        // at once instead of when the driver first names them.  Orientations
+        // can change later clusters; a result nobody asks for is dropped.
+        if (!std::getenv("ULG_TRIPLET_LOOKAHEAD_ONLY")) {
+            std::vector<uint64_t> first = first_sweep_clusters(t);
+            std::stable_sort(first.begin(), first.end(), [](uint64_t a, uint64_t b) {
+                return __builtin_popcountll(a) > __builtin_popcountll(b);
+            });
+            for (uint64_t cl : first)
+                if (!t.memo->count(cl)) pool.submit(cl, false);
+        }
     }
     for (int i = 0; i < n && !t.rc; ++i) {
         const uint64_t pin = t.nb[i];
@@ -832,20 +864,9 @@ extern "C" int ulg_triplet_clusters(ulg_ctx *c, const uint64_t *edges, uint64_t 
     Triplet t;
     t.n = c->search->n;
     init_skeleton(t, edges);
-    std::unordered_set<uint64_t> seen;
-    int64_t k = 0;
-    for (int i = 0; i < t.n; ++i) {
-        std::vector<int> unc;
-        for (int j = 0; j < t.n; ++j)
-            if (bit(t.nb[i], j)) unc.push_back(j);
-        for (size_t j = 0; j < unc.size(); ++j)
-            for (size_t q = 0; q < j; ++q) {
-                const uint64_t big = t.clusters[i] | t.clusters[unc[j]] | t.clusters[unc[q]];
-                if (__builtin_popcountll(big) > kMaxCluster || !seen.insert(big).second) continue;
-                if (k < cap) clusters[k] = big;
-                ++k;
-            }
-    }
+    const std::vector<uint64_t> first = first_sweep_clusters(t);
+    const int64_t k = (int64_t)first.size();
+    for (int64_t i = 0; i < k && i < cap; ++i) clusters[i] = first[i];
     *count = k;
     return k > cap && cap > 0 ? set_err(c, ULG_ERR_ARG, "ulg_triplet_clusters: cap too small") : ULG_OK;
 }

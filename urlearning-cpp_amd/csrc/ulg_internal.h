@@ -82,6 +82,8 @@ struct ulg_ctx {
     int wide_prune = 1;            // wide walks: skip absent nodes whose subsets hold no key >= -ts
     int wide_reduced = 1;          // wide walks: skip the recursion's no-op re-tests
     int wide_lds = 1;              // wide walks: long ones replayed with their bitsets in LDS
+    int wide_pool = 1;             // wide layers variable by variable on score_streams host threads
+    uint64_t wide_host_iters = 4096;     // LDS replays past this many iterations finish on host threads (0: never)
     int score_xcd = 1;             // scoring kernels: contiguous runs of sets per XCD
     int score_graph = 1;           // scoring call: replay the captured launch sequence
     hipGraph_t graph = nullptr;    // the captured scoring launches, its instance, its key
@@ -102,6 +104,9 @@ struct ulg_ctx {
     ulg::DevBuf<uint64_t> d_queue;                // score_variant bit 4: undecided lanes
     ulg::DevBuf<unsigned long long> d_qcount;
     ulg::DevBuf<uint64_t> d_workg;                // per stream-group work prefixes
+    ulg::DevBuf<uint64_t> d_vwork;                // per-variable work prefixes of the wide-layer pool
+    ulg::DevBuf<uint32_t> d_hq;                   // per stream group: replays handed to the host
+    ulg::DevBuf<unsigned int> d_hqc;
     ulg::DevBuf<uint64_t> out_sets;
     ulg::DevBuf<float> out_scores;
     ulg::DevBuf<int64_t> out_offsets;
@@ -121,7 +126,7 @@ struct ulg_ctx {
     std::set<std::string> prof_only;  // ulg_profile_select: time only these kernels
     std::mutex mu;  // err / pending: the wide scoring layers use one host thread per stream group
     std::vector<hipEvent_t> event_pool;
-    ulg::Mirror mir_tbl_off, mir_work, mir_cand, mir_meta, mir_workg, mir_hoff;
+    ulg::Mirror mir_tbl_off, mir_work, mir_cand, mir_meta, mir_workg, mir_hoff, mir_vwork;
     ulg::DevBuf<float> d_hmax;      // wide walks: hi-cover tables (subset max of the present keys), then the present keys
     uint64_t hmax_half = 0;         // entries of each half of d_hmax
     ulg::DevBuf<uint64_t> d_hoff;   // [nv] table offsets, ~0 = no table
