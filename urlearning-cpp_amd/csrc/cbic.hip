@@ -1119,7 +1119,7 @@ __global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, 
 #pragma unroll
         for (int r = 0; r < S::NV0; ++r) {
             const int t0 = r * S::E;
-            constexpr uint32_t EM = S::E == 32 ? ~0u : ((1u << S::E) - 1u);
+            constexpr uint32_t EM = (uint32_t)((1ull << S::E) - 1ull);
             const uint32_t hb = (uint32_t)(hw[t0 >> 6] >> (t0 & 63)) & EM;
             const uint32_t ob = (uint32_t)(ow[t0 >> 6] >> (t0 & 63)) & EM;
             uint32_t hs, os;
@@ -3160,6 +3160,21 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     const bool use_graph =
         c->score_graph && !c->prof && kmax <= kMaxL && c->time_limit_ms == 0 && !wck && !(variant & 8);
     std::vector<uint64_t> gkey;
+    // An early return between BeginCapture and EndCapture (a failed launch,
+    // "layer too large") must not leave the context stream capturing: the
+    // guard ends the capture, drops the partial graph and the key.
+    struct CaptureGuard {
+        ulg_ctx *c;
+        bool active;
+        ~CaptureGuard() {
+            if (!active) return;
+            hipGraph_t g = nullptr;
+            (void)hipStreamEndCapture(c->stream, &g);
+            if (g) (void)hipGraphDestroy(g);
+            c->gkey.clear();
+            (void)hipGetLastError();
+        }
+    } capture_guard{c, false};
     if (use_graph) {
         gkey.assign({(uint64_t)nv, (uint64_t)max_parents, (uint64_t)variant, (uint64_t)G, (uint64_t)Ls,
                      (uint64_t)c->score_xcd, (uint64_t)n, (uint64_t)c->N, dbits(c->lambda), (uint64_t)c->prof,
@@ -3182,6 +3197,7 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
         }
         graph_reset(c);
         ULG_HIP(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed));
+        capture_guard.active = true;
     }
     {
     const size_t pend0 = c->pending.size();
@@ -3403,6 +3419,7 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     ULG_HIP(c, hipGetLastError());
     if (use_graph) {
         hipGraph_t graph = nullptr;
+        capture_guard.active = false;
         ULG_HIP(c, hipStreamEndCapture(c->stream, &graph));
         c->graph = graph;
         ULG_HIP(c, hipGraphInstantiate(&c->gexec, graph, nullptr, nullptr, 0));
@@ -3424,7 +3441,8 @@ launched:
     prof_collect(c);
     if (wide_err)
         return set_err(c, ULG_ERR_UNSUPPORTED,
-                       "ulg_cbic_score: a find_best_subset_score walk exceeded 2^30 steps in a wide layer");
+                       "ulg_cbic_score: a find_best_subset_score walk in a wide layer exceeded its cap (2^30 steps "
+                       "in walk_wide_kernel, 2^32 iterations or 24 frames in the LDS / host replay)");
 
     c->nv = nv;
     c->kmax = kmax;

@@ -19,6 +19,7 @@
 // remaining bits in a second pass over strided tiles whose rows are 16
 // contiguous entries.  Both passes stream the table once (HBM-bound).
 // Lookup: cost = ord_cost(T_v[pext(S, D_v)]).
+#include <chrono>
 #include <hipcub/hipcub.hpp>
 #include <sys/mman.h>
 
@@ -693,8 +694,9 @@ void HostHuge::release() {
     pinned = false;
 }
 
-int search_cost_rows_host(ulg_ctx *c, uint64_t scope, uint64_t scc) {
+int search_cost_rows_host(ulg_ctx *c, uint64_t scope, uint64_t scc, int64_t deadline_ns, bool *timed_out) {
     SearchState &s = *c->search;
+    if (timed_out) *timed_out = false;
     if (s.rows_ready && s.rows_scope == scope && s.rows_scc == scc) return ULG_OK;
     const int m = __builtin_popcountll(scope), nl = __builtin_popcountll(scc);
     const uint64_t rows = 1ull << m, total = rows * (uint64_t)nl;
@@ -714,7 +716,15 @@ int search_cost_rows_host(ulg_ctx *c, uint64_t scope, uint64_t scc) {
     ULG_HIP(c, hipMemcpyAsync(s.d_rowmeta.p, meta.data(), 128 * 4, hipMemcpyHostToDevice, c->stream));
     const SearchDev d = s.dev();
     float *host = static_cast<float *>(s.host_rows.p);
+    s.rows_ready = false;
     for (uint64_t r0 = 0; r0 < rows; r0 += chunk_rows) {
+        if (deadline_ns &&
+            std::chrono::steady_clock::now().time_since_epoch().count() > deadline_ns) {
+            ULG_HIP(c, hipStreamSynchronize(c->stream));
+            prof_collect(c);
+            if (timed_out) *timed_out = true;
+            return ULG_OK;
+        }
         const uint64_t cnt = std::min(chunk_rows, rows - r0);
         const uint64_t work = cnt * (uint64_t)nl;
         prof_begin(c, "bs_cost_rows");

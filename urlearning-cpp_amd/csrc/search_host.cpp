@@ -603,7 +603,18 @@ int ulg_astar_scc(ulg_ctx *c, const uint64_t *edges, int pd_count, int mode, uin
         ExactResult r;
         const bool dense = dense_eligible(ancestors | comp, comp) && !std::getenv("ULG_EXACT_SPARSE");
         if ((rc = search_ensure_scope(c, ancestors | comp))) return rc;
-        if ((rc = dense ? search_cost_rows_host(c, ancestors | comp, comp) : search_cost_table_host(c))) return rc;
+        // the -r budget also covers the successor-cost rows (up to 8 GiB)
+        bool rows_late = false;
+        const int64_t dl_ns =
+            c->time_limit_ms > 0 ? std::chrono::duration_cast<std::chrono::nanoseconds>(deadline.time_since_epoch()).count()
+                                 : 0;
+        if ((rc = dense ? search_cost_rows_host(c, ancestors | comp, comp, dl_ns, &rows_late) : search_cost_table_host(c)))
+            return rc;
+        if (rows_late) {  // out of time before the search started: no goal (astar_main.cpp:266)
+            c->out_of_time = 1;
+            fail = true;
+            continue;
+        }
         HostTables T;
         host_tables(s, T);
         const Clock::time_point *dl = c->time_limit_ms > 0 ? &deadline : nullptr;

@@ -319,7 +319,11 @@ int search_quantize_device(ulg_ctx *c, const float *d_scores, float *d_costs, in
 int search_cost_table_host(ulg_ctx *c);
 // row table (SearchState::host_rows) for the dense exact-order search over
 // scope = ancestors | scc; the tables must cover scope
-int search_cost_rows_host(ulg_ctx *c, uint64_t scope, uint64_t scc);
+// deadline_ns (steady_clock nanoseconds since its epoch, 0 = none): checked
+// before every chunk of rows; past it the build stops, the rows stay
+// unbuilt and *timed_out is set (the -r budget covers this preprocessing)
+int search_cost_rows_host(ulg_ctx *c, uint64_t scope, uint64_t scc, int64_t deadline_ns = 0,
+                          bool *timed_out = nullptr);
 int search_query(ulg_ctx *c, int64_t count, const int *vars, const uint64_t *S, float *costs, uint64_t *parents);
 int search_pdb_query(ulg_ctx *c, int64_t count, const uint64_t *S, float *h, int *complete);
 
