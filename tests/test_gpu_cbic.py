@@ -210,14 +210,12 @@ def test_scorer_variants_identical(ulg_ctx, oracle_built, variant):
         ulg_ctx.set_option("score_variant", 17)
 
 
-@pytest.mark.parametrize("sets_per_lane", ["1", "1w2", "2", "4", "8"])
+@pytest.mark.parametrize("sets_per_lane", ["2", "4", "8"])
 def test_walk_forms_identical(ulg_ctx, oracle_built, monkeypatch, sets_per_lane):
-    """The walk forms (ULG_SLICED_K: 1 = lane-transposed scalar walk, 64 sets
-    per wave, or 128 at layer 6 with ULG_LANE_NW=2; 2/4/8 = bit-sliced walk)
-    store exactly the oracle's sets, with and without variable 0 among the
+    """The bit-sliced walk with 2, 4 or 8 sets per lane (ULG_SLICED_K) stores
+    exactly the oracle's sets, with and without variable 0 among the
     candidates (both N4 phases)."""
-    monkeypatch.setenv("ULG_SLICED_K", sets_per_lane[0])
-    monkeypatch.setenv("ULG_LANE_NW", "2" if sets_per_lane.endswith("w2") else "1")
+    monkeypatch.setenv("ULG_SLICED_K", sets_per_lane)
     n = 12
     X, _ = synth.gaussian_sem(n, 3000, 9250)
     ulg_ctx.load(X, 2.0)
@@ -230,17 +228,16 @@ def test_walk_forms_identical(ulg_ctx, oracle_built, monkeypatch, sets_per_lane)
 
 
 def test_walk_forms_identical_c3(ulg_ctx, monkeypatch):
-    """At C3 (n=25, N=10k, k=6, full skeleton: 4,751,275 sets) the
-    lane-transposed walk stores the bit-sliced walk's lists bit for bit."""
+    """At C3 (n=25, N=10k, k=6, full skeleton: 4,751,275 sets) 2 and 8 sets
+    per lane store the default walk's lists bit for bit."""
     n = 25
     X, _ = synth.gaussian_sem(n, 10000, 9200)
     ulg_ctx.load(X, 2.0)
     res = {}
-    for k in ("4", "1", "1w2"):
-        monkeypatch.setenv("ULG_SLICED_K", k[0])
-        monkeypatch.setenv("ULG_LANE_NW", "2" if k.endswith("w2") else "1")
+    for k in ("4", "2", "8"):
+        monkeypatch.setenv("ULG_SLICED_K", k)
         res[k] = ulg_ctx.score_all(list(range(n)), [(1 << n) - 1] * n, 6)
-    for k in ("1", "1w2"):
+    for k in ("2", "8"):
         for a, b in zip(res["4"], res[k]):
             assert a.tobytes() == b.tobytes(), k
 

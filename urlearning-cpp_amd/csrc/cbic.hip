@@ -447,9 +447,6 @@ __device__ __forceinline__ void best_subset_stack(uint32_t Ptop, uint32_t pvtop,
     }
 }
 
-#ifndef ULG_PRES_NB
-#define ULG_PRES_NB 0  // > 0: subsets per batch of branch-free gathers (measured no faster, r2an/r2ao)
-#endif
 // Presence of every key with a fully unrolled subset loop: the rank of each
 // subset t of the Q local bits is a compile-time sum of per-(bit, position)
 // binomials preloaded into registers.  Q = L when variable 0 is in P (local
@@ -457,10 +454,6 @@ __device__ __forceinline__ void best_subset_stack(uint32_t Ptop, uint32_t pvtop,
 template <int L, int PHASE, int Q, int W>
 __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi, float thr, const uint32_t *binom,
                                                   uint64_t cpack, bool z, const float *table, const uint64_t *toffv) {
-#ifdef ULG_PROBE_NOPRES
-    // timing probe only (wrong lists, scripts/r2ap.sh): the scorer's floor without the gathers and walks
-    return;
-#endif
     constexpr uint32_t Plocal = (Q == L) ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
     uint32_t RB[Q][L + 1];
 #pragma unroll
@@ -472,47 +465,6 @@ __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi,
     uint64_t off[L + 1];
 #pragma unroll
     for (int pc = 1; pc <= L; ++pc) off[pc] = toffv[pc];
-#if ULG_PRES_NB > 0
-    // Branch-free, in batches of ULG_PRES_NB subsets: every load of a batch
-    // is issued before the first is used.  (Skipping the subsets with local
-    // bit 0 when variable 0 is no candidate with a branch serialised the
-    // gathers: one L2 round trip per subset.)  Those subsets read a valid
-    // slot instead and their bits are masked out.
-    const float *safe = table + off[1];
-#pragma clang loop unroll(full)
-    for (uint32_t t0 = 1; t0 < (1u << Q); t0 += ULG_PRES_NB) {
-        float v[ULG_PRES_NB];
-#pragma unroll
-        for (uint32_t j = 0; j < ULG_PRES_NB; ++j) {
-            const uint32_t t = t0 + j;
-            const int pc = __builtin_popcount(t);
-            if (t >= (1u << Q) || pc > L || t == Plocal) continue;
-            if (pc == L && (PHASE == 0 || !(t & 1u))) continue;
-            uint64_t rk = 0;
-            int jj = 0;
-#pragma unroll
-            for (int b = 0; b < Q; ++b)
-                if ((t >> b) & 1u) {
-                    ++jj;
-                    rk += RB[b][jj];
-                }
-            const float *p = table + off[pc] + rk;
-            if (t & 1u) p = z ? p : safe;
-            v[j] = *p;
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < ULG_PRES_NB; ++j) {
-            const uint32_t t = t0 + j;
-            const int pc = __builtin_popcount(t);
-            if (t >= (1u << Q) || pc > L || t == Plocal) continue;
-            if (pc == L && (PHASE == 0 || !(t & 1u))) continue;
-            const bool ok = !(t & 1u) || z;
-            // the absent sentinel is a NaN: never >= thr
-            present.w[t >> 6] |= (uint64_t)(ok && fbits(v[j]) != kAbsentBits) << (t & 63);
-            hi.w[t >> 6] |= (uint64_t)(ok && v[j] >= thr) << (t & 63);
-        }
-    }
-#else
 #pragma clang loop unroll(full)
     for (uint32_t t = 1; t < (1u << Q); ++t) {
         const int pc = __builtin_popcount(t);
@@ -531,7 +483,6 @@ __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi,
         if (fbits(val) != kAbsentBits) present.set(t);
         if (val >= thr) hi.set(t);  // the absent sentinel is a NaN: never >= thr
     }
-#endif
 }
 
 struct ScoreArgs {
@@ -598,16 +549,8 @@ __device__ __forceinline__ BS make_bits(uint64_t *lds_base) {
 // PHASE 0: sets containing variable 0; 1: the rest.  V = variant bits (see
 // ulg_set_option "score_variant"), compile-time so each form gets its own
 // register allocation.
-#ifndef ULG_SCORE_WPE
-#define ULG_SCORE_WPE 0  // A/B builds: minimum waves per SIMD asked of the scoring kernel's register budget
-#endif
-#if ULG_SCORE_WPE > 0
-#define ULG_SCORE_ATTR __attribute__((amdgpu_waves_per_eu(ULG_SCORE_WPE)))
-#else
-#define ULG_SCORE_ATTR
-#endif
 template <int L, int PHASE, int V>
-__global__ void __launch_bounds__(kBlock) ULG_SCORE_ATTR score_layer_kernel(ScoreArgs a) {
+__global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const LdsLayout lay = lds_layout(a.n, a.nv, a.S, L, V);
     double *g = reinterpret_cast<double *>(smem + lay.gram);
@@ -1159,183 +1102,6 @@ __global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, 
         const uint64_t e0 = queue[(mine + k) * (uint64_t)(1 + 2 * W)];
         const float ts = __uint_as_float((uint32_t)(e0 >> 32));
         table[(uint32_t)e0] = ((dom >> k) & 1u) ? absent_f() : -ts;
-    }
-}
-
-// ---- lane-transposed walk: the union tree on the scalar unit ----------------
-// The sliced walk pays ~450 cycles per union-tree point: every per-set test is
-// a VALU op on an indexed register field followed by a ballot and a branch.
-// Here one wave takes 64 queued sets and stores the bit matrix transposed:
-// lane t of register r holds the 64-bit mask "which of the wave's sets have
-// local subset 64r + t in hi / open".  A tree point then reads its subset's
-// two masks with v_readlane (uniform lane index) into SGPRs, and every test,
-// mask update and branch is a 64-bit SALU op; only a cleared open entry goes
-// back with v_writelane.  Same walks as walk_sliced_kernel (and the reference
-// recursion, BIC_OLS.cpp:125-172): each set takes exactly its own steps.
-template <int L>
-struct LaneT {
-    static constexpr int NT = 1 << (L + 1);         // local subsets (phase 0 uses the lower half)
-    static constexpr int R = NT <= 64 ? 1 : NT / 64;  // registers per 32-bit half of a mask vector
-};
-// a wave's set mask: NW words of 64 sets
-template <int NW>
-struct Sets {
-    uint64_t w[NW];
-};
-template <int NW>
-__device__ __forceinline__ bool sets_any(const Sets<NW> &a) {
-    uint64_t x = 0;
-#pragma unroll
-    for (int i = 0; i < NW; ++i) x |= a.w[i];
-    return x != 0ull;
-}
-__device__ __forceinline__ uint32_t rlane(uint32_t v, uint32_t lane) {
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
-}
-// lane `lane` of a register <- v (a compare and a select)
-__device__ __forceinline__ uint32_t wlane(uint32_t v, uint32_t lane, uint32_t old) {
-    return threadIdx.x == lane ? v : old;
-}
-// V[w][r][h]: word w of the set mask, register r (subsets 64r..64r+63), 32-bit half h
-template <int R, int NW>
-__device__ __forceinline__ Sets<NW> lt_get(const uint32_t (&V)[NW][R][2], uint32_t t) {
-    static_assert(R == 1 || R == 2, "lane-transposed walk covers layers up to 6");
-    const uint32_t lane = t & 63u;
-    Sets<NW> m;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-        const uint64_t a = (uint64_t)rlane(V[w][0][0], lane) | ((uint64_t)rlane(V[w][0][1], lane) << 32);
-        if constexpr (R == 1) {
-            m.w[w] = a;
-        } else {
-            const uint64_t b = (uint64_t)rlane(V[w][R - 1][0], lane) | ((uint64_t)rlane(V[w][R - 1][1], lane) << 32);
-            m.w[w] = (t >> 6) ? b : a;
-        }
-    }
-    return m;
-}
-template <int R, int NW>
-__device__ __forceinline__ void lt_set(uint32_t (&V)[NW][R][2], uint32_t t, const Sets<NW> &m) {
-    const uint32_t lane = t & 63u;
-    const int r = (R == 1) ? 0 : (int)(t >> 6);
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-        if (r == 0) {
-            V[w][0][0] = wlane((uint32_t)m.w[w], lane, V[w][0][0]);
-            V[w][0][1] = wlane((uint32_t)(m.w[w] >> 32), lane, V[w][0][1]);
-        } else {
-            V[w][R - 1][0] = wlane((uint32_t)m.w[w], lane, V[w][R - 1][0]);
-            V[w][R - 1][1] = wlane((uint32_t)(m.w[w] >> 32), lane, V[w][R - 1][1]);
-        }
-    }
-}
-
-template <int R, int NW, int M>
-__device__ __forceinline__ void walk_lane(uint32_t T, uint32_t pv, Sets<NW> act, const uint32_t (&HV)[NW][R][2],
-                                          uint32_t (&OV)[NW][R][2], Sets<NW> &alive, Sets<NW> &dom) {
-#pragma nounroll
-    for (int idx = 0; idx < M; ++idx) {
-#pragma unroll
-        for (int w = 0; w < NW; ++w) act.w[w] &= alive.w[w];
-        if (!sets_any(act)) return;
-        const uint32_t u = (pv >> (4 * idx)) & 15u;
-        const uint32_t T2 = T ^ (1u << u);
-        // a hit ends that set's walk (the reference returns up the recursion)
-        const Sets<NW> h = lt_get<R, NW>(HV, T2);
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            const uint64_t hw = h.w[w] & act.w[w];
-            dom.w[w] |= hw;
-            alive.w[w] &= ~hw;
-            act.w[w] &= ~hw;
-        }
-        if constexpr (M > 1) {
-            Sets<NW> o = lt_get<R, NW>(OV, T2), x;
-#pragma unroll
-            for (int w = 0; w < NW; ++w) x.w[w] = o.w[w] & act.w[w];
-            if (!sets_any(x)) continue;
-            uint32_t npv = 0;
-            int j = 0;
-            bool first = true;
-#pragma nounroll
-            for (int i = 0; i < M; ++i) {
-                const uint32_t pi = (pv >> (4 * i)) & 15u;
-                if (pi == u) continue;
-                npv |= pi << (4 * j);
-                ++j;
-                // checked.insert(T2) for the sets that run the call.  A call
-                // toggles distinct bits of T2 and never reaches T2 itself, so
-                // clearing once before the first call is the reference's
-                // order; with no call (every entry equals u) nothing is cleared.
-                if (first) {
-#pragma unroll
-                    for (int w = 0; w < NW; ++w) o.w[w] &= ~x.w[w];
-                    lt_set<R, NW>(OV, T2, o);
-                    first = false;
-                }
-                walk_lane<R, NW, M - 1>(T2, npv, x, HV, OV, alive, dom);
-#pragma unroll
-                for (int w = 0; w < NW; ++w) x.w[w] &= alive.w[w];
-                if (!sets_any(x)) break;
-            }
-        }
-    }
-}
-
-// one wave per 64 * NW queued sets (word w: sets first + 64w + lane); entries
-// as walk_kernel's
-template <int L, int PHASE, int NW>
-__global__ void __launch_bounds__(64) walk_lane_kernel(const uint64_t *queue, const unsigned long long *qcount,
-                                                       float *table, uint64_t *) {
-    using S = LaneT<L>;
-    constexpr int W = bits_words(L);
-    static_assert(W * 64 >= S::NT, "queue entry bitsets cover the local subsets");
-    const uint64_t qn = *qcount;
-    const uint64_t first = (uint64_t)blockIdx.x * 64 * NW;
-    if (first >= qn) return;
-    uint32_t HV[NW][S::R][2], OV[NW][S::R][2];
-    Sets<NW> alive, dom;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-        const uint64_t mine = first + 64 * w + threadIdx.x;
-        const bool valid = mine < qn;
-        const uint64_t *e = queue + (valid ? mine : first) * (uint64_t)(1 + 2 * W);
-        uint64_t hw[W], ow[W];
-#pragma unroll
-        for (int wj = 0; wj < W; ++wj) {
-            hw[wj] = valid ? e[1 + wj] : 0ull;
-            ow[wj] = valid ? e[1 + W + wj] : 0ull;
-        }
-        // transpose: lane t of register r <- ballot over the word's sets of subset 64r + t
-#pragma unroll
-        for (int r = 0; r < S::R; ++r) HV[w][r][0] = HV[w][r][1] = OV[w][r][0] = OV[w][r][1] = 0u;
-#pragma unroll
-        for (int t = 0; t < S::NT; ++t) {
-            const uint64_t mh = __ballot((int)((hw[t >> 6] >> (t & 63)) & 1ull));
-            const uint64_t mo = __ballot((int)((ow[t >> 6] >> (t & 63)) & 1ull));
-            const bool me = threadIdx.x == (uint32_t)(t & 63);
-            HV[w][t >> 6][0] = me ? (uint32_t)mh : HV[w][t >> 6][0];
-            HV[w][t >> 6][1] = me ? (uint32_t)(mh >> 32) : HV[w][t >> 6][1];
-            OV[w][t >> 6][0] = me ? (uint32_t)mo : OV[w][t >> 6][0];
-            OV[w][t >> 6][1] = me ? (uint32_t)(mo >> 32) : OV[w][t >> 6][1];
-        }
-        alive.w[w] = __ballot(valid);
-        dom.w[w] = 0ull;
-    }
-    constexpr bool v0inP = PHASE == 0;
-    constexpr uint32_t Plocal = v0inP ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
-    uint32_t pvtop = 0;
-#pragma unroll
-    for (int i = 0; i < L; ++i) pvtop |= (uint32_t)(i + (v0inP ? 0 : 1)) << (4 * i);
-    walk_lane<S::R, NW, L>(Plocal, pvtop, alive, HV, OV, alive, dom);
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-        const uint64_t mine = first + 64 * w + threadIdx.x;
-        if (mine < qn) {
-            const uint64_t e0 = queue[mine * (uint64_t)(1 + 2 * W)];
-            const float ts = __uint_as_float((uint32_t)(e0 >> 32));
-            table[(uint32_t)e0] = ((dom.w[w] >> threadIdx.x) & 1ull) ? absent_f() : -ts;
-        }
     }
 }
 
@@ -2425,50 +2191,20 @@ SlicedFn sliced_fn_wide(int L, int phase) {
 constexpr int kSlicedKSmall = 2;  // default sets per lane up to layer 5
 int sliced_k(int L) {
     if (L >= 7) return L == 7 ? 2 : 1;
-    // ULG_SLICED_K=a (every layer) or a,b (layers <= 5, layer 6); 1 selects
-    // the lane-transposed walk
+    // ULG_SLICED_K=a (every layer) or a,b (layers <= 5, layer 6): A/B only
     const char *e = std::getenv("ULG_SLICED_K");
     int k = L <= 5 ? kSlicedKSmall : 4;
     if (e) {
         const char *comma = std::strchr(e, ',');
         k = (L <= 5 || !comma) ? std::atoi(e) : std::atoi(comma + 1);
     }
-    return (k == 1 || k == 2 || k == 8) ? k : 4;
-}
-template <int L, int NW>
-SlicedFn lane_pick(int phase) {
-    return phase == 0 ? walk_lane_kernel<L, 0, NW> : walk_lane_kernel<L, 1, NW>;
-}
-template <int NW>
-SlicedFn lane_fn_nw(int L, int phase) {
-    switch (L) {
-        case 1: return lane_pick<1, NW>(phase);
-        case 2: return lane_pick<2, NW>(phase);
-        case 3: return lane_pick<3, NW>(phase);
-        case 4: return lane_pick<4, NW>(phase);
-        case 5: return lane_pick<5, NW>(phase);
-        case 6: return lane_pick<6, NW>(phase);
-        default: return nullptr;
-    }
-}
-// the lane-transposed scalar walk with 64 * lane_words(L) sets per wave
-int lane_words(int L) {
-    const char *e = std::getenv("ULG_LANE_NW");
-    const int w = e ? std::atoi(e) : 1;
-    return (w == 2 && L == 6) ? 2 : 1;
-}
-SlicedFn lane_fn(int L, int phase) {
-    return lane_words(L) == 2 ? lane_fn_nw<2>(L, phase) : lane_fn_nw<1>(L, phase);
+    return (k == 2 || k == 8) ? k : 4;
 }
 // queued sets per walk wave
-uint64_t walk_sets_per_wave(int L) {
-    const int k = sliced_k(L);
-    return k == 1 ? 64ull * (uint64_t)lane_words(L) : 64ull * (uint64_t)k;
-}
+uint64_t walk_sets_per_wave(int L) { return 64ull * (uint64_t)sliced_k(L); }
 SlicedFn sliced_fn(int L, int phase) {
     if (L >= 7) return sliced_fn_wide(L, phase);
     switch (sliced_k(L)) {
-        case 1: return lane_fn(L, phase);
         case 2: return sliced_fn_k<2>(L, phase);
         case 4: return sliced_fn_k<4>(L, phase);
         default: return sliced_fn_k<8>(L, phase);
