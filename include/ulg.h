@@ -271,12 +271,16 @@ int ulg_sweep_shard_end(ulg_ctx *ctx, uint64_t *vpar, int *order, float *goal_co
                         int64_t *expanded);
 
 /* ---- tuning knobs -------------------------------------------------------
- * "score_variant" (0..7, 13, 16, 17; default 17): bit 0 = fully unrolled
- * presence gather in the scorer (layers <= 6), bit 1 = stack-machine
- * dominance recursion, bit 2 = decision-only walk (stops at the first
- * visited key >= -ts), bit 4 = two-pass layers: the scoring kernel settles
- * every set it can without a walk and queues the rest for a dense walk
- * kernel with the hi-cover prune (overrides bits 1-2).  13 = bit 2 plus
+ * "score_variant" (0..7, 13, 16, 17, 48, 49, 81, 113; default 113): bit 0 =
+ * fully unrolled presence gather in the scorer (layers <= 6), bit 1 =
+ * stack-machine dominance recursion, bit 2 = decision-only walk (stops at the
+ * first visited key >= -ts), bit 4 = two-pass layers: the scoring kernel
+ * settles every set it can without a walk and queues the rest for a dense
+ * walk kernel with the hi-cover prune (overrides bits 1-2), bit 5 = that walk
+ * bit-sliced (64 x K sets per wave), bit 6 (with bits 0 and 4) = subset
+ * maxima: a per-slot table of the largest stored value below each set settles
+ * sets with 2L-3L reads before the block compacts the rest for the
+ * 2^(L+1) presence gathers.  All variants store identical lists.  13 = bit 2 plus
  * per-launch decision statistics on stderr (and, with ULG_DUMP_DIR set, the
  * walking lanes' presence words); diagnostics only, it synchronises.
  * "table_budget_kb" (KiB; default 0 = half the free HBM): memory for the dense

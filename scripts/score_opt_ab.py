@@ -43,6 +43,16 @@ def run(name, X, variables, cands, k, reps=100, rounds=2):
                 best = min(best, (time.perf_counter() - t) / reps)
             print(f"{name} {OPT}={val}: {best * 1e3:.4f} ms per call, {stored} of {scored} stored, digest {dg}",
                   flush=True)
+            if os.environ.get("PROFILE") == "1":
+                # per-kernel times of one profiled call (HIP events, eager launches)
+                ctx.profile(True)
+                ctx.profile_select(None)
+                ctx.profile_reset()
+                ctx.score(variables, cands, k)
+                kern = ctx.profile_dump()
+                ctx.profile(False)
+                print("   ", " ".join(f"{kk}={v['total_ms']:.4f}" for kk, v in sorted(kern.items())
+                                      if v["total_ms"] >= 0.01), flush=True)
     ctx.close()
 
 

@@ -13,6 +13,7 @@ import synth
 pytestmark = pytest.mark.gpu
 
 REL_TOL = 1e-6
+DEFAULT_VARIANT = 113  # the library default (ulg_internal.h)
 
 
 def _compare_lists(o_offs, o_sets, o_scores, g_offs, g_sets, g_scores, variables, ctx=""):
@@ -190,11 +191,11 @@ def test_rescoring_is_deterministic(ulg_ctx):
         assert x.tobytes() == y.tobytes()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 16, 17, 48, 49])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 16, 17, 48, 49, 81, 113])
 def test_scorer_variants_identical(ulg_ctx, oracle_built, variant):
     """Every scorer variant (presence gather x recursion form x decision-only
-    walk) stores exactly the oracle's sets (k=6 exercises the unrolled
-    presence, k=7,8 the loop)."""
+    walk x subset-maxima settling) stores exactly the oracle's sets (k=6
+    exercises the unrolled presence, k=7,8 the loop)."""
     n = 11
     X, _ = synth.gaussian_sem(n, 2500, 9230 + variant)
     variables = list(range(n))
@@ -207,7 +208,7 @@ def test_scorer_variants_identical(ulg_ctx, oracle_built, variant):
             o = _oracle_lists(oracle_built, X, 2.0, variables, cands, k)
             _compare_lists(*o, *g, variables, ctx=f"variant {variant} k={k}")
     finally:
-        ulg_ctx.set_option("score_variant", 17)
+        ulg_ctx.set_option("score_variant", DEFAULT_VARIANT)
 
 
 @pytest.mark.parametrize("sets_per_lane", ["2", "4", "8"])
@@ -225,6 +226,27 @@ def test_walk_forms_identical(ulg_ctx, oracle_built, monkeypatch, sets_per_lane)
         g = ulg_ctx.score_all(variables, cands, 6)
         o = _oracle_lists(oracle_built, X, 2.0, variables, cands, 6)
         _compare_lists(*o, *g, variables, ctx=f"ULG_SLICED_K={sets_per_lane}")
+
+
+def test_subset_maxima_identical_c3_and_without_var0(ulg_ctx):
+    """Variant 113 (subset maxima settle sets before the presence gathers)
+    against 49 (every set gathered): identical lists at C3 and on candidate
+    lists without variable 0 (phase 1 then has no P\\a+{0} keys)."""
+    n = 25
+    X, _ = synth.gaussian_sem(n, 10000, 9200)
+    ulg_ctx.load(X, 2.0)
+    cases = [(list(range(n)), [(1 << n) - 1] * n, 6), (list(range(1, n)), [((1 << n) - 1) & ~1] * (n - 1), 6),
+             (list(range(n)), [((1 << n) - 1) & ~(1 << (v % 5)) for v in range(n)], 7)]
+    try:
+        for variables, cands, k in cases:
+            res = {}
+            for variant in (49, 113):
+                ulg_ctx.set_option("score_variant", variant)
+                res[variant] = ulg_ctx.score_all(variables, cands, k)
+            for a, b in zip(res[49], res[113]):
+                assert np.asarray(a).tobytes() == np.asarray(b).tobytes(), (len(variables), k)
+    finally:
+        ulg_ctx.set_option("score_variant", DEFAULT_VARIANT)
 
 
 def test_walk_forms_identical_c3(ulg_ctx, monkeypatch):

@@ -493,6 +493,8 @@ struct ScoreArgs {
     const uint64_t *tbl_off; // [nv*S + 1] start of (vi, layer) slab
     const uint64_t *work;    // [nv + 1] prefix of this launch's sets
     float *table;
+    float *hsub;                // variant bit 6: per slot, the maximum stored value over the set's
+                                // nonempty subsets (the set included; NaN = none), table layout
     unsigned long long *stats;  // variant bit 3: per-launch decision statistics
     uint64_t *dump;             // variant bit 3: presence words of the walking lanes
     uint64_t dump_cap;
@@ -518,10 +520,14 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, int on) {
 __host__ __device__ constexpr int bits_words(int L) { return (L + 1) <= 6 ? 1 : (1 << ((L + 1) - 6)); }
 
 // LDS carve: gram | binom | work | tbl_off | recursion stack (variant bit 1)
-// | LDS bitsets (3 per lane when they have >= 4 words) (16-B aligned)
+// | LDS bitsets (3 per lane when they have >= 4 words) | the block's
+// undecided sets after the subset-maxima test (variant bits 4 + 6: a count,
+// then per entry compact mask, slot, ts, children maximum, variable) (16-B
+// aligned)
 struct LdsLayout {
-    int gram, binom, work, toff, stack, bits, total;
+    int gram, binom, work, toff, stack, bits, cmp, total;
 };
+constexpr int kCmpEntryBytes = 8 + 4 + 4 + 4 + 4;
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
 __host__ __device__ inline LdsLayout lds_layout(int n, int nv, int S, int L, int V) {
     LdsLayout l;
@@ -532,7 +538,8 @@ __host__ __device__ inline LdsLayout lds_layout(int n, int nv, int S, int L, int
     l.stack = align16(l.toff + (nv * S + 1) * 8);
     l.bits = align16(l.stack + ((V & 2) && !(V & 4) ? L * kBlock * 8 : 0));
     const int W = bits_words(L);
-    l.total = l.bits + (W >= 4 ? 3 * W * kBlock * 8 : 0);
+    l.cmp = align16(l.bits + (W >= 4 ? 3 * W * kBlock * 8 : 0));
+    l.total = l.cmp + ((V & 80) == 80 ? 16 + kBlock * kCmpEntryBytes : 0);
     return l;
 }
 
@@ -543,6 +550,221 @@ __device__ __forceinline__ BS make_bits(uint64_t *lds_base) {
         return BS{};
     } else {
         return BS{lds_base};
+    }
+}
+
+// A parent set in local numbering: local bit 0 is variable 0 (compact index
+// 0 when it is a candidate), local bits 1..L the other members of P in
+// increasing order (all L members of P when P contains variable 0).
+template <int L>
+struct LocalSet {
+    uint64_t cpack;   // local bit -> compact index, 6 bits each (bit 0 -> 0)
+    uint32_t Plocal;  // P itself
+    uint32_t pvtop;   // the top-level parent vector: P's local bits, 4 bits each
+    bool v0inP;
+};
+template <int L>
+__device__ __forceinline__ LocalSet<L> local_set(uint64_t cm, bool z) {
+    LocalSet<L> s;
+    s.v0inP = z && (cm & 1ull);
+    const uint64_t E = z ? (cm & ~1ull) : cm;
+    s.cpack = 0;
+    uint64_t rem = E;
+#pragma unroll
+    for (int i = 1; i <= L; ++i) {
+        if (rem) {
+            const uint64_t b = (uint64_t)__builtin_ctzll(rem);
+            rem &= rem - 1;
+            s.cpack |= b << (6 * i);
+        }
+    }
+    s.Plocal = s.v0inP ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
+    s.pvtop = 0;
+#pragma unroll
+    for (int i = 0; i < L; ++i) s.pvtop |= (uint32_t)(i + (s.v0inP ? 0 : 1)) << (4 * i);
+    return s;
+}
+
+// Presence of every candidate key below P u {var 0} in the cache as it
+// stands now (`present`), and which of them hold a value >= thr (`hi`).
+template <int L, int PHASE, int V, class BS>
+__device__ __forceinline__ void gather_keys(BS &present, BS &hi, const LocalSet<L> &ls, float thr,
+                                            const uint32_t *binom, bool z, const float *table,
+                                            const uint64_t *toffv) {
+    constexpr int W = BS::kWords;
+    if constexpr (L <= 6 && (V & 1)) {
+        presence_unrolled<L, PHASE, (PHASE == 0 ? L : L + 1), W>(present, hi, thr, binom, ls.cpack, z, table, toffv);
+    } else {
+        const int q = ls.v0inP ? L : L + 1;
+        const uint32_t full = 1u << q;
+#pragma nounroll
+        for (uint32_t t = 1; t < full; ++t) {
+            const int pc = __builtin_popcount(t);
+            bool cand = pc <= L && t != ls.Plocal && (z || !(t & 1u));
+            if (pc == L) cand = cand && PHASE == 1 && (t & 1u);
+            if (!cand) continue;
+            uint64_t rk = 0;
+            uint32_t rem = t;
+            int j = 0;
+            while (rem) {
+                const int lb = __builtin_ctz(rem);
+                rem &= rem - 1;
+                ++j;
+                rk += B(binom, (int)((ls.cpack >> (6 * lb)) & 63ull), j);
+            }
+            const float val = table[toffv[pc] + rk];
+            if (fbits(val) != kAbsentBits) present.set(t);
+            if (val >= thr) hi.set(t);
+        }
+    }
+}
+
+// The two-pass form's decision for a set with ts < 0 from its presence and hi
+// bitsets (variant bit 4).  Returns true when P is not stored; `queued` = the
+// set needs the walk.
+//  * no present key >= -ts: nothing the walk visits can prune P;
+//  * a present direct child >= -ts: always visited at the top;
+//  * (P without var 0) a present P\{a,b} or P\{a}+{0} >= -ts
+//    with P\{a} absent: P\{a} is first reached at the top
+//    level (nothing below P\{a'} contains a' != 0 again), so it
+//    is expanded with the full list, and its j = L-1 call tests
+//    every P\{a,b}, its j = 1 call (L >= 3) the toggle of var 0.
+//    Present keys never enter `checked`, so those are visited.
+template <int L, int PHASE, class BS>
+__device__ __forceinline__ bool settle_rules(const BS &present, const BS &hi, const LocalSet<L> &ls, bool &queued) {
+    constexpr int W = BS::kWords;
+    bool any = false;
+#pragma unroll
+    for (int wj = 0; wj < W; ++wj) any |= hi.word(wj) != 0ull;
+    bool dom = false;
+    queued = false;
+    if (!any) return false;
+#pragma unroll
+    for (int i = 0; i < L; ++i) dom |= hi.test(ls.Plocal ^ (1u << ((ls.pvtop >> (4 * i)) & 15u)));
+    if constexpr (PHASE == 1) {
+        constexpr uint32_t P1 = ((1u << L) - 1u) << 1;
+#pragma unroll
+        for (int ea = 1; ea <= L; ++ea) {
+            const uint32_t Ta = P1 ^ (1u << ea);
+            bool d2 = false;
+#pragma unroll
+            for (int eb = 1; eb <= L; ++eb)
+                if (eb != ea) d2 |= hi.test(Ta ^ (1u << eb));
+            if constexpr (L >= 3) d2 |= hi.test(Ta | 1u);
+            dom |= d2 && !present.test(Ta);
+        }
+        // One level further: X = P\{a,b} (a < b), absent, is first
+        // tested below P\{a} if that is absent (in its j = b-1
+        // call), else below P\{b} if absent (in its j = a call),
+        // else never.  Its expansion list holds the entries before
+        // the removed one: {1..b-1}\{a} in the first case, {1..a-1}
+        // in the second, plus zeros (the var-0 toggle, L >= 4).
+        if constexpr (L >= 3) {
+#pragma unroll
+            for (int ea = 1; ea <= L; ++ea)
+#pragma unroll
+                for (int eb = ea + 1; eb <= L; ++eb) {
+                    const uint32_t X = P1 ^ (1u << ea) ^ (1u << eb);
+                    bool h1 = false, h2 = false;
+#pragma unroll
+                    for (int ec = 1; ec < eb; ++ec) {
+                        if (ec == ea) continue;
+                        const bool hc = hi.test(X ^ (1u << ec));
+                        h1 |= hc;
+                        if (ec < ea) h2 |= hc;
+                    }
+                    if constexpr (L >= 4) {
+                        const bool ht = hi.test(X | 1u);
+                        h1 |= ht;
+                        h2 |= ht;
+                    }
+                    const bool pa = present.test(P1 ^ (1u << ea));
+                    const bool pb = present.test(P1 ^ (1u << eb));
+                    const bool hx = pa ? (!pb && h2) : h1;
+                    dom |= hx && !present.test(X);
+                }
+        }
+    } else {
+        // P\{0} is the very first node tested; if absent it is
+        // expanded with every list (1..j) + zeros, so each present
+        // P\{0,c} is visited.
+        constexpr uint32_t P0 = (1u << L) - 1u;
+        bool d2 = false;
+#pragma unroll
+        for (int ec = 1; ec < L; ++ec) d2 |= hi.test(P0 ^ 1u ^ (1u << ec));
+        dom |= d2 && !present.test(P0 ^ 1u);
+    }
+    queued = !dom;
+    return dom;
+}
+
+// Append a set to the walk queue (wave-aggregated: one atomic per wave):
+// table slot | ts bits << 32, the hi words, then the open words
+// (open = absent & cover(T without var 0) & not checked; checked = {empty}).
+template <class BS>
+__device__ __forceinline__ void queue_walk(const BS &present, const BS &hi, uint64_t *queue,
+                                           unsigned long long *qcount, uint64_t slot, float ts) {
+    constexpr int W = BS::kWords;
+    const unsigned long long act = __ballot(1);
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)act) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(qcount, (unsigned long long)__popcll(act));
+    base = __shfl(base, leader);
+    const uint64_t pos = base + (uint64_t)__popcll(act & ((1ull << lane) - 1ull));
+    uint64_t ow[W];
+#pragma unroll
+    for (int wj = 0; wj < W; ++wj) ow[wj] = hi.word(wj);
+    cover_words<W>(ow);
+#pragma unroll
+    for (int wj = 0; wj < W; ++wj) {
+        const uint64_t ce = ow[wj] & 0x5555555555555555ull;
+        ow[wj] = (ce | (ce << 1)) & ~present.word(wj) & (wj == 0 ? ~1ull : ~0ull);
+    }
+    uint64_t *e = queue + pos * (uint64_t)(1 + 2 * W);
+    e[0] = slot | ((uint64_t)fbits(ts) << 32);
+#pragma unroll
+    for (int wj = 0; wj < W; ++wj) e[1 + wj] = hi.word(wj);
+#pragma unroll
+    for (int wj = 0; wj < W; ++wj) e[1 + W + wj] = ow[wj];
+}
+
+// Subset maxima (variant bit 6).  hsub[slot of X] = the largest stored value
+// over the nonempty subsets of X, X included (NaN: none stored).  The walk of
+// P only ever visits keys in U(P) = the nonempty subsets of P u {var 0} other
+// than P and P u {var 0} (checked starts as {empty}; a layer-L key with var 0
+// is in the cache only in phase 1), so
+//   max over U(P) = max_a hsub[P\a]                    (P with var 0, or no var 0 candidate)
+//                 = max_a max(hsub[P\a], hsub[P\a+{0}]) (P without var 0, phase 1)
+// and a set whose U(P) holds no key >= -ts is stored without its 2^(L+1)
+// presence gathers.  Children ranks: for P = {a_1 < ... < a_L} (compact),
+//   rank(P\a_i)       = sum_{j<i} C(a_j, j)   + sum_{j>i} C(a_j, j-1)
+//   rank(P\a_i + {0}) = sum_{j<i} C(a_j, j+1) + sum_{j>i} C(a_j, j)   (a_1 >= 1)
+template <int L, bool WITH0>
+__device__ __forceinline__ void child_ranks(uint64_t cm, const uint32_t *binom, uint64_t (&rc)[L], uint64_t (&rz)[L]) {
+    uint32_t e[L], d[L], f[L];
+    uint64_t rem = cm;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+        const int aj = __builtin_ctzll(rem);
+        rem &= rem - 1;
+        e[j] = B(binom, aj, j + 1);
+        d[j] = B(binom, aj, j);
+        f[j] = WITH0 ? B(binom, aj, j + 2) : 0u;
+    }
+    uint64_t pe = 0, pf = 0;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        uint64_t sd = 0, se = 0;
+#pragma unroll
+        for (int j = i + 1; j < L; ++j) {
+            sd += d[j];
+            se += e[j];
+        }
+        rc[i] = pe + sd;
+        rz[i] = pf + se;
+        pe += e[i];
+        pf += f[i];
     }
 }
 
@@ -564,8 +786,14 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
     for (int i = threadIdx.x; i <= a.nv * a.S; i += kBlock) toff[i] = a.tbl_off[i];
     __syncthreads();
 
-    const uint64_t gid = (uint64_t)xcd_block(blockIdx.x, gridDim.x, a.xcd) * kBlock + threadIdx.x;
-    if (gid >= work[a.nv]) return;
+    constexpr bool HM = (V & 64) != 0;           // subset maxima kept up to date
+    constexpr bool CMP = HM && (V & 16) != 0;     // ... and the sets settled by them first
+    const uint64_t gid0 = (uint64_t)xcd_block(blockIdx.x, gridDim.x, a.xcd) * kBlock + threadIdx.x;
+    const bool valid = gid0 < work[a.nv];
+    if (!CMP && !valid) return;
+    // CMP: every lane reaches the block's barrier; a lane past the launch's
+    // sets scores the last one again and writes nothing
+    const uint64_t gid = valid ? gid0 : work[a.nv] - 1;
     int lo = 0, hi = a.nv;
     while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
@@ -638,6 +866,94 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
     const double the_score = a.N * log(rss / a.N) + a.lambda * log(a.N) * (double)L - 0.0;
     const float ts = (float)the_score;
 
+    if constexpr (CMP) {
+        // 1. settle by the subset maxima: ts >= 0, no key >= -ts in U(P), or a
+        //    present direct child >= -ts (always visited at the top level)
+        const uint64_t vbase = (uint64_t)vi * a.S;
+        const uint64_t slot = toff[vbase + L] + rankP;
+        uint64_t rc[L], rz[L];
+        child_ranks<L, PHASE == 1>(cm, binom, rc, rz);
+        float hch = absent_f();  // max over the proper nonempty subsets of P
+        if constexpr (L > 1) {
+#pragma unroll
+            for (int i = 0; i < L; ++i) hch = fmaxf(hch, a.hsub[toff[vbase + L - 1] + rc[i]]);
+        }
+        bool need = false;
+        float out;
+        if (ts >= 0.0f) {
+            const float s = -ts;
+            out = (s < 0.0f) ? s : absent_f();
+        } else {
+            const float thr = -ts;
+            float hu = hch;
+            if constexpr (PHASE == 1) {
+                if (z) {
+#pragma unroll
+                    for (int i = 0; i < L; ++i) hu = fmaxf(hu, a.hsub[toff[vbase + L] + rz[i]]);
+                }
+            }
+            out = -ts;
+            if (hu >= thr) {
+                bool dh = false;
+                if constexpr (L > 1) {
+#pragma unroll
+                    for (int i = 0; i < L; ++i) dh |= a.table[toff[vbase + L - 1] + rc[i]] >= thr;
+                }
+                out = absent_f();
+                need = !dh;
+            }
+        }
+        if (valid && !need) {
+            a.table[slot] = out;
+            a.hsub[slot] = fmaxf(out, hch);
+        }
+        // 2. the rest of the block's sets, compacted in LDS, so the presence
+        //    gathers (2^(L+1) reads each) run on dense waves
+        unsigned int *cnt = reinterpret_cast<unsigned int *>(smem + lay.cmp);
+        uint64_t *ecm = reinterpret_cast<uint64_t *>(smem + lay.cmp + 16);
+        uint32_t *eslot = reinterpret_cast<uint32_t *>(ecm + kBlock);
+        float *ets = reinterpret_cast<float *>(eslot + kBlock);
+        float *ehch = ets + kBlock;
+        int *evi = reinterpret_cast<int *>(ehch + kBlock);
+        if (threadIdx.x == 0) *cnt = 0u;
+        __syncthreads();
+        if (valid && need) {
+            const unsigned int k = atomicAdd(cnt, 1u);
+            ecm[k] = cm;
+            eslot[k] = (uint32_t)slot;
+            ets[k] = ts;
+            ehch[k] = hch;
+            evi[k] = vi;
+        }
+        __syncthreads();
+        if (threadIdx.x >= *cnt) return;
+        const int k = threadIdx.x;
+        const int vk = evi[k];
+        const bool zk = a.meta[vk * 4 + 2] != 0;
+        const float tk = ets[k];
+        const uint64_t sk = eslot[k];
+        constexpr int W = bits_words(L);
+        using BS = std::conditional_t<(W >= 4), BitsLds<W>, Bits<W>>;
+        uint64_t *lds_bits = reinterpret_cast<uint64_t *>(smem + lay.bits) + threadIdx.x;
+        const LocalSet<L> ls = local_set<L>(ecm[k], zk);
+        BS present = make_bits<BS>(lds_bits);
+        BS hib = make_bits<BS>(lds_bits + (size_t)W * kBlock);
+        present.clear();
+        hib.clear();
+        gather_keys<L, PHASE, V>(present, hib, ls, -tk, binom, zk, a.table, toff + (uint64_t)vk * a.S);
+        bool q;
+        const bool dom = settle_rules<L, PHASE>(present, hib, ls, q);
+        if (q) {
+            queue_walk(present, hib, a.queue, a.qcount, sk, tk);
+            a.hsub[sk] = ehch[k];  // the walk raises it to -ts if it stores P
+        } else {
+            const float o = dom ? absent_f() : -tk;
+            a.table[sk] = o;
+            a.hsub[sk] = fmaxf(o, ehch[k]);
+        }
+        return;
+    }
+
     float out;
     bool queued = false;  // variant bit 4: left for walk_kernel
     int cat = 1;          // variant bit 3 statistics: 1 ts >= 0, 2 no key >= -ts,
@@ -650,22 +966,11 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         constexpr int W = bits_words(L);
         using BS = std::conditional_t<(W >= 4), BitsLds<W>, Bits<W>>;
         uint64_t *lds_bits = reinterpret_cast<uint64_t *>(smem + lay.bits) + threadIdx.x;
-        const bool v0inP = z && (cm & 1ull);
-        const uint64_t E = z ? (cm & ~1ull) : cm;
-        uint64_t cpack = 0;  // local bit -> compact index, 6 bits each (bit 0 -> 0)
-        {
-            uint64_t rem = E;
-#pragma unroll
-            for (int i = 1; i <= L; ++i) {
-                if (rem) {
-                    const uint64_t b = (uint64_t)__builtin_ctzll(rem);
-                    rem &= rem - 1;
-                    cpack |= b << (6 * i);
-                }
-            }
-        }
-        const uint32_t Plocal = v0inP ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
-        const int q = v0inP ? L : L + 1;
+        const LocalSet<L> ls = local_set<L>(cm, z);
+        const uint64_t cpack = ls.cpack;
+        const uint32_t Plocal = ls.Plocal;
+        const uint32_t pvtop = ls.pvtop;
+        const bool v0inP = ls.v0inP;
         const uint64_t vbase = (uint64_t)vi * a.S;
 
         // presence of every candidate key in the cache as it stands now
@@ -676,134 +981,12 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         present.clear();
         if constexpr ((V & 20) != 0) hi.clear();
         const float thr = -ts;
-        if constexpr (L <= 6 && (V & 1)) {
-            presence_unrolled<L, PHASE, (PHASE == 0 ? L : L + 1), W>(present, hi, thr, binom, cpack, z, a.table,
-                                                                     toff + vbase);
-        } else {
-            const uint32_t full = 1u << q;
-    #pragma nounroll
-            for (uint32_t t = 1; t < full; ++t) {
-                const int pc = __builtin_popcount(t);
-                bool cand = pc <= L && t != Plocal && (z || !(t & 1u));
-                if (pc == L) cand = cand && PHASE == 1 && (t & 1u);
-                if (!cand) continue;
-                uint64_t rk = 0;
-                uint32_t rem = t;
-                int j = 0;
-                while (rem) {
-                    const int lb = __builtin_ctz(rem);
-                    rem &= rem - 1;
-                    ++j;
-                    rk += B(binom, (int)((cpack >> (6 * lb)) & 63ull), j);
-                }
-                const float val = a.table[toff[vbase + pc] + rk];
-                if (fbits(val) != kAbsentBits) present.set(t);
-                if (val >= thr) hi.set(t);
-            }
-        }
+        gather_keys<L, PHASE, V>(present, hi, ls, thr, binom, z, a.table, toff + vbase);
 
-        uint32_t pvtop = 0;
-#pragma unroll
-        for (int i = 0; i < L; ++i) pvtop |= (uint32_t)(i + (v0inP ? 0 : 1)) << (4 * i);
         if constexpr ((V & 16) != 0) {
-            // Decide what needs no walk; queue the rest for walk_kernel.
-            //  * no present key >= -ts: nothing the walk visits can prune P;
-            //  * a present direct child >= -ts: always visited at the top;
-            //  * (P without var 0) a present P\{a,b} or P\{a}+{0} >= -ts
-            //    with P\{a} absent: P\{a} is first reached at the top
-            //    level (nothing below P\{a'} contains a' != 0 again), so it
-            //    is expanded with the full list, and its j = L-1 call tests
-            //    every P\{a,b}, its j = 1 call (L >= 3) the toggle of var 0.
-            //    Present keys never enter `checked`, so those are visited.
-            bool any = false;
-#pragma unroll
-            for (int wj = 0; wj < W; ++wj) any |= hi.word(wj) != 0ull;
-            bool dom = false;
-            if (any) {
-#pragma unroll
-                for (int i = 0; i < L; ++i) dom |= hi.test(Plocal ^ (1u << ((pvtop >> (4 * i)) & 15u)));
-                if constexpr (PHASE == 1) {
-                    constexpr uint32_t P1 = ((1u << L) - 1u) << 1;
-#pragma unroll
-                    for (int ea = 1; ea <= L; ++ea) {
-                        const uint32_t Ta = P1 ^ (1u << ea);
-                        bool d2 = false;
-#pragma unroll
-                        for (int eb = 1; eb <= L; ++eb)
-                            if (eb != ea) d2 |= hi.test(Ta ^ (1u << eb));
-                        if constexpr (L >= 3) d2 |= hi.test(Ta | 1u);
-                        dom |= d2 && !present.test(Ta);
-                    }
-                    // One level further: X = P\{a,b} (a < b), absent, is first
-                    // tested below P\{a} if that is absent (in its j = b-1
-                    // call), else below P\{b} if absent (in its j = a call),
-                    // else never.  Its expansion list holds the entries before
-                    // the removed one: {1..b-1}\{a} in the first case, {1..a-1}
-                    // in the second, plus zeros (the var-0 toggle, L >= 4).
-                    if constexpr (L >= 3) {
-#pragma unroll
-                        for (int ea = 1; ea <= L; ++ea)
-#pragma unroll
-                            for (int eb = ea + 1; eb <= L; ++eb) {
-                                const uint32_t X = P1 ^ (1u << ea) ^ (1u << eb);
-                                bool h1 = false, h2 = false;
-#pragma unroll
-                                for (int ec = 1; ec < eb; ++ec) {
-                                    if (ec == ea) continue;
-                                    const bool hc = hi.test(X ^ (1u << ec));
-                                    h1 |= hc;
-                                    if (ec < ea) h2 |= hc;
-                                }
-                                if constexpr (L >= 4) {
-                                    const bool ht = hi.test(X | 1u);
-                                    h1 |= ht;
-                                    h2 |= ht;
-                                }
-                                const bool pa = present.test(P1 ^ (1u << ea));
-                                const bool pb = present.test(P1 ^ (1u << eb));
-                                const bool hx = pa ? (!pb && h2) : h1;
-                                dom |= hx && !present.test(X);
-                            }
-                    }
-                } else {
-                    // P\{0} is the very first node tested; if absent it is
-                    // expanded with every list (1..j) + zeros, so each present
-                    // P\{0,c} is visited.
-                    constexpr uint32_t P0 = (1u << L) - 1u;
-                    bool d2 = false;
-#pragma unroll
-                    for (int ec = 1; ec < L; ++ec) d2 |= hi.test(P0 ^ 1u ^ (1u << ec));
-                    dom |= d2 && !present.test(P0 ^ 1u);
-                }
-                queued = !dom;
-            }
-            if (queued) {
-                // wave-aggregated append: one atomic per wave
-                const unsigned long long act = __ballot(1);
-                const int lane = threadIdx.x & 63;
-                const int leader = __ffsll((long long)act) - 1;
-                unsigned long long base = 0;
-                if (lane == leader) base = atomicAdd(a.qcount, (unsigned long long)__popcll(act));
-                base = __shfl(base, leader);
-                const uint64_t pos = base + (uint64_t)__popcll(act & ((1ull << lane) - 1ull));
-                // open = absent & cover(T without var 0) & not checked
-                // (checked = {empty})
-                uint64_t ow[W];
-#pragma unroll
-                for (int wj = 0; wj < W; ++wj) ow[wj] = hi.word(wj);
-                cover_words<W>(ow);
-#pragma unroll
-                for (int wj = 0; wj < W; ++wj) {
-                    const uint64_t ce = ow[wj] & 0x5555555555555555ull;
-                    ow[wj] = (ce | (ce << 1)) & ~present.word(wj) & (wj == 0 ? ~1ull : ~0ull);
-                }
-                uint64_t *e = a.queue + pos * (uint64_t)(1 + 2 * W);
-                e[0] = (toff[(uint64_t)vi * a.S + L] + rankP) | ((uint64_t)fbits(ts) << 32);
-#pragma unroll
-                for (int wj = 0; wj < W; ++wj) e[1 + wj] = hi.word(wj);
-#pragma unroll
-                for (int wj = 0; wj < W; ++wj) e[1 + W + wj] = ow[wj];
-            }
+            // decide what needs no walk; queue the rest for the walk kernel
+            const bool dom = settle_rules<L, PHASE>(present, hi, ls, queued);
+            if (queued) queue_walk(present, hi, a.queue, a.qcount, toff[vbase + L] + rankP, ts);
             out = dom ? absent_f() : -ts;
         } else if constexpr ((V & 4) != 0) {
             // decision-only walk: no key >= -ts at all -> stored; a direct
@@ -870,6 +1053,18 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         }
     }
     if (!queued) a.table[toff[(uint64_t)vi * a.S + L] + rankP] = out;
+    if constexpr (HM && !CMP) {
+        // the one-pass form keeps the subset maxima for the layers above it
+        const uint64_t vbase = (uint64_t)vi * a.S;
+        uint64_t rc[L], rz[L];
+        child_ranks<L, false>(cm, binom, rc, rz);
+        float hch = absent_f();
+        if constexpr (L > 1) {
+#pragma unroll
+            for (int i = 0; i < L; ++i) hch = fmaxf(hch, a.hsub[toff[vbase + L - 1] + rc[i]]);
+        }
+        a.hsub[toff[vbase + L] + rankP] = fmaxf(out, hch);
+    }
     if constexpr ((V & 8) != 0) {
         // per wave: lanes per category, waves with any walking lane, walk
         // steps summed over lanes and the wave's max (what the wave pays)
@@ -898,7 +1093,7 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
 // `hi` words.
 template <int L, int PHASE>
 __global__ void __launch_bounds__(kBlock) walk_kernel(const uint64_t *queue, const unsigned long long *qcount,
-                                                      float *table, uint64_t *wclock) {
+                                                      float *table, float *hsub, uint64_t *wclock) {
     const uint64_t t_start = wclock ? wall_clock64() : 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int W = bits_words(L);
@@ -934,6 +1129,7 @@ __global__ void __launch_bounds__(kBlock) walk_kernel(const uint64_t *queue, con
     if (wclock) dom = walk_open<L, BS, true>(Plocal, pvtop, hi, open, steps);
     else dom = walk_open<L, BS>(Plocal, pvtop, hi, open, steps);
     table[(uint32_t)e[0]] = dom ? absent_f() : -ts;
+    if (hsub && !dom) hsub[(uint32_t)e[0]] = fmaxf(hsub[(uint32_t)e[0]], -ts);  // subset maxima (variant bit 6)
     if (wclock) {
         // per lane: steps | dom << 31 | open count << 32 (at the queue index)
         int pc = 0;
@@ -1032,7 +1228,7 @@ __device__ __forceinline__ void walk_sliced(uint32_t T, uint32_t pv, uint32_t ac
 // one wave (64 threads) per 64*K queued sets; entries as walk_kernel's
 template <int L, int PHASE, int K>
 __global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, const unsigned long long *qcount,
-                                                         float *table, uint64_t *wclock) {
+                                                         float *table, float *hsub, uint64_t *wclock) {
     using S = Sliced<L, K>;
     const uint64_t t_start = wclock ? wall_clock64() : 0;
     constexpr int W = bits_words(L);
@@ -1101,7 +1297,9 @@ __global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, 
         if (mine + k >= qn) break;
         const uint64_t e0 = queue[(mine + k) * (uint64_t)(1 + 2 * W)];
         const float ts = __uint_as_float((uint32_t)(e0 >> 32));
-        table[(uint32_t)e0] = ((dom >> k) & 1u) ? absent_f() : -ts;
+        const bool d = (dom >> k) & 1u;
+        table[(uint32_t)e0] = d ? absent_f() : -ts;
+        if (hsub && !d) hsub[(uint32_t)e0] = fmaxf(hsub[(uint32_t)e0], -ts);  // subset maxima (variant bit 6)
     }
 }
 
@@ -2135,10 +2333,12 @@ KernelFn pick(int phase, int variant) {
         case 13: return pick_phase<L, 13>(phase);
         case 16: case 48: return pick_phase<L, 16>(phase);
         case 17: case 49: return pick_phase<L, 17>(phase);
+        case 65: return pick_phase<L, 65>(phase);
+        case 81: case 113: return pick_phase<L, 81>(phase);
         default: return nullptr;
     }
 }
-using WalkFn = void (*)(const uint64_t *, const unsigned long long *, float *, uint64_t *);
+using WalkFn = void (*)(const uint64_t *, const unsigned long long *, float *, float *, uint64_t *);
 template <int L>
 WalkFn walk_pick(int phase) {
     return phase == 0 ? walk_kernel<L, 0> : walk_kernel<L, 1>;
@@ -2156,7 +2356,7 @@ WalkFn walk_fn(int L, int phase) {
         default: return nullptr;
     }
 }
-using SlicedFn = void (*)(const uint64_t *, const unsigned long long *, float *, uint64_t *);
+using SlicedFn = void (*)(const uint64_t *, const unsigned long long *, float *, float *, uint64_t *);
 template <int L, int K>
 SlicedFn sliced_pick(int phase) {
     return phase == 0 ? walk_sliced_kernel<L, 0, K> : walk_sliced_kernel<L, 1, K>;
@@ -2769,6 +2969,7 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     sa.meta = c->d_meta.p;
     sa.tbl_off = c->d_tbl_off.p;
     sa.table = c->table.p;
+    sa.hsub = nullptr;
     sa.stats = nullptr;
     sa.dump = nullptr;
     sa.dump_cap = 0;
@@ -2783,6 +2984,10 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     // queue entries address the table with 32 bits; beyond that the one-pass
     // form (identical results) is used
     const int variant = (c->score_variant & 16) && (total_slots >> 32) ? 1 : c->score_variant;
+    if (variant & 64) {
+        if ((rc = ensure(c, c->d_hsub, total_slots))) return rc;
+        sa.hsub = c->d_hsub.p;
+    }
     const char *wck = std::getenv("ULG_WALK_CLOCK");  // walk diagnostics (synchronising)
     // Variables never read each other's slabs, so they are striped over G
     // groups on concurrent streams: a group's latency-bound walk kernels
@@ -2879,7 +3084,7 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     // per phase over all variables on the context stream -- no queue, no walk
     // launch, no stream groups.  The rest: per group, score + queued walk.
     const int Ls = (variant & 16) && !(variant & 8) && !wck ? std::min(kmax, std::min(kMaxL, c->score_small_layers)) : 0;
-    const int vsmall = variant & 1;
+    const int vsmall = variant & 65;  // the one-pass form (keeping the subset maxima under bit 6)
     bool forked = false;
     // -r (score_calculator.cpp:33-52,78): checked after every complete layer
     const auto t_call = std::chrono::steady_clock::now();
@@ -2921,7 +3126,7 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
                      (uint64_t)(uintptr_t)c->out_sets.p, (uint64_t)(uintptr_t)c->out_scores.p,
                      (uint64_t)(uintptr_t)c->out_offsets.p, (uint64_t)(uintptr_t)c->d_blk.p,
                      (uint64_t)(uintptr_t)c->gram.p, (uint64_t)(uintptr_t)c->d_binom.p,
-                     (uint64_t)(uintptr_t)c->d_binom64.p, (uint64_t)total_slots});
+                     (uint64_t)(uintptr_t)c->d_binom64.p, (uint64_t)(uintptr_t)c->d_hsub.p, (uint64_t)total_slots});
         for (int i = 0; i < nv; ++i) gkey.push_back((uint64_t)vars[i]);
         for (int i = 0; i < nv; ++i) gkey.push_back(candidates[i]);
         for (const std::string &nm : c->prof_only) gkey.push_back(std::hash<std::string>{}(nm));
@@ -3028,7 +3233,7 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
                         if (wck) ULG_HIP(c, hipMemsetAsync(c->d_dump.p, 0, 24 * sb, st));
                         prof_begin_s(c, kWalkNames[ph][L], st);
                         hipLaunchKernelGGL(sliced_fn(L, ph), dim3((unsigned)sb), dim3(64), 0, st, sa.queue, qc,
-                                           c->table.p, wck ? c->d_dump.p : nullptr);
+                                           c->table.p, sa.hsub, wck ? c->d_dump.p : nullptr);
                         prof_end_s(c, st);
                         if (wck) {
                             std::vector<uint64_t> hw((size_t)3 * sb);
@@ -3054,7 +3259,7 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
                         if (wck) ULG_HIP(c, hipMemsetAsync(c->d_dump.p, 0, 8 * wck_words, st));
                         prof_begin_s(c, kWalkNames[ph][L], st);
                         hipLaunchKernelGGL(wfn, dim3((unsigned)blocks), dim3(kBlock), wl, st, sa.queue, qc, c->table.p,
-                                           wck ? c->d_dump.p : nullptr);
+                                           sa.hsub, wck ? c->d_dump.p : nullptr);
                         prof_end_s(c, st);
                         if (wck) {
                             std::vector<uint64_t> hw(wck_words);

@@ -162,7 +162,7 @@ void ulg_destroy(ulg_ctx *c) {
     c->sync_events.clear();
     release(c->raw); release(c->z); release(c->gram); release(c->partials); release(c->colstat);
     release(c->table); release(c->d_tbl_off); release(c->d_work); release(c->d_blk);
-    release(c->d_cand); release(c->d_meta); release(c->d_binom); release(c->d_binom64); release(c->d_wqueue); release(c->d_wbits); release(c->d_stats); release(c->d_dump); release(c->d_queue); release(c->d_qcount); release(c->d_workg); release(c->d_vwork); release(c->d_hq); release(c->d_hqc); release(c->d_hmax); release(c->d_hoff); release(c->d_hmeta); release(c->d_scount);
+    release(c->d_cand); release(c->d_meta); release(c->d_binom); release(c->d_binom64); release(c->d_wqueue); release(c->d_wbits); release(c->d_stats); release(c->d_dump); release(c->d_queue); release(c->d_qcount); release(c->d_workg); release(c->d_vwork); release(c->d_hq); release(c->d_hqc); release(c->d_hmax); release(c->d_hoff); release(c->d_hmeta); release(c->d_scount); release(c->d_hsub);
     release(c->out_sets); release(c->out_scores); release(c->out_offsets);
     release(c->qbuf_in); release(c->qbuf_out);
     pss_release(c);
@@ -191,8 +191,9 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         return ULG_OK;
     }
     if (std::strcmp(name, "score_variant") == 0) {
-        if (value < 0 || (value > 7 && value != 13 && value != 16 && value != 17 && value != 48 && value != 49))
-            return set_err(c, ULG_ERR_ARG, "score_variant must be 0..7, 13, 16, 17, 48 or 49");
+        if (value < 0 || (value > 7 && value != 13 && value != 16 && value != 17 && value != 48 && value != 49 &&
+                          value != 81 && value != 113))
+            return set_err(c, ULG_ERR_ARG, "score_variant must be 0..7, 13, 16, 17, 48, 49, 81 or 113");
         c->score_variant = (int)value;
         return ULG_OK;
     }

@@ -69,7 +69,7 @@ struct ulg_ctx {
     int64_t total_stored = 0;
     int64_t total_scored = 0;
     bool scored = false;
-    int score_variant = 49;
+    int score_variant = 113;
     int score_streams = 3;                  // scorer variable groups on concurrent streams
     int score_small_layers = 4;             // layers <= this run one-pass on one stream (two-pass variants)
     std::vector<hipStream_t> aux_streams;   // created on first use
@@ -92,6 +92,7 @@ struct ulg_ctx {
     std::vector<ulg::ProfRec> gprof;  // profiling events inside the graph
     int sweep_xcd = 1;             // GPU sweep launches: contiguous runs of nodes per XCD           // GPU search: successor costs in the sweep's (layer, colex) order
     ulg::DevBuf<float> table;
+    ulg::DevBuf<float> d_hsub;    // score_variant bit 6: subset maxima, table layout
     ulg::DevBuf<uint64_t> d_tbl_off, d_work, d_blk;
     ulg::DevBuf<uint8_t> d_cand;  // [nv][64] compact index -> variable
     ulg::DevBuf<int> d_meta;      // [nv][4]: var, m, var0in, pad
