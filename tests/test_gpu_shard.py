@@ -151,14 +151,17 @@ def _sweep_worker(rank, world, port, out_dir, n, N, k, seed):
     dist.destroy_process_group()
 
 
-@pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,n,N,k,seed", [(2, 20, 10000, 4, 9200), (3, 22, 6000, 5, 9751)])
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world,n,N,k,seed", [(2, 20, 10000, 4, 9200), (3, 22, 6000, 5, 9751),
+                                              (2, 26, 5000, 3, 9760), (2, 28, 5000, 3, 9761)])
 def test_table_sharded_sweep_equals_single_gpu(tmp_path, ulg_ctx, world, n, N, k, seed):
-    """SURVEY 8e's n >= 31 path, rehearsed at small n: each rank holds the
+    """SURVEY 8e's n >= 31 path, rehearsed below n = 31: each rank holds the
     best-score tables and sweep slices of its own variables only
     (ulg_sweep_shard_begin), one MIN all-reduce per layer combines the ranks'
     (cost, leaf) keys.  Cost bits, order, parent sets and the reached-node
-    count equal the single-GPU sweep's; the owned variables partition 0..n-1."""
+    count equal the single-GPU sweep's; the owned variables partition 0..n-1.
+    n = 26 and 28 run the 32-bit colex and key paths near C5's sizes (the
+    middle layer of n = 28 holds C(28, 14) = 40,116,600 nodes)."""
     import synth
     mp.start_processes(_sweep_worker, args=(world, _free_port(), str(tmp_path), n, N, k, seed), nprocs=world,
                        join=True, start_method="spawn")

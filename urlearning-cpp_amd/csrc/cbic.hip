@@ -2462,6 +2462,12 @@ struct WideGroup {
     unsigned int *hqc = nullptr;
 };
 
+// table[pairs[2j]] = pairs[2j + 1] (the bits of a float): the host walks' decisions
+__global__ void scatter_decisions_kernel(const uint64_t *pairs, uint32_t cnt, float *table) {
+    const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+    if (j < cnt) table[pairs[2 * (uint64_t)j]] = __uint_as_float((uint32_t)pairs[2 * (uint64_t)j + 1]);
+}
+
 constexpr uint64_t kHostFewReplays = 64;  // launches of at most this many replays ...
 constexpr uint64_t kHostFewBudget = 512;   // ... hand walks to the host after this many iterations
 
@@ -2474,6 +2480,7 @@ int host_walks(ulg_ctx *c, WideGroup &G, int L, int ph, int q, uint64_t sn, uint
     unsigned int cnt = 0;
     ULG_HIP(c, hipMemcpyAsync(&cnt, G.hqc, 4, hipMemcpyDeviceToHost, G.st));
     ULG_HIP(c, hipStreamSynchronize(G.st));
+    const auto th1 = std::chrono::steady_clock::now();  // the LDS replays are done
     if (cnt == 0) return ULG_OK;
     if (cnt > sn) return set_err(c, ULG_ERR_STATE, "ulg_cbic_score: host walk queue overflow");
     std::vector<uint32_t> idx(cnt);
@@ -2487,6 +2494,8 @@ int host_walks(ulg_ctx *c, WideGroup &G, int L, int ph, int q, uint64_t sn, uint
     std::vector<uint64_t> bits;
     std::vector<uint32_t> vals(cnt);
     std::vector<uint64_t> slots(cnt);
+    double walk_ms = 0.0, copy_ms = 0.0;
+    const auto th2 = std::chrono::steady_clock::now();
     for (uint64_t b0 = 0; b0 < cnt; b0 += per) {
         const uint64_t k = std::min<uint64_t>(per, cnt - b0);
         // this chunk's queue indices (the kernel's list is on the host now)
@@ -2497,8 +2506,11 @@ int host_walks(ulg_ctx *c, WideGroup &G, int L, int ph, int q, uint64_t sn, uint
         prof_end_s(c, G.st);
         ULG_HIP(c, hipGetLastError());
         bits.resize((size_t)(k * 2 * nw));
+        ULG_HIP(c, hipStreamSynchronize(G.st));
+        const auto tf0 = std::chrono::steady_clock::now();
         ULG_HIP(c, hipMemcpyAsync(bits.data(), G.bits, bits.size() * 8, hipMemcpyDeviceToHost, G.st));
         ULG_HIP(c, hipStreamSynchronize(G.st));
+        copy_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count();
         if (const char *dd = std::getenv("ULG_DUMP_HOSTWALK")) {  // diagnostics: the bitsets of the largest ones
             static std::atomic<int> nd{0};
             if (q >= 15 && nd < 16) {
@@ -2523,24 +2535,43 @@ int host_walks(ulg_ctx *c, WideGroup &G, int L, int ph, int q, uint64_t sn, uint
                 slots[b0 + j] = en[0];
             }
         };
-        const unsigned nth = (unsigned)std::min<uint64_t>(k, std::min(8u, std::max(1u, std::thread::hardware_concurrency())));
+        const unsigned nth = (unsigned)std::min<uint64_t>(
+            k, std::min((unsigned)c->wide_host_threads, std::max(1u, std::thread::hardware_concurrency())));
+        const auto twa = std::chrono::steady_clock::now();
         std::vector<std::thread> th;
         for (unsigned t = 1; t < nth; ++t) th.emplace_back(work);
         work();
         for (auto &t : th) t.join();
+        walk_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - twa).count();
         if (bad) {
             const unsigned long long one = 1;
             ULG_HIP(c, hipMemcpyAsync(errf, &one, 8, hipMemcpyHostToDevice, G.st));
         }
     }
-    for (unsigned j = 0; j < cnt; ++j)
-        ULG_HIP(c, hipMemcpyAsync(G.wa.table + slots[j], &vals[j], 4, hipMemcpyHostToDevice, G.st));
-    ULG_HIP(c, hipStreamSynchronize(G.st));  // vals is about to go
+    // the decisions: one copy of (slot, value) pairs into the group's bitset
+    // slice (free again), then one scatter launch
+    const auto tw1 = std::chrono::steady_clock::now();
+    std::vector<uint64_t> pairs((size_t)2 * cnt);
+    for (unsigned j = 0; j < cnt; ++j) {
+        pairs[2 * (size_t)j] = slots[j];
+        pairs[2 * (size_t)j + 1] = vals[j];
+    }
+    ULG_HIP(c, hipMemcpyAsync(G.bits, pairs.data(), pairs.size() * 8, hipMemcpyHostToDevice, G.st));
+    scatter_decisions_kernel<<<(cnt + 255) / 256, 256, 0, G.st>>>(G.bits, cnt, G.wa.table);
+    ULG_HIP(c, hipGetLastError());
+    ULG_HIP(c, hipStreamSynchronize(G.st));  // pairs is about to go
     static const bool wstat = std::getenv("ULG_WALK_STATS") != nullptr;
-    if (wstat)
-        std::fprintf(stderr, "walk_host_stats L=%d phase=%d q=%d handed=%u of %llu ms=%.2f\n", L, ph, q, cnt,
-                     (unsigned long long)sn,
-                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count());
+    if (wstat) {
+        const auto tw2 = std::chrono::steady_clock::now();
+        auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+            return std::chrono::duration<double, std::milli>(b - a).count();
+        };
+        std::fprintf(stderr,
+                     "walk_host_stats L=%d phase=%d q=%d handed=%u of %llu ms=%.2f (gpu replays %.2f, lists %.2f, "
+                     "bits copy %.2f, walks %.2f, write %.2f)\n",
+                     L, ph, q, cnt, (unsigned long long)sn, ms(th0, tw2), ms(th0, th1), ms(th1, th2), copy_ms, walk_ms,
+                     ms(tw1, tw2));
+    }
     return ULG_OK;
 }
 

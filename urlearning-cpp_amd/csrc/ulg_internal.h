@@ -84,6 +84,7 @@ struct ulg_ctx {
     int wide_lds = 1;              // wide walks: long ones replayed with their bitsets in LDS
     int wide_pool = 1;             // wide layers variable by variable on score_streams host threads
     uint64_t wide_host_iters = 4096;     // LDS replays past this many iterations finish on host threads (0: never)
+    int wide_host_threads = 8;           // host threads per wide-layer launch for those replays
     int score_xcd = 1;             // scoring kernels: contiguous runs of sets per XCD
     int score_graph = 1;           // scoring call: replay the captured launch sequence
     hipGraph_t graph = nullptr;    // the captured scoring launches, its instance, its key
