@@ -150,10 +150,13 @@ def test_wide_hicover_prune_identical_lists(ulg_ctx):
 @pytest.mark.timeout(300)
 def test_wide_pool_identical_lists_c4(ulg_ctx):
     """ulg_set_option("wide_pool"): the wide layers variable by variable on
-    score_streams host threads (default) or every stream group's part of a
-    layer together; "wide_host": LDS replays past that many iterations
-    finish on host threads (1: every replay does, so host_walk re-decides
-    all of them; 0: none).  All 30 C4 variables (n=30, N=100k, MMPC,
+    score_streams host threads, every stream group's part of a layer
+    together, or picked by the candidate-count spread (2, default);
+    "wide_host": LDS replays past that many iterations finish on host threads
+    (1: every replay does, so host_walk re-decides all of them; 0: none) in
+    launches of at most "wide_host_max" replays, "wide_host_first": launches
+    of at most that many replays go to the host whole, "wide_host_threads":
+    host threads per launch.  All 30 C4 variables (n=30, N=100k, MMPC,
     -p = n-1; the wide layers reach 18) give bit-identical lists in every
     combination, and the pool's repeat call too."""
     import ulg
@@ -164,17 +167,20 @@ def test_wide_pool_identical_lists_c4(ulg_ctx):
     cands = ulg.candidates_from_edges(rows, n)
     vs = list(range(n))
     out = []
+    defaults = dict(wide_pool=2, score_streams=3, wide_host=1024, wide_host_max=4096, wide_host_first=0,
+                    wide_host_threads=16)
+    combos = [dict(wide_pool=0, wide_host=0), dict(), dict(), dict(wide_pool=1, wide_host=4096),
+              dict(wide_pool=1, score_streams=2), dict(wide_pool=1, wide_host=1, wide_host_max=1 << 40),
+              dict(wide_pool=0, score_streams=1, wide_host=64), dict(wide_host_first=64, wide_host_threads=3)]
     try:
-        for pool, streams, host in ((0, 3, 0), (1, 3, 4096), (1, 3, 4096), (1, 2, 4096), (1, 3, 1), (0, 1, 64)):
-            ulg_ctx.set_option("wide_pool", pool)
-            ulg_ctx.set_option("score_streams", streams)
-            ulg_ctx.set_option("wide_host", host)
+        for combo in combos:
+            for name, val in dict(defaults, **combo).items():
+                ulg_ctx.set_option(name, val)
             offs, sets, scores = ulg_ctx.score_all(vs, [cands[v] for v in vs], n - 1)
             out.append((np.asarray(offs).copy(), np.asarray(sets).copy(), np.asarray(scores).copy()))
     finally:
-        ulg_ctx.set_option("wide_pool", 1)
-        ulg_ctx.set_option("score_streams", 3)
-        ulg_ctx.set_option("wide_host", 4096)
+        for name, val in defaults.items():
+            ulg_ctx.set_option(name, val)
     for o in out[1:]:
         assert np.array_equal(out[0][0], o[0])
         assert np.array_equal(out[0][1], o[1])

@@ -2738,8 +2738,27 @@ int score_wide_groups(ulg_ctx *c, int L, int ph, std::vector<WideGroup> &gs, int
         // walks past this many iterations finish on the host; with few
         // replays in the launch the host takes them sooner (it runs them in
         // parallel threads, while the GPU's launch time is its longest walk)
-        const uint64_t hbud = sn <= kHostFewReplays ? std::min<uint64_t>(c->wide_host_iters, kHostFewBudget)
-                                                    : c->wide_host_iters;
+        // Host threads take the long walks only of launches with few replays
+        // (wide_host_max): with thousands of long walks (C1 at lambda 0.5) a
+        // few host threads would queue them behind each other while the GPU
+        // runs them all at once (C1 10.7 s GPU-only against 32 s with every
+        // launch handing over).
+        const uint64_t hbud = sn > c->wide_host_max ? 0
+                              : sn <= kHostFewReplays ? std::min<uint64_t>(c->wide_host_iters, kHostFewBudget)
+                                                      : c->wide_host_iters;
+        if (hbud && sn <= c->wide_host_first) {
+            // so few replays that the host takes them all at once: no GPU
+            // replay phase (its length is its longest walk's), straight to
+            // the fills, the copy and the host threads
+            std::vector<uint32_t> all((size_t)sn);
+            for (uint32_t j = 0; j < (uint32_t)sn; ++j) all[j] = j;
+            const unsigned int n32 = (unsigned int)sn;
+            ULG_HIP(c, hipMemcpyAsync(G.hq, all.data(), all.size() * 4, hipMemcpyHostToDevice, G.st));
+            ULG_HIP(c, hipMemcpyAsync(G.hqc, &n32, 4, hipMemcpyHostToDevice, G.st));
+            int rc2;
+            if ((rc2 = host_walks(c, G, L, ph, q, sn, slice, errf))) return rc2;
+            continue;
+        }
         if (hbud) ULG_HIP(c, hipMemsetAsync(G.hqc, 0, 4, G.st));
         for (uint64_t base = 0; base < sn; base += per) {
             const uint64_t k = std::min<uint64_t>(per, sn - base);
@@ -3117,6 +3136,23 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     const int Ls = (variant & 16) && !(variant & 8) && !wck ? std::min(kmax, std::min(kMaxL, c->score_small_layers)) : 0;
     const int vsmall = variant & 65;  // the one-pass form (keeping the subset maxima under bit 6)
     bool forked = false;
+    // The wide layers variable by variable (wide_pool 1) pay when the
+    // variables that reach them differ in size: the long replays of one then
+    // hold no other's next layer (C4: 2-hop sets of 10..18 candidates).  On
+    // equal candidate sets (C1: a full skeleton) the grouped form's larger
+    // launches keep more replays in flight (C1 at lambda 0.5: 10.7 s against
+    // 15.2 s).  wide_pool 2 (default) picks the pool when the wide variables'
+    // candidate counts span at least 2.
+    bool use_pool = c->wide_pool == 1;
+    if (c->wide_pool == 2) {
+        int lo_m = 64, hi_m = -1;
+        for (int i = 0; i < nv; ++i)
+            if (std::min(mv[i], max_parents) > kMaxL) {
+                lo_m = std::min(lo_m, mv[i]);
+                hi_m = std::max(hi_m, mv[i]);
+            }
+        use_pool = hi_m >= 0 && hi_m - lo_m >= 2;
+    }
     // -r (score_calculator.cpp:33-52,78): checked after every complete layer
     const auto t_call = std::chrono::steady_clock::now();
     c->out_of_time = 0;
@@ -3200,7 +3236,7 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
                 for (int g = 1; g < G; ++g) ULG_HIP(c, hipStreamWaitEvent(gst[g], c->sync_events[0], 0));
                 forked = true;
             }
-            if (L > kMaxL && G > 1 && c->time_limit_ms == 0 && c->wide_pool) {
+            if (L > kMaxL && G > 1 && c->time_limit_ms == 0 && use_pool) {
                 // The wide layers variable by variable on G host threads (one
                 // stream each): a variable's layers depend only on its own
                 // lower layers, and the long LDS replays of one variable no
@@ -3334,7 +3370,7 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
                                                          hoff, meta, c->wide_pinned)))
                 return rc;
         }
-        if (L > kMaxL && G > 1 && c->time_limit_ms == 0 && c->wide_pool) break;  // the pool ran every wide layer
+        if (L > kMaxL && G > 1 && c->time_limit_ms == 0 && use_pool) break;  // the pool ran every wide layer
         if (c->time_limit_ms > 0 && L < kmax) {
             for (int g = 0; g < (forked ? G : 1); ++g) ULG_HIP(c, hipStreamSynchronize(gst[g]));
             const double ms =

@@ -228,13 +228,23 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         c->wide_host_iters = (uint64_t)value;
         return ULG_OK;
     }
+    if (std::strcmp(name, "wide_host_max") == 0) {
+        if (value < 0) return set_err(c, ULG_ERR_ARG, "wide_host_max must be >= 0");
+        c->wide_host_max = (uint64_t)value;
+        return ULG_OK;
+    }
+    if (std::strcmp(name, "wide_host_first") == 0) {
+        if (value < 0) return set_err(c, ULG_ERR_ARG, "wide_host_first must be >= 0");
+        c->wide_host_first = (uint64_t)value;
+        return ULG_OK;
+    }
     if (std::strcmp(name, "wide_host_threads") == 0) {
         if (value < 1 || value > 64) return set_err(c, ULG_ERR_ARG, "wide_host_threads must be 1..64");
         c->wide_host_threads = (int)value;
         return ULG_OK;
     }
     if (std::strcmp(name, "wide_pool") == 0) {
-        if (value < 0 || value > 1) return set_err(c, ULG_ERR_ARG, "wide_pool must be 0 or 1");
+        if (value < 0 || value > 2) return set_err(c, ULG_ERR_ARG, "wide_pool must be 0, 1 or 2");
         c->wide_pool = (int)value;
         return ULG_OK;
     }

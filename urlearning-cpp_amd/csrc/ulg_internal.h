@@ -82,9 +82,11 @@ struct ulg_ctx {
     int wide_prune = 1;            // wide walks: skip absent nodes whose subsets hold no key >= -ts
     int wide_reduced = 1;          // wide walks: skip the recursion's no-op re-tests
     int wide_lds = 1;              // wide walks: long ones replayed with their bitsets in LDS
-    int wide_pool = 1;             // wide layers variable by variable on score_streams host threads
-    uint64_t wide_host_iters = 4096;     // LDS replays past this many iterations finish on host threads (0: never)
-    int wide_host_threads = 8;           // host threads per wide-layer launch for those replays
+    int wide_pool = 2;             // wide layers variable by variable on score_streams host threads (2: auto)
+    uint64_t wide_host_iters = 1024;     // LDS replays past this many iterations finish on host threads (0: never)
+    int wide_host_threads = 16;          // host threads per wide-layer launch for those replays
+    uint64_t wide_host_max = 4096;       // ... in launches of at most this many LDS replays
+    uint64_t wide_host_first = 0;        // launches of at most this many replays go to the host whole
     int score_xcd = 1;             // scoring kernels: contiguous runs of sets per XCD
     int score_graph = 1;           // scoring call: replay the captured launch sequence
     hipGraph_t graph = nullptr;    // the captured scoring launches, its instance, its key
