@@ -95,7 +95,9 @@ def cpu_baseline(cfg, X, target_s=15.0):
 
 
 PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r2")
-PMC_TRAFFIC = os.path.join(PROFILES, "pmc_traffic.json")
+# the scorer's passes were re-taken in round 3 (score_variant 113); the
+# sweep's kernel is unchanged since round 2
+PMC_TRAFFIC = os.path.join(os.path.dirname(PROFILES), "r3", "pmc_traffic.json")
 
 
 def pmc_traffic(cfg, sets, label):
@@ -109,7 +111,7 @@ def pmc_traffic(cfg, sets, label):
     if (t.get("config_id") != cfg["id"] or round(t.get("sets_per_launch", -1)) != round(sets)
             or t.get("label") != label):
         return None, None
-    return t["traffic_bytes_per_launch"], "profiles/r2/pmc_traffic.json"
+    return t["traffic_bytes_per_launch"], "profiles/r3/pmc_traffic.json"
 
 
 def roofline(ctx, cfg, per_layer_sets, steps):

@@ -39,6 +39,15 @@ constexpr int kTileBits = 14;  // pass A: 2^14 u32 = 64 KiB LDS
 constexpr int kRowBits = 4;    // pass B rows: 16 contiguous u32 = 64 B
 constexpr int kColBits = 10;   // pass B: 2^10 rows x 16 = 2^14 u32
 
+// HIP caps blocks x threads along one grid dimension at 2^32 - 1, so launches
+// of more blocks spread them over y (n = 28 full skeleton: the last pass B
+// has 28 x 2^20 blocks of 1024 threads); flat_block() is the block's index.
+constexpr uint64_t kGridX = 1ull << 20;
+inline dim3 flat_grid(uint64_t blocks) {
+    return dim3((unsigned)std::min<uint64_t>(blocks, kGridX), (unsigned)((blocks + kGridX - 1) / kGridX));
+}
+__device__ __forceinline__ uint64_t flat_block() { return (uint64_t)blockIdx.y * gridDim.x + blockIdx.x; }
+
 // D_v = union of v's stored sets inside scope (variables outside scope get
 // D_v = {} and a one-entry table)
 __global__ void __launch_bounds__(kB) support_kernel(const uint64_t *sets, const int64_t *offsets, int n,
@@ -73,17 +82,19 @@ __global__ void __launch_bounds__(1024) zeta_tile_kernel(uint32_t *table, const 
                                                          const int *mbits, int nvar) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t *t = reinterpret_cast<uint32_t *>(smem);
+    const int64_t blk = (int64_t)flat_block();
+    if (blk >= tiles_prefix[nvar]) return;
     // which variable / tile
     int lo = 0, hi = nvar;
     while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
-        if (tiles_prefix[mid] <= (int)blockIdx.x) lo = mid; else hi = mid;
+        if (tiles_prefix[mid] <= blk) lo = mid; else hi = mid;
     }
     const int v = lo;
     const int m = mbits[v];
     const int T = m < kTileBits ? m : kTileBits;
     const uint64_t size = 1ull << T;
-    const uint64_t base = tb_off[v] + ((uint64_t)(blockIdx.x - tiles_prefix[v]) << T);
+    const uint64_t base = tb_off[v] + ((uint64_t)(blk - tiles_prefix[v]) << T);
     for (uint64_t i = threadIdx.x; i < size; i += 1024) t[i] = table[base + i];
     __syncthreads();
     for (int b = 0; b < T; ++b) {
@@ -110,17 +121,19 @@ struct ZetaBArgs {
 __global__ void __launch_bounds__(1024) zeta_strided_kernel(ZetaBArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t *t = reinterpret_cast<uint32_t *>(smem);
+    const int64_t blk = (int64_t)flat_block();
+    if (blk >= a.blocks_prefix[a.nvar]) return;
     int lo = 0, hi = a.nvar;
     while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
-        if (a.blocks_prefix[mid] <= (int)blockIdx.x) lo = mid; else hi = mid;
+        if (a.blocks_prefix[mid] <= blk) lo = mid; else hi = mid;
     }
     const int v = lo;
     const int m = a.mbits[v];
     const int bit_lo = a.bit_lo;
     const int G = std::min(kColBits, m - bit_lo);
     const int nlow = bit_lo - kRowBits;
-    const uint64_t bid = blockIdx.x - a.blocks_prefix[v];
+    const uint64_t bid = (uint64_t)(blk - a.blocks_prefix[v]);
     // tile origin inside v's table; v's table itself starts at tb_off[v], which
     // is not aligned to 2^m when the supports differ in size: add, never OR
     uint32_t *tv = a.table + a.tb_off[v];
@@ -205,7 +218,8 @@ __global__ void __launch_bounds__(1024) zeta_tile_reg_kernel(uint32_t *table, ui
     uint32_t *t = reinterpret_cast<uint32_t *>(smem);
     __shared__ int64_t range[2];
     const int tid = threadIdx.x;
-    const uint64_t base = (uint64_t)blockIdx.x << kRegTileBits;  // tiles are contiguous over all variables
+    if (flat_block() >= ntiles_total) return;
+    const uint64_t base = flat_block() << kRegTileBits;  // tiles are contiguous over all variables
     if (tid == 0) {
         range[0] = lower_bound_u64(eidx, nent, base);
         range[1] = lower_bound_u64(eidx, nent, base + (1ull << kRegTileBits));
@@ -250,15 +264,17 @@ __global__ void __launch_bounds__(1024) zeta_tile_reg_kernel(uint32_t *table, ui
 __global__ void __launch_bounds__(1024) zeta_strided_reg_kernel(ZetaBArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t *t = reinterpret_cast<uint32_t *>(smem);
+    const int64_t blk = (int64_t)flat_block();
+    if (blk >= a.blocks_prefix[a.nvar]) return;
     int lo = 0, hi = a.nvar;
     while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
-        if (a.blocks_prefix[mid] <= (int)blockIdx.x) lo = mid; else hi = mid;
+        if (a.blocks_prefix[mid] <= blk) lo = mid; else hi = mid;
     }
     const int v = lo;
     const int bit_lo = a.bit_lo;
     const int nlow = bit_lo - kRowBits;
-    const uint64_t bid = blockIdx.x - a.blocks_prefix[v];
+    const uint64_t bid = (uint64_t)(blk - a.blocks_prefix[v]);
     uint32_t *tv = a.table + a.tb_off[v];
     const uint64_t base = ((bid & ((1ull << nlow) - 1)) << kRowBits) | ((bid >> nlow) << (bit_lo + 10));
     const int tid = threadIdx.x, c = tid & 15, q = tid >> 4;
@@ -306,7 +322,7 @@ __global__ void __launch_bounds__(kB) cost_rows_kernel(SearchDev d, const int *m
 }
 
 __global__ void __launch_bounds__(kB) cost_table_kernel(const uint32_t *table, uint64_t total, float *costs) {
-    const uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x;
+    const uint64_t i = flat_block() * kB + threadIdx.x;
     if (i < total) costs[i] = ord_cost(table[i]);
 }
 
@@ -487,7 +503,7 @@ int search_build_tables(ulg_ctx *c, uint64_t scope, uint64_t tvars) {
         ULG_HIP(c, hipFuncSetAttribute((const void *)zeta_tile_reg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        kPadLds * 4));
         prof_begin(c, "bs_zeta_tile");
-        zeta_tile_reg_kernel<<<(unsigned)(total >> kRegTileBits), 1024, (size_t)kPadLds * 4, c->stream>>>(
+        zeta_tile_reg_kernel<<<flat_grid(total >> kRegTileBits), 1024, (size_t)kPadLds * 4, c->stream>>>(
             s.d_table.p, total >> kRegTileBits, s.e_idx2.p, s.e_key2.p, nsets);
         prof_end(c);
         ULG_HIP(c, hipGetLastError());
@@ -509,7 +525,7 @@ int search_build_tables(ulg_ctx *c, uint64_t scope, uint64_t tvars) {
     const size_t ldsA = (size_t)4 << std::min(maxm0, kTileBits);
     ULG_HIP(c, hipFuncSetAttribute((const void *)zeta_tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 << kTileBits)));
     prof_begin(c, "bs_zeta_tile");
-    zeta_tile_kernel<<<tiles_prefix[n], 1024, ldsA, c->stream>>>(s.d_table.p, s.d_tb_off.p, s.d_prefix.p, s.d_mbits.p, n);
+    zeta_tile_kernel<<<flat_grid((uint64_t)tiles_prefix[n]), 1024, ldsA, c->stream>>>(s.d_table.p, s.d_tb_off.p, s.d_prefix.p, s.d_mbits.p, n);
     prof_end(c);
     ULG_HIP(c, hipGetLastError());
     }
@@ -535,9 +551,9 @@ int search_build_tables(ulg_ctx *c, uint64_t scope, uint64_t tvars) {
         if (full_window) {
             ULG_HIP(c, hipFuncSetAttribute((const void *)zeta_strided_reg_kernel,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, kPadLds * 4));
-            zeta_strided_reg_kernel<<<blocks_prefix[n], 1024, (size_t)kPadLds * 4, c->stream>>>(za);
+            zeta_strided_reg_kernel<<<flat_grid((uint64_t)blocks_prefix[n]), 1024, (size_t)kPadLds * 4, c->stream>>>(za);
         } else {
-            zeta_strided_kernel<<<blocks_prefix[n], 1024, (size_t)4 << (G + kRowBits), c->stream>>>(za);
+            zeta_strided_kernel<<<flat_grid((uint64_t)blocks_prefix[n]), 1024, (size_t)4 << (G + kRowBits), c->stream>>>(za);
         }
         prof_end(c);
         ULG_HIP(c, hipGetLastError());
@@ -651,7 +667,7 @@ int search_cost_table_host(ulg_ctx *c) {
     int rc;
     if ((rc = ensure(c, s.d_cost_table, total))) return rc;
     prof_begin(c, "bs_cost_table");
-    cost_table_kernel<<<(unsigned)((total + kB - 1) / kB), kB, 0, c->stream>>>(s.d_table.p, total, s.d_cost_table.p);
+    cost_table_kernel<<<flat_grid((total + kB - 1) / kB), kB, 0, c->stream>>>(s.d_table.p, total, s.d_cost_table.p);
     prof_end(c);
     if (s.host_cost_cap < total) {
         if (s.host_costs) (void)hipHostFree(s.host_costs);
