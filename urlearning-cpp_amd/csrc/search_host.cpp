@@ -231,8 +231,12 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
     // prefetched before its pop, so they arrive while the pop descends the
     // heap (C3 16.9 -> 14.0 s, 2 alternating A/B runs); bit 3 adds the coming
     // decrease-keys' heap entries after the pop (measured no better).
-    static const int pfmode = std::getenv("ULG_EXACT_PF") ? std::atoi(std::getenv("ULG_EXACT_PF")) : 6;
+    const int pfmode = std::getenv("ULG_EXACT_PF") ? std::atoi(std::getenv("ULG_EXACT_PF")) : 6;
     open.pf5 = (pfmode & 2) != 0;
+    // bit 4: the next pop's bottom ULG_EXACT_SPEC_DEEP levels are prefetched
+    // before the successor visits (DenseHeap::spec_prefetch)
+    const bool spec = (pfmode & 16) != 0;
+    const int spec_deep = std::getenv("ULG_EXACT_SPEC_DEEP") ? std::atoi(std::getenv("ULG_EXACT_SPEC_DEEP")) : 6;
 
     // slot bit of each variable, and its column in the row table
     uint32_t sbit[64] = {0};
@@ -253,6 +257,7 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
     const float upperBound = FLT_MAX;
     int64_t nexp = 0;
     static const bool prof = std::getenv("ULG_EXACT_PROF") != nullptr;
+    open.spec_track = spec && prof;
     uint64_t c_pop = 0, c_succ = 0, t0 = 0, t1 = 0;
     uint64_t pop_hist[64][2] = {};  // pop cycles by log2(heap length)
     int64_t n_push = 0, n_upd = 0, n_succ = 0;
@@ -273,6 +278,14 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
             __builtin_prefetch(trow);
             __builtin_prefetch(trow + nl - 1);
             for (uint64_t x = the_scc & ~tv; x; x &= x - 1) __builtin_prefetch(&recs[top | sbit[__builtin_ctzll(x)]], 1);
+            if ((pfmode & 96) == 96)
+                // bit 6 (with bit 5): those records arrived during the last
+                // expansion, so the heap entries of the coming decrease-keys
+                // can be requested before the pop too
+                for (uint64_t x = the_scc & ~tv; x; x &= x - 1) {
+                    const int32_t p = recs[top | sbit[__builtin_ctzll(x)]].pq;
+                    if (p > 0) __builtin_prefetch(&open.a[p - 1], 1);
+                }
         }
         const uint32_t ui = open.pop();
         if (prof) {
@@ -309,6 +322,19 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
                 if (p > 0) __builtin_prefetch(&open.a[p - 1], 1);
             }
         }
+        // the next pop's bottom levels, fetched during the visits (DenseHeap::spec_prefetch)
+        if (spec) open.spec_prefetch(spec_deep);
+        if ((pfmode & 32) && open.len > 0) {
+            // bit 5: the next pop is the heap top now (a successor hardly ever
+            // takes the root): its successor records and cost row start
+            // arriving during these visits instead of during its own pop
+            const uint32_t nt = open.a[0].slot();
+            const uint64_t ntv = g_have_bmi2 ? pdep_bmi2(nt, scope) : pdep64(nt, scope);
+            const float *nrow = rows + (uint64_t)nt * (uint64_t)nl;
+            __builtin_prefetch(nrow);
+            __builtin_prefetch(nrow + nl - 1);
+            for (uint64_t x = the_scc & ~ntv; x; x &= x - 1) __builtin_prefetch(&recs[nt | sbit[__builtin_ctzll(x)]], 1);
+        }
         for (uint64_t x = leaves; x; x &= x - 1) {
             const int leaf = __builtin_ctzll(x);
             const uint32_t si = ui | sbit[leaf];
@@ -337,9 +363,10 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
     if (prof)
         std::fprintf(stderr,
                      "exact_prof(dense) expanded=%lld successors=%lld pushes=%lld updates=%lld heap_peak=%lld | "
-                     "Gcycles pop=%.3f succ_loop=%.3f stale_scans=%lld\n",
+                     "Gcycles pop=%.3f succ_loop=%.3f stale_scans=%lld spec=%d walks_ended_on_the_path=%lld/%lld root_moves=%lld\n",
                      (long long)nexp, (long long)n_succ, (long long)n_push, (long long)n_upd, (long long)open.hwm,
-                     c_pop * 1e-9, c_succ * 1e-9, (long long)open.scans);
+                     c_pop * 1e-9, c_succ * 1e-9, (long long)open.scans, (int)spec, (long long)open.spec_hits,
+                     (long long)open.spec_tries, (long long)open.root_moves);
     if (prof)
         for (int b = 0; b < 64; ++b)
             if (pop_hist[b][1])

@@ -205,6 +205,9 @@ bool astar_cluster_dense(const HostTables &T, uint64_t cluster, ClusterRun &R, c
         int i = 0;
         for (uint64_t x = cluster; x; x &= x - 1) sbit[__builtin_ctzll(x)] = 1u << i++;
     }
+    const int pfmode = std::getenv("ULG_EXACT_PF") ? std::atoi(std::getenv("ULG_EXACT_PF")) : 6;
+    const bool spec = (pfmode & 16) != 0;
+    const int spec_deep = std::getenv("ULG_EXACT_SPEC_DEEP") ? std::atoi(std::getenv("ULG_EXACT_SPEC_DEEP")) : 6;
     const uint32_t goal_slot = (uint32_t)(nslots - 1);
     const uint64_t r1 = cluster >> 1;
     recs[0] = DenseRec{0.0f, 0.0f, 0, (uint8_t)(r1 ? __builtin_ctzll(r1) + 1 : 0), {0, 0, 0}};
@@ -222,6 +225,11 @@ bool astar_cluster_dense(const HostTables &T, uint64_t cluster, ClusterRun &R, c
             const uint32_t top = open.a[0].slot();
             const uint64_t tv = g_have_bmi2 ? pdep_bmi2(top, cluster) : pdep64(top, cluster);
             for (uint64_t x = cluster & ~tv; x; x &= x - 1) __builtin_prefetch(&recs[top | sbit[__builtin_ctzll(x)]], 1);
+            if ((pfmode & 96) == 96)  // the coming decrease-keys' heap entries (search_host.cpp)
+                for (uint64_t x = cluster & ~tv; x; x &= x - 1) {
+                    const int32_t p = recs[top | sbit[__builtin_ctzll(x)]].pq;
+                    if (p > 0) __builtin_prefetch(&open.a[p - 1], 1);
+                }
         }
         const uint32_t ui = open.pop();
         ++nexp;
@@ -233,6 +241,15 @@ bool astar_cluster_dense(const HostTables &T, uint64_t cluster, ClusterRun &R, c
         const uint64_t variables = g_have_bmi2 ? pdep_bmi2(ui, cluster) : pdep64(ui, cluster);
         const uint64_t cand = cluster & ~variables;
         for (uint64_t x = cand; x; x &= x - 1) T.prefetch_bs(__builtin_ctzll(x), variables);
+        if (spec) open.spec_prefetch(spec_deep);  // the next pop's bottom levels (search_host.cpp)
+        if ((pfmode & 32) && open.len > 0) {  // the next pop's successor records and costs (search_host.cpp)
+            const uint32_t nt = open.a[0].slot();
+            const uint64_t ntv = g_have_bmi2 ? pdep_bmi2(nt, cluster) : pdep64(nt, cluster);
+            for (uint64_t x = cluster & ~ntv; x; x &= x - 1) {
+                __builtin_prefetch(&recs[nt | sbit[__builtin_ctzll(x)]], 1);
+                T.prefetch_bs(__builtin_ctzll(x), ntv);
+            }
+        }
         for (uint64_t x = cand; x; x &= x - 1) {
             const int leaf = __builtin_ctzll(x);
             const uint32_t si = ui | sbit[leaf];
