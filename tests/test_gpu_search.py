@@ -309,3 +309,25 @@ def test_exact_astar_dense_and_indexed_forms_agree(ulg_ctx, oracle_built, monkey
         assert res["net_text"] == ref["net_text"]
         out.append(res["expanded"])
     assert out[0] == out[1]
+
+
+@pytest.mark.parametrize("pf", ["0", "22", "54", "118"])
+def test_exact_astar_prefetch_modes_identical(ulg_ctx, oracle_built, monkeypatch, pf):
+    """ULG_EXACT_PF only moves prefetches (bit 4: the next pop's bottom heap
+    levels, DenseHeap::spec_prefetch; bits 5-6: the next pop's records and
+    its decrease-keys' heap entries one expansion early): the dense replay's
+    DAG, order, cost and expansion count stay the oracle's in every mode."""
+    import ulg
+    o = oracle_built
+    n, k = 18, 4
+    X, _ = synth.gaussian_sem(n, 4000, 9351)
+    rows = [(1 << n) - 1] * n
+    offs, sets, scores, costs = _oracle_pipeline(o, X, 2.0, k, ulg.candidates_from_edges(rows, n))
+    ulg_ctx.search_load(offs, sets, costs)
+    ref = o.Search(n, offs, sets, costs).astar(edges=rows)
+    monkeypatch.setenv("ULG_EXACT_PF", pf)
+    res = ulg_ctx.astar(edges=rows, mode=0)
+    assert [int(x) for x in res["vpar"]] == [int(x) for x in ref["vpar"]]
+    assert list(res["order"]) == list(ref["order"])
+    assert np.float32(res["cost"]).tobytes() == np.float32(ref["cost"]).tobytes()
+    assert res["expanded"] == ref["expanded"]

@@ -210,10 +210,12 @@ def test_triplet_look_ahead_threads_equal_sequential(ulg_ctx, oracle_built, monk
     rows = [r & ~(1 << i) for i, r in enumerate(synth.true_skeleton_edges(W, 0.15, 9413))]
     offs, sets, costs = _oracle_costs(o, X, 2.0, 3, ulg.candidates_from_edges(rows, n))
     res = {}
-    for threads in ("1", "8"):
+    for threads, pf in (("1", "6"), ("8", "6"), ("8", "118")):
+        # ULG_EXACT_PF 118: the cluster searches' prefetch modes (search_host.cpp), results unchanged
         monkeypatch.setenv("ULG_TRIPLET_THREADS", threads)
+        monkeypatch.setenv("ULG_EXACT_PF", pf)
         ulg_ctx.search_load(offs, sets, costs)
-        res[threads] = ulg_ctx.triplet(edges=rows)
+        res[threads + "/" + pf] = ulg_ctx.triplet(edges=rows)
     ref = o.triplet(o.Search(n, offs, sets, costs), edges=rows)
     for r in res.values():
         assert r["mec"].tolist() == ref["mec"].tolist()

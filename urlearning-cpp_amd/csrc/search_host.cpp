@@ -367,6 +367,15 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
                      (long long)nexp, (long long)n_succ, (long long)n_push, (long long)n_upd, (long long)open.hwm,
                      c_pop * 1e-9, c_succ * 1e-9, (long long)open.scans, (int)spec, (long long)open.spec_hits,
                      (long long)open.spec_tries, (long long)open.root_moves);
+    if (prof) {  // are the records and heap on huge pages?  (THP can be off on a box)
+        if (FILE *f = std::fopen("/proc/self/smaps_rollup", "r")) {
+            char line[256];
+            while (std::fgets(line, sizeof line, f))
+                if (std::strncmp(line, "AnonHugePages", 13) == 0 || std::strncmp(line, "Rss:", 4) == 0)
+                    std::fprintf(stderr, "exact_prof(dense) %s", line);
+            std::fclose(f);
+        }
+    }
     if (prof)
         for (int b = 0; b < 64; ++b)
             if (pop_hist[b][1])
