@@ -307,6 +307,12 @@ int ulg_sweep_shard_end(ulg_ctx *ctx, uint64_t *vpar, int *order, float *goal_co
  * cached until the tables change) when that fits the free HBM; 0 reads the
  * binary-indexed lattice per predecessor instead; 2 uses the slices with
  * 64-bit index arithmetic (1 = 32-bit).
+ * "exact_settled" (0/1, default 0): the exact-order A* (ULG_ASTAR_EXACT,
+ * dense form, no ancestors) first computes on the GPU every node's smallest
+ * reachable g (the same float sums, minimised over all predecessors) and
+ * which in-edges attain it; a node whose g reaches that value can never be
+ * improved (strict <), so later visits of it skip its record.  Same pops,
+ * DAG and expansion count (C3: 47 % of the visits skipped, but no faster).
  * "wide_prune" (0/1, default 1): the wide-layer walks skip absent nodes
  * below which no present key reaches -ts (hi-cover tables per variable);
  * "wide_reduced" (0/1, default 1): they skip the recursion's re-tests that

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--modes", nargs="+", default=["6", "22"])
     ap.add_argument("--deep", nargs="+", default=["6"], help="ULG_EXACT_SPEC_DEEP values (spec modes only)")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--settled", nargs="+", default=None, help="exact_settled values to alternate (pf modes: first only)")
     a = ap.parse_args()
     n, N, k = CFG[a.config]
     X, _ = synth.gaussian_sem(n, N, 9200)
@@ -38,6 +39,26 @@ def main():
     r0 = ctx.astar(edges=full, mode=0, net_text=False)
     print(json.dumps({"first_call_s": time.perf_counter() - t, "expanded": r0["expanded"], "cost": r0["cost"]}),
           flush=True)
+    if a.settled:
+        res = {f"settled={v}": [] for v in a.settled}
+        keys = list(res)
+        for rep in range(a.reps):
+            for v in a.settled:
+                v, _, pf = v.partition("/")  # "1/134": exact_settled 1 under ULG_EXACT_PF 134
+                os.environ["ULG_EXACT_PF"] = pf or "6"
+                ctx.set_option("exact_settled", int(v))
+                ctx.astar(edges=full, mode=0, net_text=False)  # rebuilds the rows for this setting
+                t = time.perf_counter()
+                r = ctx.astar(edges=full, mode=0, net_text=False)
+                dt = time.perf_counter() - t
+                assert r["expanded"] == r0["expanded"] and r["cost"] == r0["cost"], (v, r["expanded"], r["cost"])
+                assert [int(x) for x in r["vpar"]] == [int(x) for x in r0["vpar"]] and list(r["order"]) == list(r0["order"])
+                res[keys[a.settled.index(v + ("/" + pf if pf else ""))]].append(round(dt, 3))
+                print(json.dumps({"rep": rep, "exact_settled": v, "s": round(dt, 3),
+                                  "expansions_per_s": r["expanded"] / dt}), flush=True)
+        print(json.dumps({"config": a.config, "seconds": res}), flush=True)
+        ctx.close()
+        return
     arms = []
     for m in a.modes:
         if int(m) & 16:
