@@ -2513,7 +2513,8 @@ int host_walks(ulg_ctx *c, WideGroup &G, int L, int ph, int q, uint64_t sn, uint
         copy_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count();
         if (const char *dd = std::getenv("ULG_DUMP_HOSTWALK")) {  // diagnostics: the bitsets of the largest ones
             static std::atomic<int> nd{0};
-            if (q >= 15 && nd < 16) {
+            static const int qmin = std::getenv("ULG_DUMP_HOSTWALK_Q") ? std::atoi(std::getenv("ULG_DUMP_HOSTWALK_Q")) : 15;
+            if (q >= qmin && nd < 64) {
                 char fn[512];
                 std::snprintf(fn, sizeof fn, "%s/hostwalk_%d_L%d_p%d_q%d.bin", dd, nd++, L, ph, q);
                 if (FILE *f = std::fopen(fn, "wb")) {
