@@ -33,7 +33,11 @@ int main(int argc, char **argv) {
             dom = ulg::host_walk(L, ph, skip.data(), buf.data() + nw, &err);
             best = std::min(best, std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
         }
-        std::printf("%-40s L=%2d ph=%d q=%2d dom=%d err=%d best_us=%.1f\n", base, L, ph, q, (int)dom, (int)err, best);
+        uint64_t its = 0, nc = 0;
+        std::memcpy(skip.data(), buf.data(), nw * 8);
+        (void)ulg::host_walk(L, ph, skip.data(), buf.data() + nw, &err, &its, &nc);
+        std::printf("%-40s L=%2d ph=%d q=%2d dom=%d err=%d best_us=%.1f iters=%llu nbr=%llu ns/iter=%.1f\n", base, L, ph,
+                    q, (int)dom, (int)err, best, (unsigned long long)its, (unsigned long long)nc, best * 1e3 / (double)its);
         total += best;
     }
     std::printf("total_us %.1f\n", total);

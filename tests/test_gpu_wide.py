@@ -155,7 +155,8 @@ def test_wide_pool_identical_lists_c4(ulg_ctx):
     "wide_host": LDS replays past that many iterations finish on host threads
     (1: every replay does, so host_walk re-decides all of them; 0: none) in
     launches of at most "wide_host_max" replays, "wide_host_first": launches
-    of at most that many replays go to the host whole, "wide_host_threads":
+    of at most that many replays go to the host whole (and, with "wide_host_q",
+    launches of <= 128 replays over 2^q >= 2^wide_host_q subsets), "wide_host_threads":
     host threads per launch.  All 30 C4 variables (n=30, N=100k, MMPC,
     -p = n-1; the wide layers reach 18) give bit-identical lists in every
     combination, and the pool's repeat call too."""
@@ -168,10 +169,11 @@ def test_wide_pool_identical_lists_c4(ulg_ctx):
     vs = list(range(n))
     out = []
     defaults = dict(wide_pool=2, score_streams=3, wide_host=1024, wide_host_max=4096, wide_host_first=0,
-                    wide_host_threads=16)
+                    wide_host_threads=16, wide_host_q=0)
     combos = [dict(wide_pool=0, wide_host=0), dict(), dict(), dict(wide_pool=1, wide_host=4096),
               dict(wide_pool=1, score_streams=2), dict(wide_pool=1, wide_host=1, wide_host_max=1 << 40),
-              dict(wide_pool=0, score_streams=1, wide_host=64), dict(wide_host_first=64, wide_host_threads=3)]
+              dict(wide_pool=0, score_streams=1, wide_host=64), dict(wide_host_first=64, wide_host_threads=3),
+              dict(wide_host_q=14)]
     try:
         for combo in combos:
             for name, val in dict(defaults, **combo).items():

@@ -2747,7 +2747,12 @@ int score_wide_groups(ulg_ctx *c, int L, int ph, std::vector<WideGroup> &gs, int
         const uint64_t hbud = sn > c->wide_host_max ? 0
                               : sn <= kHostFewReplays ? std::min<uint64_t>(c->wide_host_iters, kHostFewBudget)
                                                       : c->wide_host_iters;
-        if (hbud && sn <= c->wide_host_first) {
+        // ... and so do launches of few replays over 2^q >= 2^wide_host_q
+        // local subsets: at the top layers of the largest candidate sets
+        // nearly every replay outlives the LDS budget anyway (C4 v = 23:
+        // L >= 15 hands over 13 of 14, 13 of 15, 1 of 1), so its LDS phase is
+        // pure latency
+        if (hbud && (sn <= c->wide_host_first || (c->wide_host_q > 0 && q >= c->wide_host_q && sn <= 128))) {
             // so few replays that the host takes them all at once: no GPU
             // replay phase (its length is its longest walk's), straight to
             // the fills, the copy and the host threads

@@ -15,18 +15,31 @@ constexpr uint64_t kStragIterCap = 1ull << 32;  // iterations before a replay fa
 // bitsets (strag_fill's): the same tests in the same order, with the wave's
 // neighbour ballots as loops over the q local bits.  Returns dominated (the
 // walk reached a present key >= -ts); err on the kernel's error conditions.
-inline bool host_walk(int L, int phase, uint64_t *skip, const uint64_t *hib, bool *err) {
+inline bool host_walk(int L, int phase, uint64_t *skip, const uint64_t *hib, bool *err, uint64_t *iters = nullptr,
+                      uint64_t *nbr_calls = nullptr) {
     const int q = phase == 0 ? L : L + 1;
-    auto get = [](const uint64_t *b, uint32_t t) { return (uint32_t)((b[t >> 6] >> (t & 63)) & 1ull); };
     // bit l of sm / hm: skip / hi bit of N ^ {l} (the wave's ballot; bits
     // from q up read as skipped)
     const uint32_t above = q >= 32 ? 0u : ~0u << q;
+    uint64_t ncalls = 0;
+    // N ^ {l} for l < 6 stays in N's word (bit b ^ 2^l); for l >= 6 it is
+    // bit b of the word w ^ 2^(l-6): one word read per neighbour, and six
+    // neighbours from one read
+    const int ql = q < 6 ? q : 6;
     auto nbr = [&](uint32_t Nn, uint32_t &sm_, uint32_t &hm_) {
+        ++ncalls;
+        const uint32_t w = Nn >> 6, b = Nn & 63u;
+        const uint64_t ws = skip[w], wh = hib[w];
         uint32_t s_ = above, h_ = 0;
-        for (int l = 0; l < q; ++l) {
-            const uint32_t t = Nn ^ (1u << l);
-            s_ |= get(skip, t) << l;
-            h_ |= get(hib, t) << l;
+        for (int l = 0; l < ql; ++l) {
+            const uint32_t bt = b ^ (1u << l);
+            s_ |= (uint32_t)((ws >> bt) & 1ull) << l;
+            h_ |= (uint32_t)((wh >> bt) & 1ull) << l;
+        }
+        for (int l = 6; l < q; ++l) {
+            const uint32_t wt = w ^ (1u << (l - 6));
+            s_ |= (uint32_t)((skip[wt] >> b) & 1ull) << l;
+            h_ |= (uint32_t)((hib[wt] >> b) & 1ull) << l;
         }
         sm_ = s_;
         hm_ = h_;
@@ -161,6 +174,8 @@ inline bool host_walk(int L, int phase, uint64_t *skip, const uint64_t *hib, boo
         mS = mc;
         nbr(N, sm, hm);
     }
+    if (iters) *iters = it;
+    if (nbr_calls) *nbr_calls = ncalls;
     return dom;
 }
 

@@ -244,6 +244,11 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         c->wide_host_first = (uint64_t)value;
         return ULG_OK;
     }
+    if (std::strcmp(name, "wide_host_q") == 0) {
+        if (value < 0 || value > 32) return set_err(c, ULG_ERR_ARG, "wide_host_q must be 0..32");
+        c->wide_host_q = (int)value;
+        return ULG_OK;
+    }
     if (std::strcmp(name, "wide_host_threads") == 0) {
         if (value < 1 || value > 64) return set_err(c, ULG_ERR_ARG, "wide_host_threads must be 1..64");
         c->wide_host_threads = (int)value;

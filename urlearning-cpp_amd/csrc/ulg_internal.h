@@ -88,6 +88,7 @@ struct ulg_ctx {
     int wide_host_threads = 16;          // host threads per wide-layer launch for those replays
     uint64_t wide_host_max = 4096;       // ... in launches of at most this many LDS replays
     uint64_t wide_host_first = 0;        // launches of at most this many replays go to the host whole
+    int wide_host_q = 0;                 // ... as do launches of <= 128 replays with q >= this (0: off)
     int score_xcd = 1;             // scoring kernels: contiguous runs of sets per XCD
     int score_graph = 1;           // scoring call: replay the captured launch sequence
     hipGraph_t graph = nullptr;    // the captured scoring launches, its instance, its key
