@@ -364,6 +364,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo + --device: rehearse the N>1 code path with several ranks on one GPU")
     ap.add_argument("--device", type=int, default=None, help="GPU for every rank (default LOCAL_RANK)")
+    ap.add_argument("--slots", type=int, default=1,
+                    help="scoring steps in flight per rank: contexts whose calls are queued with "
+                         "ulg_cbic_score_async and collected slots - 1 steps later (every step complete)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
@@ -423,8 +426,49 @@ def main():
             ex.allgather()  # the one collective of the data path
         return scored
 
-    for _ in range(args.warmup):
-        step()
+    # --slots S > 1: S contexts on this GPU (same data), step i on context
+    # i % S; its scoring call is queued without waiting and collected (then
+    # its lists exchanged) S - 1 steps later, so the latency-bound parts of
+    # one step's launch chain overlap the next steps' work.  Collectives stay
+    # in step order on one thread.
+    slots = max(1, args.slots)
+    sctx, sex = [ctx], [ex]
+    for _ in range(slots - 1):
+        c2 = ulg.Context(local)
+        for kv in args.option:
+            k_, v_ = kv.split("=", 1)
+            c2.set_option(k_, int(v_))
+        if args.score_variant is not None:
+            c2.set_option("score_variant", args.score_variant)
+        c2.load(X, lam)
+        sctx.append(c2)
+        sex.append(shard.ListExchange(n, parts, cands_all, k, rank, device="cuda", comm_device=cdev)
+                   if ex is not None else None)
+
+    def run_steps(nsteps):
+        """nsteps complete steps; returns the sets scored and the steps run on context 0."""
+        if slots == 1:
+            return sum(step() for _ in range(nsteps)), nsteps
+        total, pend, on0 = 0, [], 0
+
+        def complete(s):
+            stored, scored = sctx[s].score_finish()
+            if sex[s] is not None:
+                sex[s].fill(sctx[s], stored)
+                sex[s].allgather()
+            return scored
+        for i in range(nsteps):
+            s = i % slots
+            on0 += s == 0
+            sctx[s].score_async(variables, cands, k)
+            pend.append(s)
+            if len(pend) == slots:
+                total += complete(pend.pop(0))
+        while pend:
+            total += complete(pend.pop(0))
+        return total, on0
+
+    run_steps(max(args.warmup, slots))
     # HIP events in the timed region only around the roofline unit's kernels
     # (two host-side event records per timed kernel would otherwise show up in
     # a ~1.5 ms step of ~35 launches); the full per-kernel breakdown comes from
@@ -437,9 +481,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    scored_total = 0
-    for _ in range(args.steps):
-        scored_total += step()
+    scored_total, steps_ctx0 = run_steps(args.steps)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -458,7 +500,17 @@ def main():
 
     # sets in one launch of the dominant kernel (layer k, sets without variable 0)
     per_launch = sum(math.comb(msz[v] - (1 if (v != 0 and cands_all[v] & 1) else 0), kk) for v in variables)
-    roof, _ = roofline(ctx, dict(cfg, k=kk), per_launch, args.steps)
+    if ex is not None and slots > 1:
+        # every slot's last exchange holds the whole job's lists: all equal
+        ds = set()
+        for e in sex:
+            o_, st_, sc_ = e.assemble()
+            ds.add(lists_digest(o_, st_.cpu().numpy(), sc_.cpu().numpy()))
+        if len(ds) != 1:
+            raise RuntimeError(f"bench.py: the {slots} slots exchanged different lists")
+    roof, _ = roofline(ctx, dict(cfg, k=kk), per_launch, steps_ctx0)
+    if roof is not None and slots > 1:
+        roof["note"] += f"; {slots} steps in flight (contexts), events on context 0's launches only"
     ctx.profile(True)
     ctx.profile_select(None)
     ctx.profile_reset()
@@ -522,6 +574,7 @@ def main():
                                       f"{n} variables balanced over {ws} GPU(s), one all-gather of the lists"),
                        "config_id": args.config, "mode": args.mode,
                        "parallelism": f"variable shard x{ws}" if args.mode == "shard" else f"replicas x{ws}",
+                       "steps_in_flight": slots,
                        "parent_sets_per_step_per_rank": units_rank},
             "roofline": roof,
             "kernel_ms_one_step": {kk2: round(vv["total_ms"], 4) for kk2, vv in kernels.items()},
@@ -533,6 +586,8 @@ def main():
         if ws == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(cfg, X)
         print(json.dumps(res), flush=True)
+    for c2 in sctx[1:]:
+        c2.close()
     ctx.close()
     if dist:
         dist.destroy_process_group()

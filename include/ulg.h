@@ -98,6 +98,16 @@ int ulg_mmpc(ulg_ctx *ctx, double alpha, int max_cond, uint64_t *rows);
 int ulg_cbic_score(ulg_ctx *ctx, const int *vars, int nv,
                    const uint64_t *candidates, int max_parents,
                    int64_t *total_stored, int64_t *total_scored);
+/* The same call split in two, so one host thread can keep several contexts'
+ * scoring in flight (e.g. two steps of a throughput loop on one GPU):
+ * ulg_cbic_score_async queues the whole call and returns without waiting
+ * (when every layer is unrolled and no time limit is set; otherwise it runs
+ * synchronously), ulg_cbic_score_finish waits for it and returns the counts
+ * ulg_cbic_score would have.  Any later scorer call on the context
+ * (ulg_cbic_score*, ulg_cbic_fetch) finishes a pending one first. */
+int ulg_cbic_score_async(ulg_ctx *ctx, const int *vars, int nv,
+                         const uint64_t *candidates, int max_parents);
+int ulg_cbic_score_finish(ulg_ctx *ctx, int64_t *total_stored, int64_t *total_scored);
 /* Copy the stored sets out.  offsets[nv+1]; variable vars[i] owns
  * [offsets[i], offsets[i+1]); within a variable, sets are ordered by
  * (|set|, set value) -- the reference's Gosper insertion order.

@@ -2940,9 +2940,40 @@ int ulg_cbic_gram(ulg_ctx *c, double *out) {
     return ULG_OK;
 }
 
+static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidates, int max_parents,
+                      int64_t *total_stored, int64_t *total_scored, bool async);
+
+int ulg_cbic_score_finish(ulg_ctx *c, int64_t *total_stored, int64_t *total_scored) {
+    if (!c) return ULG_ERR_ARG;
+    if (c->async_pending) {
+        c->async_pending = false;
+        ULG_HIP(c, hipSetDevice(c->device));
+        ULG_HIP(c, hipStreamSynchronize(c->stream));
+        prof_collect(c);
+        c->total_stored = (int64_t)*c->async_pinned;
+    }
+    if (!c->scored) return set_err(c, ULG_ERR_STATE, "ulg_cbic_score_finish: nothing scored");
+    if (total_stored) *total_stored = c->total_stored;
+    if (total_scored) *total_scored = c->total_scored;
+    return ULG_OK;
+}
+
 int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidates, int max_parents,
                    int64_t *total_stored, int64_t *total_scored) {
+    return cbic_score(c, vars, nv, candidates, max_parents, total_stored, total_scored, false);
+}
+
+int ulg_cbic_score_async(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidates, int max_parents) {
+    return cbic_score(c, vars, nv, candidates, max_parents, nullptr, nullptr, true);
+}
+
+static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidates, int max_parents,
+                      int64_t *total_stored, int64_t *total_scored, bool async) {
     if (!c) return ULG_ERR_ARG;
+    if (c->async_pending) {  // the previous async call's launches still own the buffers
+        int rc0 = ulg_cbic_score_finish(c, nullptr, nullptr);
+        if (rc0) return rc0;
+    }
     if (!c->loaded) return set_err(c, ULG_ERR_STATE, "ulg_cbic_score: call ulg_cbic_load first");
     if (!vars || !candidates || nv < 1 || nv > c->n) return set_err(c, ULG_ERR_ARG, "ulg_cbic_score: bad variable list");
     ULG_HIP(c, hipSetDevice(c->device));
@@ -3447,6 +3478,24 @@ int ulg_cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidat
     }
     }
 launched:
+    if (async && kmax <= kMaxL) {
+        // no host sync on this path: the stored count is copied into pinned
+        // memory behind the launches and collected by ulg_cbic_score_finish
+        if (!c->async_pinned)
+            ULG_HIP(c, hipHostMalloc((void **)&c->async_pinned, sizeof(unsigned long long), hipHostMallocDefault));
+        ULG_HIP(c, hipMemcpyAsync(c->async_pinned, c->d_blk.p + nb, 8, hipMemcpyDeviceToHost, c->stream));
+        c->nv = nv;
+        c->kmax = kmax;
+        c->vars.assign(vars, vars + nv);
+        c->m = mv;
+        c->tbl_off = toff;
+        c->total_slots = (int64_t)total_slots;
+        c->total_stored = 0;
+        c->total_scored = scored;
+        c->scored = true;
+        c->async_pending = true;
+        return ULG_OK;
+    }
     uint64_t stored = 0;
     unsigned long long wide_err = 0;
     ULG_HIP(c, hipMemcpyAsync(&stored, c->d_blk.p + nb, 8, hipMemcpyDeviceToHost, c->stream));
@@ -3474,6 +3523,10 @@ launched:
 
 int ulg_cbic_fetch(ulg_ctx *c, uint64_t *sets, float *scores, int64_t *offsets, int device_ptrs) {
     if (!c) return ULG_ERR_ARG;
+    if (c->async_pending) {
+        int rc0 = ulg_cbic_score_finish(c, nullptr, nullptr);
+        if (rc0) return rc0;
+    }
     if (!c->scored) return set_err(c, ULG_ERR_STATE, "ulg_cbic_fetch: nothing scored");
     ULG_HIP(c, hipSetDevice(c->device));
     const hipMemcpyKind k = device_ptrs ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;

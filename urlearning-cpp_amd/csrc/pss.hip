@@ -296,6 +296,10 @@ extern "C" {
 int ulg_pss_format(ulg_ctx *c, const char *header, const char *const *names, const int *arity, const char **text,
                    int64_t *len) {
     if (!c || !header || !names || !arity || !text || !len) return ULG_ERR_ARG;
+    if (c->async_pending) {  // an async scoring call still owns the lists
+        const int rc0 = ulg_cbic_score_finish(c, nullptr, nullptr);
+        if (rc0) return rc0;
+    }
     if (!c->scored) return set_err(c, ULG_ERR_STATE, "ulg_pss_format: call ulg_cbic_score first");
     if (c->nv != c->n) return set_err(c, ULG_ERR_STATE, "ulg_pss_format: every variable must be scored in this context");
     ULG_HIP(c, hipSetDevice(c->device));

@@ -534,6 +534,10 @@ int ulg_search_load(ulg_ctx *c, int n, const int64_t *offsets, const uint64_t *s
 
 int ulg_search_from_scores(ulg_ctx *c) {
     if (!c) return ULG_ERR_ARG;
+    if (c->async_pending) {  // an async scoring call still owns the lists
+        const int rc0 = ulg_cbic_score_finish(c, nullptr, nullptr);
+        if (rc0) return rc0;
+    }
     if (!c->scored) return set_err(c, ULG_ERR_STATE, "ulg_search_from_scores: call ulg_cbic_score first");
     if (c->nv != c->n) return set_err(c, ULG_ERR_STATE, "ulg_search_from_scores: every variable must be scored in this context");
     ULG_HIP(c, hipSetDevice(c->device));

@@ -154,6 +154,8 @@ void ulg_destroy(ulg_ctx *c) {
     graph_reset(c);
     if (c->wide_pinned) (void)hipHostFree(c->wide_pinned);
     c->wide_pinned = nullptr;
+    if (c->async_pinned) (void)hipHostFree(c->async_pinned);
+    c->async_pinned = nullptr;
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
     c->event_pool.clear();
     for (hipStream_t s : c->aux_streams) (void)hipStreamDestroy(s);

@@ -139,6 +139,10 @@ struct ulg_ctx {
     ulg::DevBuf<int> d_hmeta;       // per stream group: launch variables and tile / block prefixes
     ulg::DevBuf<unsigned long long> d_scount;  // per stream group: long wide walks handed to the LDS kernel
     unsigned long long *wide_pinned = nullptr;  // pinned queue / long-walk counts of the wide stages
+    // ulg_cbic_score_async: the stored count lands here when the launches
+    // finish; ulg_cbic_score_finish (or any later scorer call) collects it
+    unsigned long long *async_pinned = nullptr;
+    bool async_pending = false;
     std::vector<unsigned long long> wide_host;
     std::map<std::string, std::vector<double>> prof_ms;
 };

@@ -39,6 +39,8 @@ def lib():
         L.ulg_cbic_load.argtypes = [P, P, I64, I, D]
         L.ulg_cbic_gram.argtypes = [P, P]
         L.ulg_cbic_score.argtypes = [P, P, I, P, I, C.POINTER(I64), C.POINTER(I64)]
+        L.ulg_cbic_score_async.argtypes = [P, P, I, P, I]
+        L.ulg_cbic_score_finish.argtypes = [P, C.POINTER(I64), C.POINTER(I64)]
         L.ulg_cbic_fetch.argtypes = [P, P, P, P, I]
         L.ulg_cbic_score_vars.argtypes = [P, P, I, P, I, P, P, P, I64]
         L.ulg_cbic_score_sets.argtypes = [P, I64, P, P, P]
@@ -142,6 +144,20 @@ class Context:
         self._check(lib().ulg_cbic_score(self._h, _ptr(v), len(v), _ptr(c), int(max_parents),
                                          C.byref(st), C.byref(sc)), "ulg_cbic_score")
         self._nv = len(v)
+        return st.value, sc.value
+
+    def score_async(self, variables, candidates, max_parents: int):
+        """ulg_cbic_score_async: queues the scoring call; score_finish() waits for it."""
+        v = np.ascontiguousarray(variables, dtype=np.int32)
+        c = np.ascontiguousarray(candidates, dtype=np.uint64)
+        self._check(lib().ulg_cbic_score_async(self._h, _ptr(v), len(v), _ptr(c), int(max_parents)),
+                    "ulg_cbic_score_async")
+        self._nv = len(v)
+
+    def score_finish(self):
+        """-> (total_stored, total_scored) of the last (async) scoring call."""
+        st, sc = C.c_int64(), C.c_int64()
+        self._check(lib().ulg_cbic_score_finish(self._h, C.byref(st), C.byref(sc)), "ulg_cbic_score_finish")
         return st.value, sc.value
 
     def fetch(self, total_stored: int):
