@@ -364,10 +364,18 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo + --device: rehearse the N>1 code path with several ranks on one GPU")
     ap.add_argument("--device", type=int, default=None, help="GPU for every rank (default LOCAL_RANK)")
-    ap.add_argument("--slots", type=int, default=1,
+    ap.add_argument("--slots", type=int, default=3,
                     help="scoring steps in flight per rank: contexts whose calls are queued with "
-                         "ulg_cbic_score_async and collected slots - 1 steps later (every step complete)")
+                         "ulg_cbic_score_async and collected slots - 1 steps later (every step complete); "
+                         "with more than one, each context scores on one stream (score_streams 1) unless "
+                         "--option score_streams=... says otherwise")
     args = ap.parse_args()
+    if args.slots > 1 and not any(o.startswith("score_streams=") for o in args.option):
+        # independent steps in flight replace the stream groups as the source of
+        # concurrency: one chain per context, S chains at once (C3: 1.18 ms per
+        # step with 1 slot x 3 groups, 0.67 ms with 3 slots x 1 stream;
+        # profiles/r3/slots/)
+        args.option.append("score_streams=1")
 
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
         sys.exit(spawn_ranks(args.gpus))
@@ -511,6 +519,15 @@ def main():
     roof, _ = roofline(ctx, dict(cfg, k=kk), per_launch, steps_ctx0)
     if roof is not None and slots > 1:
         roof["note"] += f"; {slots} steps in flight (contexts), events on context 0's launches only"
+    if roof is not None:
+        # the same compulsory bytes (4 (L + 1) per set) over the whole step:
+        # every layer of every variable of this rank, per ms_per_step
+        step_bytes = sum(math.comb(msz[v], L) * 4 * (L + 1) for v in variables for L in range(0, k + 1))
+        roof["step_level"] = {"algorithmic_bytes_per_step": step_bytes,
+                              "achieved_gbs": step_bytes / (elapsed / args.steps) / 1e9,
+                              "frac": step_bytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS,
+                              "note": "all of this rank's sets per timed step (the per-launch figure above is "
+                                      "the dominant kernel's; concurrent steps stretch each launch)"}
     ctx.profile(True)
     ctx.profile_select(None)
     ctx.profile_reset()

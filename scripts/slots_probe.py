@@ -54,6 +54,7 @@ def main():
     ap.add_argument("--slots", type=int, nargs="+", default=[2, 3])
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--options", default="", help="ulg_set_option name=value,... on every context")
     a = ap.parse_args()
     n, N, k = 25, 10000, 6
     X, _ = synth.gaussian_sem(n, N, 9200)
@@ -61,6 +62,9 @@ def main():
     ctxs = []
     for _ in range(max(a.slots)):
         c = ulg.Context(0)
+        for kv in filter(None, a.options.split(",")):
+            x, y = kv.split("=")
+            c.set_option(x, int(y))
         c.load(X, 2.0)
         ctxs.append(c)
     shares = [("whole", list(range(n)))]
