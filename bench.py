@@ -364,12 +364,15 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo + --device: rehearse the N>1 code path with several ranks on one GPU")
     ap.add_argument("--device", type=int, default=None, help="GPU for every rank (default LOCAL_RANK)")
-    ap.add_argument("--slots", type=int, default=3,
+    ap.add_argument("--slots", type=int, default=None,
                     help="scoring steps in flight per rank: contexts whose calls are queued with "
                          "ulg_cbic_score_async and collected slots - 1 steps later (every step complete); "
                          "with more than one, each context scores on one stream (score_streams 1) unless "
-                         "--option score_streams=... says otherwise")
+                         "--option score_streams=... says otherwise (default 3 when every layer is unrolled, "
+                         "k <= 8; 1 for the wide layers of C1/C4, whose calls synchronise anyway)")
     args = ap.parse_args()
+    if args.slots is None:
+        args.slots = 3 if CONFIGS[args.config]["k"] <= 8 else 1
     if args.slots > 1 and not any(o.startswith("score_streams=") for o in args.option):
         # independent steps in flight replace the stream groups as the source of
         # concurrency: one chain per context, S chains at once (C3: 1.18 ms per
