@@ -266,6 +266,7 @@ def exact_astar_legs(ctx, cfg, skel, lists, oracle_budget_s=15.0):
     out["exact"] = {"config": f"{cfg['id'].upper()} (n={n}, N={cfg['N']}, k={cfg['k']}), "
                               + ("full skeleton" if skel == [(1 << n) - 1] * n else "skeleton"),
                     "expansions": e["expanded"], "ms": 1e3 * dt, "expansions_per_s": e["expanded"] / dt,
+                    "ns_per_expansion": 1e9 * dt / max(e["expanded"], 1),
                     "goal_cost": e["cost"],
                     "same_netfile_cost_expansions_as_oracle_fixture": same,
                     "oracle_fixture": os.path.relpath(fx, ROOT) if os.path.exists(fx) else None,
@@ -298,6 +299,58 @@ def exact_astar_legs(ctx, cfg, skel, lists, oracle_budget_s=15.0):
         "full_run": full_run,
         "expansions_reached_fraction_of_exact": r["expanded"] / max(e["expanded"], 1)}
     return out
+
+
+def c4_leg(device, budget_s=1.0):
+    """BASELINE config C4 beside the headline (rank 0, N = 1): n=30, N=100k,
+    the MMPC skeleton built on the GPU from the same data (alpha 0.01), 2-hop
+    candidate sets (score_main.cpp:146-153) and the reference's default
+    parent limit -p = n - 1 (score_main.cpp:296-298), so layers 9..18 run the
+    wide kernels.  One step = one complete synchronised scoring call over all
+    30 variables (every call decides every parent set; the wide layers sync
+    for their queue lengths, so steps are not overlapped); steps are repeated
+    for about budget_s after two warm-up calls.  The three variables of
+    tests/golden/c45_oracle.json (the oracle's lists, up to 52 min each) are
+    checked by count and SHA-256 after the timed calls."""
+    cfg = dict(CONFIGS["c4"], id="c4")
+    n, N, k = cfg["n"], cfg["N"], cfg["k"]
+    X, _ = synth.gaussian_sem(n, N, 9200)
+    ctx = ulg.Context(device)
+    try:
+        t0 = time.perf_counter()
+        ctx.load(X, cfg["lam"])
+        rows = ctx.mmpc(cfg["alpha"])
+        prep_ms = 1e3 * (time.perf_counter() - t0)
+        cands = ulg.candidates_from_edges(rows, n)
+        variables = list(range(n))
+        for _ in range(2):
+            ctx.score(variables, cands, k)
+        ts = []
+        scored = stored = 0
+        tb = time.perf_counter()
+        while not ts or (time.perf_counter() - tb < budget_s and len(ts) < 200):
+            a = time.perf_counter()
+            stored, scored = ctx.score(variables, cands, k)
+            ts.append(time.perf_counter() - a)
+        offs, sets, _ = ctx.fetch(stored)
+        chk = lists_vs_fixture(cfg, variables, offs, sets)
+        if chk is not None and chk[1]:
+            raise RuntimeError(f"bench.py: C4 lists differ from tests/golden/c45_oracle.json for variables {chk[1]}")
+        msz = [bin(c & ~(1 << v)).count("1") for v, c in enumerate(cands)]
+        return {"workload": "C4 cBIC scoring: n=30, N=100000, MMPC skeleton (ulg_mmpc alpha 0.01, "
+                            f"{sum(bin(r).count('1') for r in rows) // 2} edges), 2-hop candidate sets "
+                            f"(largest {max(msz)}), -p 29 (the reference's default n - 1), all 30 variables",
+                "steps": len(ts), "ms_per_step": 1e3 * float(np.mean(ts)),
+                "ms_per_step_median": 1e3 * float(np.median(ts)), "ms_per_step_min": 1e3 * float(np.min(ts)),
+                "value": scored / float(np.mean(ts)), "unit": "parent-set scores/s",
+                "parent_sets_per_step": scored, "stored_per_step": stored,
+                "load_and_mmpc_ms": prep_ms,
+                "lists_equal_oracle": (chk is not None and not chk[1]),
+                "oracle_variables_checked": chk[0] if chk else [],
+                "note": "synchronised calls timed on the host clock (data resident in HBM); the oracle check "
+                        "covers the fixture's variables (counts + SHA-256 of the sorted masks)"}
+    finally:
+        ctx.close()
 
 
 def cpu_quota():
@@ -350,6 +403,35 @@ def lists_digest(offsets, sets, scores):
     return h.hexdigest()
 
 
+def lists_vs_fixture(cfg, variables, offs, sets):
+    """Compare one context's stored lists with the oracle command lines'
+    per-variable counts and SHA-256 digests of the sorted masks
+    (tests/golden/<config>_oracle.json for C2/C3; c45_oracle.json's sampled
+    variables for C4).  Returns (checked variables, mismatching variables),
+    or None when no fixture covers this config."""
+    fx = os.path.join(GOLDEN, f"{cfg['id']}_oracle.json")
+    per = {}
+    if os.path.exists(fx):
+        ref = json.load(open(fx))
+        for v in range(cfg["n"]):
+            per[v] = (ref["stored_per_variable"][v], ref["sets_sha256_per_variable"][v])
+    elif cfg["id"] == "c4" and os.path.exists(os.path.join(GOLDEN, "c45_oracle.json")):
+        ref = json.load(open(os.path.join(GOLDEN, "c45_oracle.json")))["c4"]
+        for vs, r in ref["per_variable"].items():
+            per[int(vs)] = (r["stored"], r["sets_sha256"])
+    else:
+        return None
+    checked, bad = [], []
+    for i, v in enumerate(variables):
+        if v not in per:
+            continue
+        s = np.sort(np.asarray(sets[offs[i]:offs[i + 1]]).astype(np.uint64))
+        checked.append(v)
+        if len(s) != per[v][0] or hashlib.sha256(s.tobytes()).hexdigest() != per[v][1]:
+            bad.append(v)
+    return checked, bad
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None, help="GPUs (ranks); default 1, or WORLD_SIZE under a launcher")
@@ -359,6 +441,7 @@ def main():
     ap.add_argument("--mode", default="shard", choices=["shard", "weak"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-search", action="store_true")
+    ap.add_argument("--no-c4", action="store_true", help="skip the extra C4 object (N=1 only)")
     ap.add_argument("--score-variant", type=int, default=None, help="A/B knob (ulg_set_option score_variant)")
     ap.add_argument("--option", action="append", default=[], help="A/B knob name=value (ulg_set_option)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -519,9 +602,62 @@ def main():
             ds.add(lists_digest(o_, st_.cpu().numpy(), sc_.cpu().numpy()))
         if len(ds) != 1:
             raise RuntimeError(f"bench.py: the {slots} slots exchanged different lists")
-    roof, _ = roofline(ctx, dict(cfg, k=kk), per_launch, steps_ctx0)
-    if roof is not None and slots > 1:
-        roof["note"] += f"; {slots} steps in flight (contexts), events on context 0's launches only"
+    # The lists the timed steps left on EVERY slot context (the last step each
+    # context ran, graph replay included) against the oracle command lines'
+    # per-variable digests; a mismatch fails the bench.
+    slot_check = None
+    if ex is None:
+        checked_all, bad_all = set(), {}
+        for si, c in enumerate(sctx):
+            st_, _ = c.score_finish()
+            o_, s_, _ = c.fetch(st_)
+            r = lists_vs_fixture(cfg, variables, o_, s_)
+            if r is None:
+                break
+            checked_all.update(r[0])
+            if r[1]:
+                bad_all[si] = r[1]
+        else:
+            if bad_all:
+                raise RuntimeError(f"bench.py: slot contexts' lists differ from the oracle fixture: {bad_all}")
+            slot_check = {"slots_lists_equal_oracle": True, "contexts": slots,
+                          "variables_checked": len(checked_all),
+                          "fixture": f"tests/golden/{cfg['id']}_oracle.json"}
+    # Non-overlapped measurement (after the timed region): context 0 alone,
+    # one call at a time on one stream, HIP events on the roofline kernels'
+    # launch stream -- their durations are not stretched by concurrent steps,
+    # so the dominant kernel's time per call is below the call's own time.
+    ctx.set_option("score_streams", 1)
+    ctx.profile(True)
+    ctx.profile_select([f"score_layer_{kk}_rest", f"walk_{kk}_rest"])
+    ctx.profile_reset()
+    solo_calls = 5
+    ts_solo = []
+    for _ in range(solo_calls):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        ctx.score(variables, cands, k)
+        ts_solo.append(time.perf_counter() - a)
+    roof, _ = roofline(ctx, dict(cfg, k=kk), per_launch, solo_calls)
+    ctx.profile(False)
+    if roof is not None:
+        roof["note"] = ("one call at a time on one stream (context 0 after the timed region, %d calls): the "
+                        "dominant pair's launches do not overlap other work" % solo_calls)
+        roof["solo_call_ms"] = 1e3 * float(np.median(ts_solo))
+    # single_call_ms: what one drop-in call (bin/score, ulg_cbic_score) takes
+    # with the library's default options on a fresh context, synchronised
+    single = ulg.Context(local)
+    single.load(X, lam)
+    for _ in range(2):
+        single.score(variables, cands, k)
+    ts_single = []
+    for _ in range(10):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        single.score(variables, cands, k)
+        ts_single.append(time.perf_counter() - a)
+    single.close()
+    single_call_ms = 1e3 * float(np.median(ts_single))
     if roof is not None:
         # the same compulsory bytes (4 (L + 1) per set) over the whole step:
         # every layer of every variable of this rank, per ms_per_step
@@ -599,12 +735,19 @@ def main():
             "roofline": roof,
             "kernel_ms_one_step": {kk2: round(vv["total_ms"], 4) for kk2, vv in kernels.items()},
         }
+        res["single_call_ms"] = single_call_ms
+        res["single_call_note"] = ("one synchronised ulg_cbic_score call at a time with the library's default "
+                                   "options (what bin/score makes), median of 10 on a fresh context")
+        if slot_check is not None:
+            res["slot_check"] = slot_check
         if split is not None:
             res["shard_step"] = split
         if search is not None:
             res["astar"] = search
         if ws == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(cfg, X)
+        if ws == 1 and args.config != "c4" and not args.no_c4:
+            res["c4"] = c4_leg(local)
         print(json.dumps(res), flush=True)
     for c2 in sctx[1:]:
         c2.close()

@@ -210,12 +210,10 @@ def test_triplet_look_ahead_threads_equal_sequential(ulg_ctx, oracle_built, monk
     rows = [r & ~(1 << i) for i, r in enumerate(synth.true_skeleton_edges(W, 0.15, 9413))]
     offs, sets, costs = _oracle_costs(o, X, 2.0, 3, ulg.candidates_from_edges(rows, n))
     res = {}
-    for threads, pf in (("1", "6"), ("8", "6"), ("8", "118")):
-        # ULG_EXACT_PF 118: the cluster searches' prefetch modes (search_host.cpp), results unchanged
+    for threads in ("1", "8"):
         monkeypatch.setenv("ULG_TRIPLET_THREADS", threads)
-        monkeypatch.setenv("ULG_EXACT_PF", pf)
         ulg_ctx.search_load(offs, sets, costs)
-        res[threads + "/" + pf] = ulg_ctx.triplet(edges=rows)
+        res[threads] = ulg_ctx.triplet(edges=rows)
     ref = o.triplet(o.Search(n, offs, sets, costs), edges=rows)
     for r in res.values():
         assert r["mec"].tolist() == ref["mec"].tolist()
@@ -249,5 +247,37 @@ def test_triplet_running_time_budget(ulg_ctx):
         assert ulg_ctx.info("out_of_time") == 1
         assert cut["distinct"] == 0 and cut["runs"] == ref["runs"]
         assert not cut["mec"].any()
+    finally:
+        ulg_ctx.set_option("time_limit_ms", 0)
+
+
+def test_triplet_budget_interrupts_a_running_search(ulg_ctx):
+    """-r bounds the wall clock: the reference's A* loop stops inside the
+    search once outOfTime is set (triplet_astar.cpp:355), so a budget shorter
+    than one cluster's search ends the call early instead of after that
+    search.  Full skeleton, n=22: one 22-variable cluster (2^22 lattice
+    nodes); with a 200 ms budget the call returns well before the uncut
+    search would finish, with the empty MEC."""
+    import time
+    n = 22
+    X, _ = synth.gaussian_sem(n, 2000, 9417)
+    full = [(1 << n) - 1] * n
+    ulg_ctx.load(X, 2.0)
+    ulg_ctx.score(list(range(n)), full, 3)
+    ulg_ctx.search_from_scores()
+    t0 = time.perf_counter()
+    ref = ulg_ctx.triplet(edges=full)
+    uncut = time.perf_counter() - t0
+    assert ulg_ctx.info("out_of_time") == 0 and ref["distinct"] == 1
+    try:
+        ulg_ctx.search_from_scores()  # an empty memo: the cluster is searched again
+        ulg_ctx.set_option("time_limit_ms", 200)
+        t0 = time.perf_counter()
+        cut = ulg_ctx.triplet(edges=full)
+        dt = time.perf_counter() - t0
+        assert ulg_ctx.info("out_of_time") == 1
+        assert cut["distinct"] == 0 and not cut["mec"].any()
+        assert uncut > 1.0, uncut  # the search itself outlasts the budget by far
+        assert dt < 0.5 * uncut and dt < 1.0, (dt, uncut)
     finally:
         ulg_ctx.set_option("time_limit_ms", 0)

@@ -231,7 +231,6 @@ struct DenseHeap {
         }
         a[hole] = value;
         setpos(value, hole);
-        if (spec_track) root_moves += hole == 0;
     }
     void push(uint32_t x) {
         const DEnt e = ent(x);
@@ -278,12 +277,6 @@ struct DenseHeap {
             mv_pos[nm++] = hole;
             hole = second - 1;
         }
-        if (spec_track && spec_last >= 0) {  // diagnostics: is the subtree the walk chose on this descent's path?
-            ++spec_tries;
-            int64_t h = hole;
-            while (h > spec_last) h = (h - 1) / 2;
-            spec_hits += h == spec_last;
-        }
         for (int i = 0; i < nm; ++i) recs[mv_slot[i]].pq = (int32_t)(mv_pos[i] + 1);
         push_hole(hole, top, value);
     }
@@ -295,41 +288,6 @@ struct DenseHeap {
         adjust(0, last, value);
         --len;
         return ret;
-    }
-    // Speculative descent.  A pop descends the min-child chain from the root
-    // to the bottom whatever value it re-inserts (adjust above, libstdc++'s
-    // __adjust_heap), and the next pop's chain is mostly fixed once this pop
-    // is done: the successors pushed or decreased in between sift up from
-    // the bottom and seldom reach it (C3: the walk ends on the next pop's
-    // path in 83 % of the expansions, a successor took the root 7 times).
-    // spec_prefetch walks that chain through the cached upper levels and
-    // prefetches the whole subtree of its last node over the bottom `deep`
-    // levels (2 + 4 + ... + 2^deep entries, a few contiguous runs), so the
-    // next pop's DRAM levels arrive while the expansion visits its
-    // successors.  It only reads: a wrong guess costs its prefetches, never a
-    // result.  (Walking one level per successor visit instead -- blocking
-    // loads in the visit loop -- moved the pops' stalls into the visits:
-    // pops 25.2 -> 15.0 Gcycles, visits 19.1 -> 31.4 Gcycles.)
-    bool spec_track = false;  // diagnostics (ULG_EXACT_PROF): where the walks ended
-    int64_t spec_last = -1, spec_tries = 0, spec_hits = 0, root_moves = 0;
-    inline void spec_prefetch(int deep) {
-        spec_last = -1;
-        if (len < 4) return;
-        const int D = 63 - __builtin_clzll((uint64_t)len);  // the bottom level
-        int64_t s = 0;
-        for (int lv = 0; lv < D - deep; ++lv) {
-            const int64_t second = 2 * (s + 1);
-            if (second >= len) break;
-            s = second - (int64_t)cns(a[second], a[second - 1]);
-        }
-        for (int d = 1; d <= deep; ++d) {
-            const int64_t b = ((s + 1) << d) - 1;
-            if (b >= len) break;
-            const int64_t e = std::min<int64_t>(b + ((int64_t)1 << d), len);
-            for (int64_t i = b; i < e; i += 8) __builtin_prefetch(&a[i]);
-            __builtin_prefetch(&a[e - 1]);
-        }
-        if (spec_track) spec_last = s;
     }
     void update(uint32_t x) {
         const int64_t pos = (int64_t)recs[x].pq - 1;

@@ -301,64 +301,24 @@ __global__ void __launch_bounds__(1024) zeta_strided_reg_kernel(ZetaBArgs a) {
     for (int i = 0; i < 16; ++i) tv[base | ((uint64_t)((i << 6) | q) << bit_lo) | c] = r[i];
 }
 
-// successor-cost rows for the dense exact-order search: thread t of a chunk
+// Successor-cost rows for the dense exact-order search: thread t of a chunk
 // fills row r = r0 + t / nl, column li: getScore(scc_li, S) with
-// S = pdep(r, scope) -- one contiguous row per popped node instead of one
-// random lattice read per successor
-// Successor-cost rows of the exact replay, W = nl + 2 words per subset r of
-// the scope: [i < nl] getScore(scc_i, S) (FLT_MAX for scc_i in S), [nl] the
-// bits of gmin[r], [nl + 1] opt[r] (both 0 without them; gmin_layer_kernel)
+// S = pdep(r, scope) (FLT_MAX for scc_li in S) -- one contiguous row per
+// popped node instead of one random lattice read per successor.
 __global__ void __launch_bounds__(kB) cost_rows_kernel(SearchDev d, const int *meta, int m, int nl, uint64_t r0,
-                                                       uint64_t cnt, float *out, const float *gmin,
-                                                       const uint32_t *opt) {
+                                                       uint64_t cnt, float *out) {
     __shared__ int bits[64], vars[64];
     for (int i = threadIdx.x; i < m; i += kB) bits[i] = meta[i];
     for (int i = threadIdx.x; i < nl; i += kB) vars[i] = meta[64 + i];
     __syncthreads();
-    const int W = nl + 2;
     const uint64_t t = flat_block() * kB + threadIdx.x;
-    if (t >= cnt * (uint64_t)W) return;
-    const uint64_t r = r0 + t / (uint64_t)W;
-    const int li = (int)(t % (uint64_t)W);
-    if (li >= nl) {
-        out[t] = !gmin ? 0.0f : li == nl ? gmin[r] : __uint_as_float(opt[r]);
-        return;
-    }
+    if (t >= cnt * (uint64_t)nl) return;
+    const uint64_t r = r0 + t / (uint64_t)nl;
+    const int li = (int)(t % (uint64_t)nl);
     uint64_t S = 0;
     for (uint64_t x = r; x; x &= x - 1) S |= 1ull << bits[__builtin_ctzll(x)];
     const int leaf = vars[li];
     out[t] = ((S >> leaf) & 1ull) ? FLT_MAX : bs_cost(d, leaf, S);
-}
-
-// The smallest g the exact replay can ever give a node (scope == the scc, so
-// the root is the empty set and every scope variable is a leaf): gmin[r] =
-// min over j in r of fl(gmin[r ^ 2^j] + getScore(bits[j], S ^ {bits[j]})),
-// gmin[0] = +0, one layer (|r| = L) per launch; opt[u] gets bit j for every
-// predecessor u = r ^ 2^j that attains the minimum.  The replay adds the same
-// getScore values in the same float operation, and rounding is monotone, so
-// a node's g is never below its gmin; a node whose g reaches gmin can never
-// be improved (search_host.cpp's settled bitset).
-__global__ void __launch_bounds__(kB) gmin_layer_kernel(SearchDev d, const int *meta, int m, int L, float *gmin,
-                                                        uint32_t *opt) {
-    __shared__ int bits[64];
-    for (int i = threadIdx.x; i < m; i += kB) bits[i] = meta[i];
-    __syncthreads();
-    const uint64_t r = flat_block() * kB + threadIdx.x;
-    if (r >> m || __popcll(r) != L) return;
-    uint64_t S = 0;
-    for (uint64_t x = r; x; x &= x - 1) S |= 1ull << bits[__builtin_ctzll(x)];
-    float best = FLT_MAX;
-    for (uint64_t x = r; x; x &= x - 1) {
-        const int j = __builtin_ctzll(x);
-        const float v = gmin[r ^ (1ull << j)] + bs_cost(d, bits[j], S ^ (1ull << bits[j]));
-        best = v < best ? v : best;
-    }
-    gmin[r] = best;
-    for (uint64_t x = r; x; x &= x - 1) {
-        const int j = __builtin_ctzll(x);
-        const float v = gmin[r ^ (1ull << j)] + bs_cost(d, bits[j], S ^ (1ull << bits[j]));
-        if (v == best) atomicOr(&opt[r ^ (1ull << j)], 1u << j);
-    }
 }
 
 __global__ void __launch_bounds__(kB) cost_table_kernel(const uint32_t *table, uint64_t total, float *costs) {
@@ -754,7 +714,7 @@ int search_cost_rows_host(ulg_ctx *c, uint64_t scope, uint64_t scc, int64_t dead
     SearchState &s = *c->search;
     if (timed_out) *timed_out = false;
     if (s.rows_ready && s.rows_scope == scope && s.rows_scc == scc) return ULG_OK;
-    const int m = __builtin_popcountll(scope), nl = __builtin_popcountll(scc), W = nl + 2;
+    const int m = __builtin_popcountll(scope), nl = __builtin_popcountll(scc), W = nl;
     const uint64_t rows = 1ull << m, total = rows * (uint64_t)W;
     if (!s.host_rows.reserve((size_t)total * 4, true))
         return set_err(c, ULG_ERR_HIP, "cannot map the host row table (" + std::to_string(total * 4 >> 20) + " MiB)");
@@ -771,25 +731,6 @@ int search_cost_rows_host(ulg_ctx *c, uint64_t scope, uint64_t scc, int64_t dead
     if ((rc = ensure(c, s.d_rows, (size_t)(chunk_rows * W))) || (rc = ensure(c, s.d_rowmeta, 128))) return rc;
     ULG_HIP(c, hipMemcpyAsync(s.d_rowmeta.p, meta.data(), 128 * 4, hipMemcpyHostToDevice, c->stream));
     const SearchDev d = s.dev();
-    // each node's smallest reachable g and its optimal in-edges (the replay's
-    // settled bitset), when the root is the empty set (no ancestors)
-    s.rows_gmin = false;
-    const float *gm = nullptr;
-    const uint32_t *go = nullptr;
-    if (scope == scc && c->exact_settled) {
-        if ((rc = ensure(c, s.d_gmin, (size_t)rows)) || (rc = ensure(c, s.d_gopt, (size_t)rows))) return rc;
-        ULG_HIP(c, hipMemsetAsync(s.d_gmin.p, 0, (size_t)rows * 4, c->stream));
-        ULG_HIP(c, hipMemsetAsync(s.d_gopt.p, 0, (size_t)rows * 4, c->stream));
-        prof_begin(c, "bs_gmin_layers");
-        for (int L = 1; L <= m; ++L)
-            gmin_layer_kernel<<<flat_grid((rows + kB - 1) / kB), kB, 0, c->stream>>>(d, s.d_rowmeta.p, m, L,
-                                                                                       s.d_gmin.p, s.d_gopt.p);
-        prof_end(c);
-        ULG_HIP(c, hipGetLastError());
-        gm = s.d_gmin.p;
-        go = s.d_gopt.p;
-        s.rows_gmin = true;
-    }
     float *host = static_cast<float *>(s.host_rows.p);
     s.rows_ready = false;
     for (uint64_t r0 = 0; r0 < rows; r0 += chunk_rows) {
@@ -804,7 +745,7 @@ int search_cost_rows_host(ulg_ctx *c, uint64_t scope, uint64_t scc, int64_t dead
         const uint64_t work = cnt * (uint64_t)W;
         prof_begin(c, "bs_cost_rows");
         cost_rows_kernel<<<flat_grid((work + kB - 1) / kB), kB, 0, c->stream>>>(d, s.d_rowmeta.p, m, nl, r0, cnt,
-                                                                                  s.d_rows.p, gm, go);
+                                                                                  s.d_rows.p);
         prof_end(c);
         ULG_HIP(c, hipGetLastError());
         ULG_HIP(c, hipMemcpyAsync(host + r0 * (uint64_t)W, s.d_rows.p, (size_t)work * 4, hipMemcpyDeviceToHost,
@@ -812,10 +753,6 @@ int search_cost_rows_host(ulg_ctx *c, uint64_t scope, uint64_t scc, int64_t dead
     }
     ULG_HIP(c, hipStreamSynchronize(c->stream));
     prof_collect(c);
-    if (s.rows_gmin) {  // only the replay's rows need them
-        release(s.d_gmin);
-        release(s.d_gopt);
-    }
     s.rows_scope = scope;
     s.rows_scc = scc;
     s.rows_ready = true;

@@ -200,7 +200,7 @@ constexpr uint64_t kDenseRowsMaxBytes = 8ull << 30;
 
 inline bool dense_eligible(uint64_t scope, uint64_t scc) {
     const int m = __builtin_popcountll(scope);
-    return m <= kDenseScopeBits && ((1ull << m) * (uint64_t)(__builtin_popcountll(scc) + 2) * 4) <= kDenseRowsMaxBytes;
+    return m <= kDenseScopeBits && ((1ull << m) * (uint64_t)__builtin_popcountll(scc) * 4) <= kDenseRowsMaxBytes;
 }
 
 // run_astar_on_one_scc (astar_main.cpp:216-546) over dense node homes
@@ -212,9 +212,9 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
     const int m = __builtin_popcountll(scope);
     const uint64_t nslots = 1ull << m;
     const int nl = __builtin_popcountll(the_scc);
-    const uint64_t W = (uint64_t)nl + 2;  // row: nl costs, gmin, opt (search_cost_rows_host)
+    const uint64_t W = (uint64_t)nl;  // row: the nl successor costs (search_cost_rows_host)
     const float *rows = static_cast<const float *>(s.host_rows.p);
-    HostHuge recmem, heapmem, setmem;
+    HostHuge recmem, heapmem;
     // the heap's buffer starts 8 B into a line, so a node's two children
     // (2i+1, 2i+2) share 16 aligned bytes and its 16 great-great-grandchildren
     // two lines
@@ -224,30 +224,14 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
     DenseHeap open;
     open.recs = recs;
     open.a = static_cast<DEnt *>(heapmem.p) + 1;
-    // settled bitset (exact_settled): one bit per node of the scope, set when
-    // the node is closed or its g reaches gmin; needs the rows' gmin / opt
-    // words, which exist when the root is the empty set
-    uint64_t *settled = nullptr;
-    if (s.rows_gmin && ancestors == 0 && scope == the_scc) {
-        const size_t sb = std::max<size_t>(8, (size_t)(nslots / 8));
-        if (!setmem.reserve(sb, false)) return set_err(c, ULG_ERR_HIP, "cannot map the settled bitset");
-        setmem.zero_prefix(sb);
-        settled = static_cast<uint64_t *>(setmem.p);
-    }
-    // pop: prefetch 5 levels ahead too (C3: 17.6 -> 16.8 s on the box's EPYC
-    // 9575F; ULG_EXACT_PF=0 turns it off).  Prefetching the entries of the
-    // coming decrease-keys (18.3 s), or the likely next pop's row and
-    // successor records (18.6 s), was measured slower and is not done.
-    // Bit 2 (default on): the heap top's successor records and cost row are
+    // Prefetch modes (ULG_EXACT_PF, default 6, A/B only): bit 1, the pop also
+    // prefetches 5 heap levels ahead (C3 17.6 -> 16.8 s on the box's EPYC
+    // 9575F); bit 2, the heap top's successor records and cost row are
     // prefetched before its pop, so they arrive while the pop descends the
-    // heap (C3 16.9 -> 14.0 s, 2 alternating A/B runs); bit 3 adds the coming
-    // decrease-keys' heap entries after the pop (measured no better).
+    // heap (C3 16.9 -> 14.0 s, 2 alternating A/B runs).  Every other layout
+    // or prefetch tried was no faster and is gone.
     const int pfmode = std::getenv("ULG_EXACT_PF") ? std::atoi(std::getenv("ULG_EXACT_PF")) : 6;
     open.pf5 = (pfmode & 2) != 0;
-    // bit 4: the next pop's bottom ULG_EXACT_SPEC_DEEP levels are prefetched
-    // before the successor visits (DenseHeap::spec_prefetch)
-    const bool spec = (pfmode & 16) != 0;
-    const int spec_deep = std::getenv("ULG_EXACT_SPEC_DEEP") ? std::atoi(std::getenv("ULG_EXACT_SPEC_DEEP")) : 6;
 
     // slot bit of each variable, and its column in the row table
     uint32_t sbit[64] = {0};
@@ -268,10 +252,9 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
     const float upperBound = FLT_MAX;
     int64_t nexp = 0;
     static const bool prof = std::getenv("ULG_EXACT_PROF") != nullptr;
-    open.spec_track = spec && prof;
     uint64_t c_pop = 0, c_succ = 0, t0 = 0, t1 = 0;
     uint64_t pop_hist[64][2] = {};  // pop cycles by log2(heap length)
-    int64_t n_push = 0, n_upd = 0, n_succ = 0, n_skip = 0;
+    int64_t n_push = 0, n_upd = 0, n_succ = 0;
     while (open.len > 0) {
         if (deadline && (nexp & 4095) == 0 && Clock::now() > *deadline) {
             c->out_of_time = 1;
@@ -288,19 +271,7 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
             const float *trow = rows + (uint64_t)top * W;
             __builtin_prefetch(trow);
             __builtin_prefetch(trow + W - 1);
-            for (uint64_t x = the_scc & ~tv; x; x &= x - 1) {
-                const uint32_t si = top | sbit[__builtin_ctzll(x)];
-                if (!settled || (pfmode & 128) || !((settled[si >> 6] >> (si & 63)) & 1ull))
-                    __builtin_prefetch(&recs[si], 1);
-            }
-            if ((pfmode & 96) == 96)
-                // bit 6 (with bit 5): those records arrived during the last
-                // expansion, so the heap entries of the coming decrease-keys
-                // can be requested before the pop too
-                for (uint64_t x = the_scc & ~tv; x; x &= x - 1) {
-                    const int32_t p = recs[top | sbit[__builtin_ctzll(x)]].pq;
-                    if (p > 0) __builtin_prefetch(&open.a[p - 1], 1);
-                }
+            for (uint64_t x = the_scc & ~tv; x; x &= x - 1) __builtin_prefetch(&recs[top | sbit[__builtin_ctzll(x)]], 1);
         }
         const uint32_t ui = open.pop();
         if (prof) {
@@ -324,50 +295,14 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
                 if ((variables & edges[leaf]) == 0) leaves &= ~(1ull << leaf);
             }
         const float *row = rows + (uint64_t)ui * W;
-        // u's g is its smallest reachable one: its optimal out-edges give
-        // their successors theirs, after which nothing can improve them
-        uint32_t uopt = 0;
-        if (settled) {
-            uint32_t om;
-            std::memcpy(&om, row + nl + 1, 4);
-            if (ug == row[nl]) uopt = om;
-            settled[ui >> 6] |= 1ull << (ui & 63);  // closed: never updated again (no re-opening)
-        }
         if (!(pfmode & 4)) {
             __builtin_prefetch(row);
             __builtin_prefetch(row + W - 1);
             for (uint64_t x = leaves; x; x &= x - 1) __builtin_prefetch(&recs[ui | sbit[__builtin_ctzll(x)]], 1);
         }
-        if (pfmode & 8) {
-            // the heap entries the coming decrease-keys start from (the
-            // records are in cache by now)
-            for (uint64_t x = leaves; x; x &= x - 1) {
-                const int32_t p = recs[ui | sbit[__builtin_ctzll(x)]].pq;
-                if (p > 0) __builtin_prefetch(&open.a[p - 1], 1);
-            }
-        }
-        // the next pop's bottom levels, fetched during the visits (DenseHeap::spec_prefetch)
-        if (spec) open.spec_prefetch(spec_deep);
-        if ((pfmode & 32) && open.len > 0) {
-            // bit 5: the next pop is the heap top now (a successor hardly ever
-            // takes the root): its successor records and cost row start
-            // arriving during these visits instead of during its own pop
-            const uint32_t nt = open.a[0].slot();
-            const uint64_t ntv = g_have_bmi2 ? pdep_bmi2(nt, scope) : pdep64(nt, scope);
-            const float *nrow = rows + (uint64_t)nt * W;
-            __builtin_prefetch(nrow);
-            __builtin_prefetch(nrow + W - 1);
-            for (uint64_t x = the_scc & ~ntv; x; x &= x - 1) __builtin_prefetch(&recs[nt | sbit[__builtin_ctzll(x)]], 1);
-        }
         for (uint64_t x = leaves; x; x &= x - 1) {
             const int leaf = __builtin_ctzll(x);
             const uint32_t si = ui | sbit[leaf];
-            // a settled node (closed, or its g at gmin) ignores every visit:
-            // its record is not read
-            if (settled && ((settled[si >> 6] >> (si & 63)) & 1ull)) {
-                if (prof) ++n_skip;
-                continue;
-            }
             DenseRec &R = recs[si];
             // getScore(leaf, S u {leaf}) == getScore(leaf, S): leaf is never in its own sets
             const float g = ug + row[col[leaf]];
@@ -377,7 +312,6 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
                 R.h = T.h(variables | (1ull << leaf), &complete);
                 R.leaf = (uint8_t)leaf;
                 open.push(si);
-                if (uopt & sbit[leaf]) settled[si >> 6] |= 1ull << (si & 63);
                 if (prof) ++n_push;
                 continue;
             }
@@ -386,7 +320,6 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
                 R.leaf = (uint8_t)leaf;
                 R.g = g;
                 open.update(si);
-                if (uopt & sbit[leaf]) settled[si >> 6] |= 1ull << (si & 63);
                 if (prof) ++n_upd;
             }
         }
@@ -395,11 +328,9 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
     if (prof)
         std::fprintf(stderr,
                      "exact_prof(dense) expanded=%lld successors=%lld pushes=%lld updates=%lld heap_peak=%lld | "
-                     "Gcycles pop=%.3f succ_loop=%.3f stale_scans=%lld spec=%d walks_ended_on_the_path=%lld/%lld root_moves=%lld "
-                     "settled=%d visits_skipped=%lld\n",
+                     "Gcycles pop=%.3f succ_loop=%.3f stale_scans=%lld\n",
                      (long long)nexp, (long long)n_succ, (long long)n_push, (long long)n_upd, (long long)open.hwm,
-                     c_pop * 1e-9, c_succ * 1e-9, (long long)open.scans, (int)spec, (long long)open.spec_hits,
-                     (long long)open.spec_tries, (long long)open.root_moves, settled != nullptr, (long long)n_skip);
+                     c_pop * 1e-9, c_succ * 1e-9, (long long)open.scans);
     if (prof) {  // are the records and heap on huge pages?  (THP can be off on a box)
         if (FILE *f = std::fopen("/proc/self/smaps_rollup", "r")) {
             char line[256];

@@ -223,11 +223,8 @@ struct SearchState {
     bool host_costs_ready = false;
     // exact-order search: one row of successor costs per subset of the scope,
     // row[pext(S, scope)][i] = getScore(scc_i, S) (FLT_MAX for scc_i in S)
-    HostHuge host_rows;        // nl + 2 words per row: the costs, gmin, opt (search.hip cost_rows_kernel)
+    HostHuge host_rows;        // nl words per row: the successor costs (search.hip cost_rows_kernel)
     DevBuf<float> d_rows;      // device staging for the row chunks
-    DevBuf<float> d_gmin;      // per subset of the scope: the smallest g the replay can give it
-    DevBuf<uint32_t> d_gopt;   // ... and the predecessors (bit j: r ^ 2^j) that attain it
-    bool rows_gmin = false;    // the rows carry gmin / opt (scope == scc)
     DevBuf<int> d_rowmeta;     // scope bit positions, scc variables
     uint64_t rows_scope = 0, rows_scc = 0;
     bool rows_ready = false;
@@ -298,7 +295,7 @@ struct SearchState {
         release(q_vars); release(q_sets); release(q_par); release(q_costs);
         if (host_costs) (void)hipHostFree(host_costs);
         host_costs = nullptr;
-        release(d_rows); release(d_rowmeta); release(d_gmin); release(d_gopt);
+        release(d_rows); release(d_rowmeta);
         release(d_sweep_w);
         sweep_ready = false;
         release(gs_bn); release(gs_edges); release(gs_layer_off); release(gs_cv); release(gs_chain);

@@ -67,6 +67,10 @@ struct Triplet {
     // clusters solved before, which the reference would search again
     bool timed = false;
     std::chrono::steady_clock::time_point deadline;
+    // set by the watchdog thread once the budget is spent: a search already
+    // running stops at its next poll, as the reference's loop stops inside
+    // run_astar_on_one_scc (`!outOfTime`, triplet_astar.cpp:355)
+    std::atomic<bool> expired{false};
     const std::vector<uint64_t> *no_solution() {
         static const std::vector<uint64_t> none(64, 0);
         c->out_of_time = 1;
@@ -205,9 +209,6 @@ bool astar_cluster_dense(const HostTables &T, uint64_t cluster, ClusterRun &R, c
         int i = 0;
         for (uint64_t x = cluster; x; x &= x - 1) sbit[__builtin_ctzll(x)] = 1u << i++;
     }
-    const int pfmode = std::getenv("ULG_EXACT_PF") ? std::atoi(std::getenv("ULG_EXACT_PF")) : 6;
-    const bool spec = (pfmode & 16) != 0;
-    const int spec_deep = std::getenv("ULG_EXACT_SPEC_DEEP") ? std::atoi(std::getenv("ULG_EXACT_SPEC_DEEP")) : 6;
     const uint32_t goal_slot = (uint32_t)(nslots - 1);
     const uint64_t r1 = cluster >> 1;
     recs[0] = DenseRec{0.0f, 0.0f, 0, (uint8_t)(r1 ? __builtin_ctzll(r1) + 1 : 0), {0, 0, 0}};
@@ -225,11 +226,6 @@ bool astar_cluster_dense(const HostTables &T, uint64_t cluster, ClusterRun &R, c
             const uint32_t top = open.a[0].slot();
             const uint64_t tv = g_have_bmi2 ? pdep_bmi2(top, cluster) : pdep64(top, cluster);
             for (uint64_t x = cluster & ~tv; x; x &= x - 1) __builtin_prefetch(&recs[top | sbit[__builtin_ctzll(x)]], 1);
-            if ((pfmode & 96) == 96)  // the coming decrease-keys' heap entries (search_host.cpp)
-                for (uint64_t x = cluster & ~tv; x; x &= x - 1) {
-                    const int32_t p = recs[top | sbit[__builtin_ctzll(x)]].pq;
-                    if (p > 0) __builtin_prefetch(&open.a[p - 1], 1);
-                }
         }
         const uint32_t ui = open.pop();
         ++nexp;
@@ -241,15 +237,6 @@ bool astar_cluster_dense(const HostTables &T, uint64_t cluster, ClusterRun &R, c
         const uint64_t variables = g_have_bmi2 ? pdep_bmi2(ui, cluster) : pdep64(ui, cluster);
         const uint64_t cand = cluster & ~variables;
         for (uint64_t x = cand; x; x &= x - 1) T.prefetch_bs(__builtin_ctzll(x), variables);
-        if (spec) open.spec_prefetch(spec_deep);  // the next pop's bottom levels (search_host.cpp)
-        if ((pfmode & 32) && open.len > 0) {  // the next pop's successor records and costs (search_host.cpp)
-            const uint32_t nt = open.a[0].slot();
-            const uint64_t ntv = g_have_bmi2 ? pdep_bmi2(nt, cluster) : pdep64(nt, cluster);
-            for (uint64_t x = cluster & ~ntv; x; x &= x - 1) {
-                __builtin_prefetch(&recs[nt | sbit[__builtin_ctzll(x)]], 1);
-                T.prefetch_bs(__builtin_ctzll(x), ntv);
-            }
-        }
         for (uint64_t x = cand; x; x &= x - 1) {
             const int leaf = __builtin_ctzll(x);
             const uint32_t si = ui | sbit[leaf];
@@ -315,7 +302,7 @@ int cluster_astar(Triplet &t, uint64_t cluster, std::vector<uint64_t> &op) {
     HostTables T;
     host_tables(*t.s, T);
     ClusterRun R;
-    search_cluster(T, cluster, R);
+    search_cluster(T, cluster, R, t.timed ? &t.expired : nullptr);
     t.expanded += R.nexp;
     if (R.hang) t.hang = true;
     return cluster_parents_of(t, R, op);
@@ -567,6 +554,7 @@ const std::vector<uint64_t> *cluster_parents(Triplet &t, uint64_t cluster) {
         ClusterRun R;
         bool ok = false;
         t.pool->take(cluster, R, ok);
+        if (R.cancelled) return t.no_solution();  // the watchdog stopped it (past the deadline)
         if (!ok) {
             t.rc = set_err(t.c, ULG_ERR_UNSUPPORTED, "pattern-database group larger than 24 variables");
             return nullptr;
@@ -779,6 +767,33 @@ extern "C" int ulg_triplet_astar(ulg_ctx *c, const uint64_t *edges, int pd_count
     init_skeleton(t, edges);
     set_parallel(t);
     SearchPool pool;  // its destructor cancels and joins whatever still runs
+    // -r: at the deadline every running cluster search stops at its next poll
+    // (t.expired for the driver's own search, the pool's cancel flag for the
+    // look-ahead threads); the driver then answers "no solution" (:657-662).
+    // Declared after the pool, so it is joined before the pool shuts down.
+    struct Watchdog {
+        std::mutex mu;
+        std::condition_variable cv;
+        bool stop = false;
+        std::thread th;
+        ~Watchdog() {
+            if (!th.joinable()) return;
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                stop = true;
+            }
+            cv.notify_all();
+            th.join();
+        }
+    } wd;
+    if (t.timed)
+        wd.th = std::thread([&t, &pool, &wd] {
+            std::unique_lock<std::mutex> lk(wd.mu);
+            if (!wd.cv.wait_until(lk, t.deadline, [&wd] { return wd.stop; })) {
+                t.expired = true;
+                pool.cancel = true;
+            }
+        });
     if (t.parallel_ok) {
         pool.start(s, pd_count, t.threads);
         t.pool = &pool;

@@ -199,12 +199,6 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         c->score_variant = (int)value;
         return ULG_OK;
     }
-    if (std::strcmp(name, "exact_settled") == 0) {
-        if (value < 0 || value > 1) return set_err(c, ULG_ERR_ARG, "exact_settled must be 0 or 1");
-        if (c->exact_settled != (int)value && c->search) c->search->rows_ready = false;  // rows with / without gmin
-        c->exact_settled = (int)value;
-        return ULG_OK;
-    }
     if (std::strcmp(name, "time_limit_ms") == 0) {
         if (value < 0) return set_err(c, ULG_ERR_ARG, "time_limit_ms must be >= 0");
         c->time_limit_ms = value;

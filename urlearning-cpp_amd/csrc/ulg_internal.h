@@ -79,7 +79,6 @@ struct ulg_ctx {
     int completed_layer = -1;      // highest fully scored layer of the last scoring call
     uint64_t table_budget_kb = 0;  // best-score table budget in KiB (0 = half the free HBM)
     int sweep_table = 1;
-    int exact_settled = 0;         // exact replay: skip visits of nodes whose g reached gmin (settled bitset; measured no faster)
     int wide_prune = 1;            // wide walks: skip absent nodes whose subsets hold no key >= -ts
     int wide_reduced = 1;          // wide walks: skip the recursion's no-op re-tests
     int wide_lds = 1;              // wide walks: long ones replayed with their bitsets in LDS
