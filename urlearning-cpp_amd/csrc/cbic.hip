@@ -31,6 +31,8 @@
 
 #include "search_internal.h"
 #include "host_walk.h"
+#include "cbic_dev.h"
+#include "cbic_pipe.h"
 
 using namespace ulg;
 
@@ -38,11 +40,8 @@ namespace {
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kBlock = 256;
 constexpr int kGramRows = 1024;  // rows of Z per Gram wave (split-K chunk)
 
-__device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
-__device__ __forceinline__ float absent_f() { return __uint_as_float(kAbsentBits); }
 
 // ------------------------------------------------------------------------
 // Normalisation (BIC_OLS.cpp:66-97): x - mean, divided by the sample std
@@ -139,246 +138,6 @@ __global__ void __launch_bounds__(kBlock) gram_reduce_kernel(const double *parti
     gram[idx] = s;
 }
 
-// ------------------------------------------------------------------------
-// Combinatorics on compact candidate indices.  colex rank of a sorted set
-// {a_1 < ... < a_L} is sum_j C(a_j, j): Gosper's next-permutation walks
-// exactly this order (typedefs.h:692-697), so rank == enumeration index.
-// ------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t B(const uint32_t *binom, int a, int k) { return binom[a * kBinomK + k]; }
-
-__device__ __forceinline__ uint64_t unrank_colex(uint64_t r, int l, int U, const uint32_t *binom) {
-    uint64_t mask = 0;
-    int c = U - 1;
-    for (int i = l; i >= 1; --i) {
-        while (c >= 0 && (uint64_t)B(binom, c, i) > r) --c;
-        mask |= 1ull << c;
-        r -= B(binom, c, i);
-        --c;
-    }
-    return mask;
-}
-
-__device__ __forceinline__ uint64_t rank_colex(uint64_t mask, const uint32_t *binom) {
-    uint64_t r = 0;
-    int j = 0;
-    while (mask) {
-        const int a = __builtin_ctzll(mask);
-        mask &= mask - 1;
-        ++j;
-        r += B(binom, a, j);
-    }
-    return r;
-}
-
-// Per-lane bitset over the subsets of (P u {var 0}) in local numbering.
-template <int W>
-struct Bits {
-    static constexpr int kWords = W;
-    uint64_t w[W];
-    __device__ __forceinline__ void clear() {
-#pragma unroll
-        for (int j = 0; j < W; ++j) w[j] = 0;
-    }
-    __device__ __forceinline__ bool test(uint32_t i) const {
-        uint64_t x = w[0];
-#pragma unroll
-        for (int j = 1; j < W; ++j) x = ((int)(i >> 6) == j) ? w[j] : x;
-        return (x >> (i & 63)) & 1ull;
-    }
-    __device__ __forceinline__ void set(uint32_t i) {
-        const uint64_t bit = 1ull << (i & 63);
-#pragma unroll
-        for (int j = 0; j < W; ++j) w[j] |= ((int)(i >> 6) == j) ? bit : 0ull;
-    }
-    __device__ __forceinline__ void reset(uint32_t i) {
-        const uint64_t bit = 1ull << (i & 63);
-#pragma unroll
-        for (int j = 0; j < W; ++j) w[j] &= ((int)(i >> 6) == j) ? ~bit : ~0ull;
-    }
-    __device__ __forceinline__ uint64_t word(int j) const { return w[j]; }
-};
-
-// The same bitset with its words in LDS, thread-interleaved (word j of this
-// thread at base[j * kBlock]).  For W >= 4 the compiler turns the register
-// select chains back into indexed accesses and puts the arrays in scratch
-// (global memory) -- every walk test then pays a memory round trip; LDS keeps
-// the indexing cheap.
-template <int W>
-struct BitsLds {
-    static constexpr int kWords = W;
-    uint64_t *base;
-    __device__ __forceinline__ void clear() {
-#pragma unroll
-        for (int j = 0; j < W; ++j) base[j * kBlock] = 0;
-    }
-    __device__ __forceinline__ bool test(uint32_t i) const { return (base[(i >> 6) * kBlock] >> (i & 63)) & 1ull; }
-    __device__ __forceinline__ void set(uint32_t i) { base[(i >> 6) * kBlock] |= 1ull << (i & 63); }
-    __device__ __forceinline__ void reset(uint32_t i) { base[(i >> 6) * kBlock] &= ~(1ull << (i & 63)); }
-    __device__ __forceinline__ uint64_t word(int j) const { return base[j * kBlock]; }
-};
-
-// find_best_subset_score (BIC_OLS.cpp:125-172) replayed on local masks.
-// pv: M entries of 4 bits (local bit numbers; entries past the filled ones
-// are 0 == variable 0, the zero-initialised arma::uvec of SURVEY N3).  Only
-// WHICH cached keys are visited matters: the return value is the max over
-// their cached values (and 0), so the recursion records them in `visited`.
-template <int M, class BS>
-__device__ __forceinline__ void best_subset(uint32_t T, uint32_t pv, const BS &present, BS &checked, BS &visited) {
-#pragma nounroll
-    for (int idx = 0; idx < M; ++idx) {
-        const uint32_t u = (pv >> (4 * idx)) & 15u;
-        const uint32_t T2 = T ^ (1u << u);
-        if (checked.test(T2)) continue;
-        if (present.test(T2)) {
-            visited.set(T2);
-            continue;
-        }
-        if constexpr (M > 1) {
-            uint32_t npv = 0;
-            int j = 0;
-#pragma nounroll
-            for (int i = 0; i < M; ++i) {
-                const uint32_t pi = (pv >> (4 * i)) & 15u;
-                if (pi == u) continue;
-                npv |= pi << (4 * j);
-                ++j;
-                best_subset<M - 1, BS>(T2, npv, present, checked, visited);
-                checked.set(T2);
-            }
-        }
-    }
-}
-
-// The same traversal with the decision folded in (variant bit 2).  The caller
-// only needs "is some visited key's value >= -ts" (BIC_OLS.cpp:234 with
-// bic_threshold 0 and best_score starting at 0 < -ts): `hi` marks the present
-// keys with value >= -ts, and the walk stops at the first one it visits.
-// Present keys never enter `checked` (only recursed, absent keys do), so a
-// present key is visited exactly when the walk tests it -- stopping early
-// cannot change the answer, and no value is reloaded afterwards.
-// Measured at C3 layer 6: 3.1 ms vs 2.8 ms for the full walk (bit 2 clear) --
-// a wave only leaves the walk when all its lanes do, so the early exit buys
-// little, while the extra exits cost issue slots.  An equivalent walk without
-// the reference's redundant re-tests (2.2x fewer union points per wave in a
-// host simulation) measured 5.6 ms: heavier control flow, occupancy 2.
-template <int M, class BS>
-__device__ __forceinline__ bool dominated(uint32_t T, uint32_t pv, const BS &present, const BS &hi, BS &checked,
-                                          uint32_t &steps) {
-#pragma nounroll
-    for (int idx = 0; idx < M; ++idx) {
-        ++steps;
-        const uint32_t u = (pv >> (4 * idx)) & 15u;
-        const uint32_t T2 = T ^ (1u << u);
-        if (checked.test(T2)) continue;
-        if (present.test(T2)) {
-            if (hi.test(T2)) return true;
-            continue;
-        }
-        if constexpr (M > 1) {
-            uint32_t npv = 0;
-            int j = 0;
-#pragma nounroll
-            for (int i = 0; i < M; ++i) {
-                const uint32_t pi = (pv >> (4 * i)) & 15u;
-                if (pi == u) continue;
-                npv |= pi << (4 * j);
-                ++j;
-                if (dominated<M - 1, BS>(T2, npv, present, hi, checked, steps)) return true;
-                checked.set(T2);
-            }
-        }
-    }
-    return false;
-}
-
-// dominated() with the hi-cover prune: an absent node T2 is expanded only if
-// some key >= -ts lies in U(T2) = subsets of T2 u {var 0} (`cover`, tested at
-// T2 without var 0).  Skipping an expansion changes `checked` only inside
-// U(T2); a later test that sees the difference expands a node of U(T2), whose
-// own expansion again stays inside U(T2) -- so every difference stays within
-// keys none of which is >= -ts, and the first such key the walk visits, if
-// any, is the same.  (The queued lanes of C3 layer 6 walk 13 steps instead of
-// 220 when stored, 113 instead of 194 when pruned.)
-template <int M, class BS>
-__device__ __forceinline__ bool dominated_cov(uint32_t T, uint32_t pv, const BS &present, const BS &hi,
-                                              const BS &cover, BS &checked) {
-#pragma nounroll
-    for (int idx = 0; idx < M; ++idx) {
-        const uint32_t u = (pv >> (4 * idx)) & 15u;
-        const uint32_t T2 = T ^ (1u << u);
-        if (checked.test(T2)) continue;
-        if (present.test(T2)) {
-            if (hi.test(T2)) return true;
-            continue;
-        }
-        if constexpr (M > 1) {
-            if (!cover.test(T2 & ~1u)) continue;
-            uint32_t npv = 0;
-            int j = 0;
-#pragma nounroll
-            for (int i = 0; i < M; ++i) {
-                const uint32_t pi = (pv >> (4 * i)) & 15u;
-                if (pi == u) continue;
-                npv |= pi << (4 * j);
-                ++j;
-                if (dominated_cov<M - 1, BS>(T2, npv, present, hi, cover, checked)) return true;
-                checked.set(T2);
-            }
-        }
-    }
-    return false;
-}
-
-// dominated_cov() with its three per-node tests folded into one: `open` =
-// absent & hi-cover & not yet checked, so a tested node is a hit (hi), an
-// expansion (open) or nothing; clearing its open bit after the first call
-// returns is the reference's checked.insert (present nodes never enter
-// `checked`, so testing hi before `checked` changes nothing).
-template <int M, class BS, bool DIAG = false>
-__device__ __forceinline__ bool walk_open(uint32_t T, uint32_t pv, const BS &hi, BS &open, uint32_t &steps) {
-#pragma nounroll
-    for (int idx = 0; idx < M; ++idx) {
-        if constexpr (DIAG) ++steps;
-        const uint32_t u = (pv >> (4 * idx)) & 15u;
-        const uint32_t T2 = T ^ (1u << u);
-        if (hi.test(T2)) return true;
-        if constexpr (M > 1) {
-            if (!open.test(T2)) continue;
-            uint32_t npv = 0;
-            int j = 0;
-#pragma nounroll
-            for (int i = 0; i < M; ++i) {
-                const uint32_t pi = (pv >> (4 * i)) & 15u;
-                if (pi == u) continue;
-                npv |= pi << (4 * j);
-                ++j;
-                if (walk_open<M - 1, BS, DIAG>(T2, npv, hi, open, steps)) return true;
-                open.reset(T2);
-            }
-        }
-    }
-    return false;
-}
-
-// cover = { T : some key of hi, without var 0, is a subset of T }: drop bit 0
-// of every key, then close upwards over bits 1 .. q-1 (in-word shifts for
-// bits 1..5, word ORs for the bits that index words).
-template <int W>
-__device__ __forceinline__ void cover_words(uint64_t *w) {
-    constexpr uint64_t kM[6] = {0xAAAAAAAAAAAAAAAAull, 0xCCCCCCCCCCCCCCCCull, 0xF0F0F0F0F0F0F0F0ull,
-                                0xFF00FF00FF00FF00ull, 0xFFFF0000FFFF0000ull, 0xFFFFFFFF00000000ull};
-#pragma unroll
-    for (int j = 0; j < W; ++j) w[j] |= (w[j] & kM[0]) >> 1;
-#pragma unroll
-    for (int b = 1; b < 6; ++b)
-#pragma unroll
-        for (int j = 0; j < W; ++j) w[j] |= (w[j] & ~kM[b]) << (1 << b);
-#pragma unroll
-    for (int c = 1; c < W; c <<= 1)
-#pragma unroll
-        for (int j = 0; j < W; ++j)
-            if (j & c) w[j] |= w[j ^ c];
-}
 
 // Same recursion as an explicit stack machine: one loop iteration advances
 // one step of this lane's own traversal, so a wave costs the max over its
@@ -447,43 +206,6 @@ __device__ __forceinline__ void best_subset_stack(uint32_t Ptop, uint32_t pvtop,
     }
 }
 
-// Presence of every key with a fully unrolled subset loop: the rank of each
-// subset t of the Q local bits is a compile-time sum of per-(bit, position)
-// binomials preloaded into registers.  Q = L when variable 0 is in P (local
-// bits = P), Q = L + 1 otherwise (P plus variable 0).
-template <int L, int PHASE, int Q, int W>
-__device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi, float thr, const uint32_t *binom,
-                                                  uint64_t cpack, bool z, const float *table, const uint64_t *toffv) {
-    constexpr uint32_t Plocal = (Q == L) ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
-    uint32_t RB[Q][L + 1];
-#pragma unroll
-    for (int lb = 0; lb < Q; ++lb) {
-        const int ci = (int)((cpack >> (6 * lb)) & 63ull);
-#pragma unroll
-        for (int p = 1; p <= L; ++p) RB[lb][p] = (p <= lb + 1) ? B(binom, ci, p) : 0u;
-    }
-    uint64_t off[L + 1];
-#pragma unroll
-    for (int pc = 1; pc <= L; ++pc) off[pc] = toffv[pc];
-#pragma clang loop unroll(full)
-    for (uint32_t t = 1; t < (1u << Q); ++t) {
-        const int pc = __builtin_popcount(t);
-        if (pc > L || t == Plocal) continue;
-        if (pc == L && (PHASE == 0 || !(t & 1u))) continue;
-        if ((t & 1u) && !z) continue;
-        uint64_t rk = 0;
-        int jj = 0;
-#pragma unroll
-        for (int b = 0; b < Q; ++b)
-            if ((t >> b) & 1u) {
-                ++jj;
-                rk += RB[b][jj];
-            }
-        const float val = table[off[pc] + rk];
-        if (fbits(val) != kAbsentBits) present.set(t);
-        if (val >= thr) hi.set(t);  // the absent sentinel is a NaN: never >= thr
-    }
-}
 
 struct ScoreArgs {
     const double *gram;      // n x n row-major
@@ -516,8 +238,6 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, int on) {
     return x * q + (x < r ? x : r) + k;
 }
 
-// bitset words per lane over the subsets of L + 1 local bits
-__host__ __device__ constexpr int bits_words(int L) { return (L + 1) <= 6 ? 1 : (1 << ((L + 1) - 6)); }
 
 // LDS carve: gram | binom | work | tbl_off | recursion stack (variant bit 1)
 // | LDS bitsets (3 per lane when they have >= 4 words) | the block's
@@ -543,160 +263,7 @@ __host__ __device__ inline LdsLayout lds_layout(int n, int nv, int S, int L, int
     return l;
 }
 
-template <class BS>
-__device__ __forceinline__ BS make_bits(uint64_t *lds_base) {
-    if constexpr (std::is_same<BS, Bits<BS::kWords>>::value) {
-        (void)lds_base;
-        return BS{};
-    } else {
-        return BS{lds_base};
-    }
-}
 
-// A parent set in local numbering: local bit 0 is variable 0 (compact index
-// 0 when it is a candidate), local bits 1..L the other members of P in
-// increasing order (all L members of P when P contains variable 0).
-template <int L>
-struct LocalSet {
-    uint64_t cpack;   // local bit -> compact index, 6 bits each (bit 0 -> 0)
-    uint32_t Plocal;  // P itself
-    uint32_t pvtop;   // the top-level parent vector: P's local bits, 4 bits each
-    bool v0inP;
-};
-template <int L>
-__device__ __forceinline__ LocalSet<L> local_set(uint64_t cm, bool z) {
-    LocalSet<L> s;
-    s.v0inP = z && (cm & 1ull);
-    const uint64_t E = z ? (cm & ~1ull) : cm;
-    s.cpack = 0;
-    uint64_t rem = E;
-#pragma unroll
-    for (int i = 1; i <= L; ++i) {
-        if (rem) {
-            const uint64_t b = (uint64_t)__builtin_ctzll(rem);
-            rem &= rem - 1;
-            s.cpack |= b << (6 * i);
-        }
-    }
-    s.Plocal = s.v0inP ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
-    s.pvtop = 0;
-#pragma unroll
-    for (int i = 0; i < L; ++i) s.pvtop |= (uint32_t)(i + (s.v0inP ? 0 : 1)) << (4 * i);
-    return s;
-}
-
-// Presence of every candidate key below P u {var 0} in the cache as it
-// stands now (`present`), and which of them hold a value >= thr (`hi`).
-template <int L, int PHASE, int V, class BS>
-__device__ __forceinline__ void gather_keys(BS &present, BS &hi, const LocalSet<L> &ls, float thr,
-                                            const uint32_t *binom, bool z, const float *table,
-                                            const uint64_t *toffv) {
-    constexpr int W = BS::kWords;
-    if constexpr (L <= 6 && (V & 1)) {
-        presence_unrolled<L, PHASE, (PHASE == 0 ? L : L + 1), W>(present, hi, thr, binom, ls.cpack, z, table, toffv);
-    } else {
-        const int q = ls.v0inP ? L : L + 1;
-        const uint32_t full = 1u << q;
-#pragma nounroll
-        for (uint32_t t = 1; t < full; ++t) {
-            const int pc = __builtin_popcount(t);
-            bool cand = pc <= L && t != ls.Plocal && (z || !(t & 1u));
-            if (pc == L) cand = cand && PHASE == 1 && (t & 1u);
-            if (!cand) continue;
-            uint64_t rk = 0;
-            uint32_t rem = t;
-            int j = 0;
-            while (rem) {
-                const int lb = __builtin_ctz(rem);
-                rem &= rem - 1;
-                ++j;
-                rk += B(binom, (int)((ls.cpack >> (6 * lb)) & 63ull), j);
-            }
-            const float val = table[toffv[pc] + rk];
-            if (fbits(val) != kAbsentBits) present.set(t);
-            if (val >= thr) hi.set(t);
-        }
-    }
-}
-
-// The two-pass form's decision for a set with ts < 0 from its presence and hi
-// bitsets (variant bit 4).  Returns true when P is not stored; `queued` = the
-// set needs the walk.
-//  * no present key >= -ts: nothing the walk visits can prune P;
-//  * a present direct child >= -ts: always visited at the top;
-//  * (P without var 0) a present P\{a,b} or P\{a}+{0} >= -ts
-//    with P\{a} absent: P\{a} is first reached at the top
-//    level (nothing below P\{a'} contains a' != 0 again), so it
-//    is expanded with the full list, and its j = L-1 call tests
-//    every P\{a,b}, its j = 1 call (L >= 3) the toggle of var 0.
-//    Present keys never enter `checked`, so those are visited.
-template <int L, int PHASE, class BS>
-__device__ __forceinline__ bool settle_rules(const BS &present, const BS &hi, const LocalSet<L> &ls, bool &queued) {
-    constexpr int W = BS::kWords;
-    bool any = false;
-#pragma unroll
-    for (int wj = 0; wj < W; ++wj) any |= hi.word(wj) != 0ull;
-    bool dom = false;
-    queued = false;
-    if (!any) return false;
-#pragma unroll
-    for (int i = 0; i < L; ++i) dom |= hi.test(ls.Plocal ^ (1u << ((ls.pvtop >> (4 * i)) & 15u)));
-    if constexpr (PHASE == 1) {
-        constexpr uint32_t P1 = ((1u << L) - 1u) << 1;
-#pragma unroll
-        for (int ea = 1; ea <= L; ++ea) {
-            const uint32_t Ta = P1 ^ (1u << ea);
-            bool d2 = false;
-#pragma unroll
-            for (int eb = 1; eb <= L; ++eb)
-                if (eb != ea) d2 |= hi.test(Ta ^ (1u << eb));
-            if constexpr (L >= 3) d2 |= hi.test(Ta | 1u);
-            dom |= d2 && !present.test(Ta);
-        }
-        // One level further: X = P\{a,b} (a < b), absent, is first
-        // tested below P\{a} if that is absent (in its j = b-1
-        // call), else below P\{b} if absent (in its j = a call),
-        // else never.  Its expansion list holds the entries before
-        // the removed one: {1..b-1}\{a} in the first case, {1..a-1}
-        // in the second, plus zeros (the var-0 toggle, L >= 4).
-        if constexpr (L >= 3) {
-#pragma unroll
-            for (int ea = 1; ea <= L; ++ea)
-#pragma unroll
-                for (int eb = ea + 1; eb <= L; ++eb) {
-                    const uint32_t X = P1 ^ (1u << ea) ^ (1u << eb);
-                    bool h1 = false, h2 = false;
-#pragma unroll
-                    for (int ec = 1; ec < eb; ++ec) {
-                        if (ec == ea) continue;
-                        const bool hc = hi.test(X ^ (1u << ec));
-                        h1 |= hc;
-                        if (ec < ea) h2 |= hc;
-                    }
-                    if constexpr (L >= 4) {
-                        const bool ht = hi.test(X | 1u);
-                        h1 |= ht;
-                        h2 |= ht;
-                    }
-                    const bool pa = present.test(P1 ^ (1u << ea));
-                    const bool pb = present.test(P1 ^ (1u << eb));
-                    const bool hx = pa ? (!pb && h2) : h1;
-                    dom |= hx && !present.test(X);
-                }
-        }
-    } else {
-        // P\{0} is the very first node tested; if absent it is
-        // expanded with every list (1..j) + zeros, so each present
-        // P\{0,c} is visited.
-        constexpr uint32_t P0 = (1u << L) - 1u;
-        bool d2 = false;
-#pragma unroll
-        for (int ec = 1; ec < L; ++ec) d2 |= hi.test(P0 ^ 1u ^ (1u << ec));
-        dom |= d2 && !present.test(P0 ^ 1u);
-    }
-    queued = !dom;
-    return dom;
-}
 
 // Append a set to the walk queue (wave-aggregated: one atomic per wave):
 // table slot | ts bits << 32, the hi words, then the open words
@@ -729,44 +296,6 @@ __device__ __forceinline__ void queue_walk(const BS &present, const BS &hi, uint
     for (int wj = 0; wj < W; ++wj) e[1 + W + wj] = ow[wj];
 }
 
-// Subset maxima (variant bit 6).  hsub[slot of X] = the largest stored value
-// over the nonempty subsets of X, X included (NaN: none stored).  The walk of
-// P only ever visits keys in U(P) = the nonempty subsets of P u {var 0} other
-// than P and P u {var 0} (checked starts as {empty}; a layer-L key with var 0
-// is in the cache only in phase 1), so
-//   max over U(P) = max_a hsub[P\a]                    (P with var 0, or no var 0 candidate)
-//                 = max_a max(hsub[P\a], hsub[P\a+{0}]) (P without var 0, phase 1)
-// and a set whose U(P) holds no key >= -ts is stored without its 2^(L+1)
-// presence gathers.  Children ranks: for P = {a_1 < ... < a_L} (compact),
-//   rank(P\a_i)       = sum_{j<i} C(a_j, j)   + sum_{j>i} C(a_j, j-1)
-//   rank(P\a_i + {0}) = sum_{j<i} C(a_j, j+1) + sum_{j>i} C(a_j, j)   (a_1 >= 1)
-template <int L, bool WITH0>
-__device__ __forceinline__ void child_ranks(uint64_t cm, const uint32_t *binom, uint64_t (&rc)[L], uint64_t (&rz)[L]) {
-    uint32_t e[L], d[L], f[L];
-    uint64_t rem = cm;
-#pragma unroll
-    for (int j = 0; j < L; ++j) {
-        const int aj = __builtin_ctzll(rem);
-        rem &= rem - 1;
-        e[j] = B(binom, aj, j + 1);
-        d[j] = B(binom, aj, j);
-        f[j] = WITH0 ? B(binom, aj, j + 2) : 0u;
-    }
-    uint64_t pe = 0, pf = 0;
-#pragma unroll
-    for (int i = 0; i < L; ++i) {
-        uint64_t sd = 0, se = 0;
-#pragma unroll
-        for (int j = i + 1; j < L; ++j) {
-            sd += d[j];
-            se += e[j];
-        }
-        rc[i] = pe + sd;
-        rz[i] = pf + se;
-        pe += e[i];
-        pf += f[i];
-    }
-}
 
 // PHASE 0: sets containing variable 0; 1: the rest.  V = variant bits (see
 // ulg_set_option "score_variant"), compile-time so each form gets its own
@@ -824,47 +353,7 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         }
     }
 
-    // ---- OLS via the Gram matrix: Cholesky of G[P,P], y = L^-1 G[P,v] ----
-    double Lm[L][L];
-    double y[L];
-    const int n = a.n;
-#pragma unroll
-    for (int i = 0; i < L; ++i)
-#pragma unroll
-        for (int j = 0; j <= i; ++j) Lm[i][j] = g[gv[i] * n + gv[j]];
-#pragma unroll
-    for (int i = 0; i < L; ++i) y[i] = g[gv[i] * n + v];
-    const double cvv = g[v * n + v];
-#pragma unroll
-    for (int j = 0; j < L; ++j) {
-        double s = Lm[j][j];
-#pragma unroll
-        for (int k = 0; k < j; ++k) s -= Lm[j][k] * Lm[j][k];
-        const double d = sqrt(s);
-        Lm[j][j] = d;
-        const double inv = 1.0 / d;
-#pragma unroll
-        for (int i = j + 1; i < L; ++i) {
-            double t = Lm[i][j];
-#pragma unroll
-            for (int k = 0; k < j; ++k) t -= Lm[i][k] * Lm[j][k];
-            Lm[i][j] = t * inv;
-        }
-    }
-    double yy = 0.0;
-#pragma unroll
-    for (int i = 0; i < L; ++i) {
-        double t = y[i];
-#pragma unroll
-        for (int k = 0; k < i; ++k) t -= Lm[i][k] * y[k];
-        t = t / Lm[i][i];
-        y[i] = t;
-        yy += t * t;
-    }
-    const double rss = cvv - yy;
-    // BIC_OLS.cpp:366  num_err*log(error_L2) + lambda*log(num_err)*k - 0
-    const double the_score = a.N * log(rss / a.N) + a.lambda * log(a.N) * (double)L - 0.0;
-    const float ts = (float)the_score;
+    const float ts = cbic_set_score<L>(g, a.n, v, gv, a.N, a.lambda);
 
     if constexpr (CMP) {
         // 1. settle by the subset maxima: ts >= 0, no key >= -ts in U(P), or a
@@ -1148,82 +637,6 @@ __global__ void __launch_bounds__(kBlock) walk_kernel(const uint64_t *queue, con
     }
 }
 
-// ---- bit-sliced walk (score_variant bit 5) ----------------------------------
-// The walk's tree (T, pv, idx, i) never depends on the data: only which
-// subtrees a set enters does.  So one wave walks the union tree ONCE for 64*K
-// sets with scalar control flow, and every per-set test becomes a K-bit mask
-// operation: lane l holds sets l*K .. l*K+K-1, and for every local subset t
-// the K bits "set k has t in hi / open" sit in K-bit fields of register
-// vectors indexed by the (uniform) t.  The union of K*64 walks grows slowly
-// with the set count (host model over the dumped C3 patterns: 706 points for
-// 64 sets, 1076 for 512), so the work per set drops by an order of
-// magnitude against one set per lane.  Same decisions: each set still takes
-// exactly its own walk's steps, in its order; sets never interact.
-template <int L, int K_>
-struct Sliced {
-    static constexpr int Q = L + 1;                   // local bits (phase 0 uses L)
-    static constexpr int K = K_;                      // sets per lane
-    static constexpr int E = 32 / K;                  // subsets per register
-    static constexpr int NV0 = (1 << Q) / E;
-    static constexpr int NV = NV0 < 2 ? 2 : NV0;      // registers per bitset vector
-    static constexpr uint32_t KM = (1u << K) - 1u;
-    typedef uint32_t Vec __attribute__((ext_vector_type(NV)));
-};
-
-template <int L, int K>
-__device__ __forceinline__ uint32_t sl_get(const typename Sliced<L, K>::Vec &v, uint32_t t) {
-    using S = Sliced<L, K>;
-    return (v[t / S::E] >> (S::K * (t % S::E))) & S::KM;
-}
-template <int L, int K>
-__device__ __forceinline__ void sl_clear(typename Sliced<L, K>::Vec &v, uint32_t t, uint32_t m) {
-    using S = Sliced<L, K>;
-    v[t / S::E] &= ~(m << (S::K * (t % S::E)));
-}
-__device__ __forceinline__ bool wave_any(uint32_t x) { return __ballot(x != 0u) != 0ull; }
-
-// [idx_lo, idx_hi): the positions this call can change anything at.  The
-// j-th call fb(T2, npv) of a node's inner loop sees the positions below j-1
-// already tested by its earlier calls (closed, or present below -ts) and zeros
-// from j on, whose child T2 ^ {0} call 1 tested at its position 1 -- so call 1
-// walks positions 0..1 and call j >= 2 position j-1 only (the reference's
-// remaining re-tests are no-ops; the same tests in the same order).
-template <int L, int K, int M, bool DIAG = false>
-__device__ __forceinline__ void walk_sliced(uint32_t T, uint32_t pv, uint32_t act, const typename Sliced<L, K>::Vec &hiV,
-                                            typename Sliced<L, K>::Vec &openV, uint32_t &alive, uint32_t &dom,
-                                            uint32_t &pts, int idx_lo = 0, int idx_hi = M) {
-#pragma nounroll
-    for (int idx = idx_lo; idx < idx_hi; ++idx) {
-        act &= alive;
-        if (!wave_any(act)) return;
-        if constexpr (DIAG) ++pts;
-        const uint32_t u = (pv >> (4 * idx)) & 15u;
-        const uint32_t T2 = T ^ (1u << u);
-        // a hit ends that set's walk (the reference returns up the recursion)
-        const uint32_t h = sl_get<L, K>(hiV, T2) & act;
-        dom |= h;
-        alive &= ~h;
-        act &= ~h;
-        if constexpr (M > 1) {
-            uint32_t x = sl_get<L, K>(openV, T2) & act;
-            if (!wave_any(x)) continue;
-            uint32_t npv = 0;
-            int j = 0;
-#pragma nounroll
-            for (int i = 0; i < M; ++i) {
-                const uint32_t pi = (pv >> (4 * i)) & 15u;
-                if (pi == u) continue;
-                npv |= pi << (4 * j);
-                ++j;
-                if (j == 1) walk_sliced<L, K, M - 1, DIAG>(T2, npv, x, hiV, openV, alive, dom, pts, 0, M - 1 < 2 ? M - 1 : 2);
-                else walk_sliced<L, K, M - 1, DIAG>(T2, npv, x, hiV, openV, alive, dom, pts, j - 1, j);
-                sl_clear<L, K>(openV, T2, x);  // checked.insert(T2) for the sets that ran the call
-                x &= alive;
-                if (!wave_any(x)) break;
-            }
-        }
-    }
-}
 
 // one wave (64 threads) per 64*K queued sets; entries as walk_kernel's
 template <int L, int PHASE, int K>
@@ -2951,6 +2364,13 @@ int ulg_cbic_score_finish(ulg_ctx *c, int64_t *total_stored, int64_t *total_scor
         ULG_HIP(c, hipStreamSynchronize(c->stream));
         prof_collect(c);
         c->total_stored = (int64_t)*c->async_pinned;
+        if (c->pipe_pending) {
+            c->pipe_pending = false;
+            if (int rcp = pipe_check(c)) {
+                c->scored = false;
+                return rcp;
+            }
+        }
     }
     if (!c->scored) return set_err(c, ULG_ERR_STATE, "ulg_cbic_score_finish: nothing scored");
     if (total_stored) *total_stored = c->total_stored;
@@ -3076,10 +2496,24 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
         sa.hsub = c->d_hsub.p;
     }
     const char *wck = std::getenv("ULG_WALK_CLOCK");  // walk diagnostics (synchronising)
+    // Every layer unrolled (k <= 6) with the default variant: the whole call is
+    // one persistent launch (cbic_pipe.hip) instead of two launches per layer
+    // and phase.  The -r budget (checked between layers) and the diagnostic
+    // variants keep the layer launches.
+    const bool use_pipe = c->score_pipe && kmax <= kPipeMaxL && variant == 113 && c->time_limit_ms == 0 && !wck &&
+                          total_slots < (1ull << 32) && pipe_lds(n, nv, S).total <= 64 * 1024;
+    PipeArgs pargs{};
+    if (use_pipe) {
+        if ((rc = pipe_prepare(c, nv, S, kmax, max_parents, mv, meta, pargs))) return rc;
+        if (!c->pipe_stall_pinned) {
+            ULG_HIP(c, hipHostMalloc((void **)&c->pipe_stall_pinned, sizeof(unsigned int), hipHostMallocDefault));
+            *c->pipe_stall_pinned = 0;
+        }
+    }
     // Variables never read each other's slabs, so they are striped over G
     // groups on concurrent streams: a group's latency-bound walk kernels
     // overlap the other groups' scoring kernels.  Diagnostics run on one.
-    const int G = ((variant & 16) && !(variant & 8) && !wck) ? std::max(1, std::min(c->score_streams, nv)) : 1;
+    const int G = ((variant & 16) && !(variant & 8) && !wck && !use_pipe) ? std::max(1, std::min(c->score_streams, nv)) : 1;
     while ((int)c->aux_streams.size() < G - 1) {
         hipStream_t st;
         ULG_HIP(c, hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -3124,7 +2558,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
             }
     // queue counters per (group, layer, phase), then the wide walks' error flag
     const size_t nqc = (size_t)G * 2 * (kmax + 1) + 1;
-    if ((variant & 16) || kmax > kMaxL) {
+    if (((variant & 16) && !use_pipe) || kmax > kMaxL) {
         if ((rc = ensure(c, c->d_queue, (size_t)G * qwords)) || (rc = ensure(c, c->d_qcount, nqc)) ||
             (rc = ensure(c, c->d_wqueue, (size_t)G * wqwords)))
             return rc;
@@ -3230,7 +2664,11 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                      (uint64_t)(uintptr_t)c->out_sets.p, (uint64_t)(uintptr_t)c->out_scores.p,
                      (uint64_t)(uintptr_t)c->out_offsets.p, (uint64_t)(uintptr_t)c->d_blk.p,
                      (uint64_t)(uintptr_t)c->gram.p, (uint64_t)(uintptr_t)c->d_binom.p,
-                     (uint64_t)(uintptr_t)c->d_binom64.p, (uint64_t)(uintptr_t)c->d_hsub.p, (uint64_t)total_slots});
+                     (uint64_t)(uintptr_t)c->d_binom64.p, (uint64_t)(uintptr_t)c->d_hsub.p, (uint64_t)total_slots,
+                     (uint64_t)use_pipe, (uint64_t)c->pipe_rounds, (uint64_t)c->pipe_rounds_small,
+                     (uint64_t)c->score_small_layers, (uint64_t)c->pipe_occ, (uint64_t)(uintptr_t)c->d_pstate.p,
+                     (uint64_t)(uintptr_t)c->d_pqueue.p, (uint64_t)(uintptr_t)c->d_pstages.p,
+                     (uint64_t)(uintptr_t)c->d_pinit.p});
         for (int i = 0; i < nv; ++i) gkey.push_back((uint64_t)vars[i]);
         for (int i = 0; i < nv; ++i) gkey.push_back(candidates[i]);
         for (const std::string &nm : c->prof_only) gkey.push_back(std::hash<std::string>{}(nm));
@@ -3246,7 +2684,8 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     }
     {
     const size_t pend0 = c->pending.size();
-    for (int L = 1; L <= kmax; ++L) {
+    if (use_pipe && (rc = pipe_launch(c, pargs, c->stream))) return rc;
+    for (int L = 1; L <= kmax && !use_pipe; ++L) {
         for (int ph = 0; ph < 2; ++ph) {
             if (L <= Ls) {
                 const size_t wo = ((size_t)L * 2 + ph) * (nv + 1);
@@ -3478,6 +2917,8 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     }
     }
 launched:
+    if (use_pipe) ULG_HIP(c, hipMemcpyAsync(c->pipe_stall_pinned, pargs.done + 1, 4, hipMemcpyDeviceToHost, c->stream));
+    c->pipe_pending = use_pipe;
     if (async && kmax <= kMaxL) {
         // no host sync on this path: the stored count is copied into pinned
         // memory behind the launches and collected by ulg_cbic_score_finish
@@ -3502,6 +2943,10 @@ launched:
     if (kmax > kMaxL) ULG_HIP(c, hipMemcpyAsync(&wide_err, c->d_qcount.p + nqc - 1, 8, hipMemcpyDeviceToHost, c->stream));
     ULG_HIP(c, hipStreamSynchronize(c->stream));
     prof_collect(c);
+    if (c->pipe_pending) {
+        c->pipe_pending = false;
+        if ((rc = pipe_check(c))) return rc;
+    }
     if (wide_err)
         return set_err(c, ULG_ERR_UNSUPPORTED,
                        "ulg_cbic_score: a find_best_subset_score walk in a wide layer exceeded its cap (2^30 steps "

@@ -156,6 +156,8 @@ void ulg_destroy(ulg_ctx *c) {
     c->wide_pinned = nullptr;
     if (c->async_pinned) (void)hipHostFree(c->async_pinned);
     c->async_pinned = nullptr;
+    if (c->pipe_stall_pinned) (void)hipHostFree(c->pipe_stall_pinned);
+    c->pipe_stall_pinned = nullptr;
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
     c->event_pool.clear();
     for (hipStream_t s : c->aux_streams) (void)hipStreamDestroy(s);
@@ -165,6 +167,7 @@ void ulg_destroy(ulg_ctx *c) {
     release(c->raw); release(c->z); release(c->gram); release(c->partials); release(c->colstat);
     release(c->table); release(c->d_tbl_off); release(c->d_work); release(c->d_blk);
     release(c->d_cand); release(c->d_meta); release(c->d_binom); release(c->d_binom64); release(c->d_wqueue); release(c->d_wbits); release(c->d_stats); release(c->d_dump); release(c->d_queue); release(c->d_qcount); release(c->d_workg); release(c->d_vwork); release(c->d_hq); release(c->d_hqc); release(c->d_hmax); release(c->d_hoff); release(c->d_hmeta); release(c->d_scount); release(c->d_hsub);
+    release(c->d_pstate); release(c->d_pqueue); release(c->d_pstages); release(c->d_pinit);
     release(c->out_sets); release(c->out_scores); release(c->out_offsets);
     release(c->qbuf_in); release(c->qbuf_out);
     pss_release(c);
@@ -212,6 +215,26 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
     if (std::strcmp(name, "sweep_xcd") == 0) {
         if (value < 0 || value > 1) return set_err(c, ULG_ERR_ARG, "sweep_xcd must be 0 or 1");
         c->sweep_xcd = (int)value;
+        return ULG_OK;
+    }
+    if (std::strcmp(name, "score_pipe") == 0) {
+        if (value < 0 || value > 1) return set_err(c, ULG_ERR_ARG, "score_pipe must be 0 or 1");
+        c->score_pipe = (int)value;
+        return ULG_OK;
+    }
+    if (std::strcmp(name, "pipe_occ") == 0) {
+        if (value != 2 && value != 3) return set_err(c, ULG_ERR_ARG, "pipe_occ must be 2 or 3");
+        c->pipe_occ = (int)value;
+        return ULG_OK;
+    }
+    if (std::strcmp(name, "pipe_rounds") == 0) {
+        if (value < 1 || value > 64) return set_err(c, ULG_ERR_ARG, "pipe_rounds must be 1..64");
+        c->pipe_rounds = (int)value;
+        return ULG_OK;
+    }
+    if (std::strcmp(name, "pipe_rounds_small") == 0) {
+        if (value < 1 || value > 64) return set_err(c, ULG_ERR_ARG, "pipe_rounds_small must be 1..64");
+        c->pipe_rounds_small = (int)value;
         return ULG_OK;
     }
     if (std::strcmp(name, "score_graph") == 0) {
