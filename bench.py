@@ -100,6 +100,11 @@ PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", 
 PMC_TRAFFIC = os.path.join(os.path.dirname(PROFILES), "r3", "pmc_traffic.json")
 
 
+def step_sets_by_layer(cfg):
+    """{L: parent sets of L parents} over the variables of this step (cfg['msz'])."""
+    return {L: sum(math.comb(m, L) for m in cfg["msz"]) for L in range(0, cfg["k"] + 1)}
+
+
 def pmc_traffic(cfg, sets, label):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3
     PMC passes of the same config (scripts/pmc_round.sh + pmc_summarize.py);
@@ -114,12 +119,31 @@ def pmc_traffic(cfg, sets, label):
     return t["traffic_bytes_per_launch"], "profiles/r3/pmc_traffic.json"
 
 
-def roofline(ctx, cfg, per_layer_sets, steps):
-    """Dominant unit = the layer-k 'rest' launch (sets without variable 0): the
-    scoring kernel plus, with the two-pass scorer (score_variant bit 4), the
-    walk kernel over the sets it queued -- both are one layer's decision, so
-    their average durations are summed (rocprof lists them separately)."""
+ROOF_KERNELS = ["score_pipe", "score_layer_{k}_rest", "walk_{k}_rest"]
+
+
+def roofline(ctx, cfg, per_layer_sets, steps, step_sets=None, step_bytes=None):
+    """Dominant unit.  With the persistent pipeline (score_pipe) it is the one
+    launch that decides every set of the call: its algorithmic bytes are the
+    step's (4 (L + 1) per set of layer L) over its average launch
+    duration.  With the layer launches it is the layer-k 'rest' launch (sets
+    without variable 0): the scoring kernel plus, with the two-pass scorer
+    (score_variant bit 4), the walk kernel over the sets it queued -- both
+    are one layer's decision, so their average durations are summed (rocprof
+    lists them separately)."""
     k = cfg["k"]
+    pp = ctx.profile_get("score_pipe")
+    if pp is not None and step_bytes is not None:
+        traffic, traffic_src = pmc_traffic(cfg, step_sets, "score_pipe")
+        fl = sum(c * (2 * L ** 3 / 3 + 2 * L * L + 2 * L) for L, c in step_sets_by_layer(cfg).items())
+        return ({"bound": "hbm", "achieved": step_bytes / (pp["avg_ms"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                 "unit": "GB/s", "frac": step_bytes / (pp["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                 "traffic": traffic, "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
+                 "kernel": "score_pipe", "avg_launch_ms": pp["avg_ms"], "launches": pp["count"],
+                 "launches_per_step": 1, "sets_per_launch": step_sets,
+                 "algorithmic_bytes_per_launch": step_bytes,
+                 "bytes_per_set": "4 (L + 1) for a set of L parents (L direct-subset reads + 1 score write)",
+                 "fp64_tflops": fl / (pp["avg_ms"] * 1e-3) / 1e12}, pp)
     names = [f"score_layer_{k}_rest", f"walk_{k}_rest"]
     ps = [ctx.profile_get(nm) for nm in names]
     if ps[0] is None:
@@ -569,7 +593,7 @@ def main():
     # one extra profiled step after it
     kk = min(k, max(msz[v] for v in variables)) if variables else k
     ctx.profile(True)
-    ctx.profile_select([f"score_layer_{kk}_rest", f"walk_{kk}_rest"])
+    ctx.profile_select([r.format(k=kk) for r in ROOF_KERNELS])
     ctx.profile_reset()
     if dist:
         dist.barrier()
@@ -629,7 +653,7 @@ def main():
     # so the dominant kernel's time per call is below the call's own time.
     ctx.set_option("score_streams", 1)
     ctx.profile(True)
-    ctx.profile_select([f"score_layer_{kk}_rest", f"walk_{kk}_rest"])
+    ctx.profile_select([r.format(k=kk) for r in ROOF_KERNELS])
     ctx.profile_reset()
     solo_calls = 5
     ts_solo = []
@@ -638,7 +662,10 @@ def main():
         a = time.perf_counter()
         ctx.score(variables, cands, k)
         ts_solo.append(time.perf_counter() - a)
-    roof, _ = roofline(ctx, dict(cfg, k=kk), per_launch, solo_calls)
+    step_bytes = sum(math.comb(msz[v], L) * 4 * (L + 1) for v in variables for L in range(0, k + 1))
+    step_sets = sum(math.comb(msz[v], L) for v in variables for L in range(0, k + 1))
+    roof, _ = roofline(ctx, dict(cfg, k=kk, msz=[msz[v] for v in variables]), per_launch, solo_calls, step_sets,
+                       step_bytes)
     ctx.profile(False)
     if roof is not None:
         roof["note"] = ("one call at a time on one stream (context 0 after the timed region, %d calls): the "
@@ -661,7 +688,6 @@ def main():
     if roof is not None:
         # the same compulsory bytes (4 (L + 1) per set) over the whole step:
         # every layer of every variable of this rank, per ms_per_step
-        step_bytes = sum(math.comb(msz[v], L) * 4 * (L + 1) for v in variables for L in range(0, k + 1))
         roof["step_level"] = {"algorithmic_bytes_per_step": step_bytes,
                               "achieved_gbs": step_bytes / (elapsed / args.steps) / 1e9,
                               "frac": step_bytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS,

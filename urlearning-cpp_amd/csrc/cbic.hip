@@ -139,74 +139,6 @@ __global__ void __launch_bounds__(kBlock) gram_reduce_kernel(const double *parti
 }
 
 
-// Same recursion as an explicit stack machine: one loop iteration advances
-// one step of this lane's own traversal, so a wave costs the max over its
-// lanes' step counts instead of the union of their recursion trees (the
-// nested form above executes a level's loops whenever ANY lane recurses).
-// Saved frames live in LDS, one u64 per frame, lane-interleaved
-// (stk[slot * kBlock + tid]): T | idx << 10 | j << 14 | pv << 18; the loop
-// position i and the partial vector npv are re-derived from (pv, u, j).
-template <int L, class BS>
-__device__ __forceinline__ void best_subset_stack(uint32_t Ptop, uint32_t pvtop, const BS &present, BS &checked,
-                                                  BS &visited, uint64_t *stk) {
-    const int tid = threadIdx.x;
-    uint32_t T = Ptop, pv = pvtop, npv = 0, u = 0;
-    int sp = 0, m = L, idx = 0, i = 0, j = 0;
-    bool inner = false;
-    while (true) {
-        if (!inner) {
-            if (idx == m) {  // fb returns
-                if (sp == 0) break;
-                const uint32_t childT = T;
-                --sp;
-                const uint64_t F = stk[sp * 256 + tid];
-                T = (uint32_t)(F & 1023u);
-                idx = (int)((F >> 10) & 15u);
-                j = (int)((F >> 14) & 15u);
-                pv = (uint32_t)(F >> 18);
-                u = (pv >> (4 * idx)) & 15u;
-                npv = 0;
-                i = 0;
-                for (int jj = 0; jj < j;) {
-                    const uint32_t pi = (pv >> (4 * i)) & 15u;
-                    ++i;
-                    if (pi == u) continue;
-                    npv |= pi << (4 * jj);
-                    ++jj;
-                }
-                m = L - sp;
-                inner = true;
-                checked.set(childT);  // checked.insert(thin_parents) after each recursive call
-                continue;
-            }
-            u = (pv >> (4 * idx)) & 15u;
-            const uint32_t T2 = T ^ (1u << u);
-            if (checked.test(T2)) { ++idx; continue; }
-            if (present.test(T2)) { visited.set(T2); ++idx; continue; }
-            inner = true;
-            i = 0;
-            j = 0;
-            npv = 0;
-        } else {
-            if (i == m) { inner = false; ++idx; continue; }
-            const uint32_t pi = (pv >> (4 * i)) & 15u;
-            ++i;
-            if (pi == u) continue;
-            npv |= pi << (4 * j);
-            ++j;
-            // recurse into fb(T ^ u, npv, m - 1)
-            stk[sp * 256 + tid] = (uint64_t)T | ((uint64_t)idx << 10) | ((uint64_t)j << 14) | ((uint64_t)pv << 18);
-            ++sp;
-            T = T ^ (1u << u);
-            pv = npv;
-            m = L - sp;
-            idx = 0;
-            inner = false;
-        }
-    }
-}
-
-
 struct ScoreArgs {
     const double *gram;      // n x n row-major
     const uint32_t *binom;   // [64][kBinomK]
@@ -217,9 +149,6 @@ struct ScoreArgs {
     float *table;
     float *hsub;                // variant bit 6: per slot, the maximum stored value over the set's
                                 // nonempty subsets (the set included; NaN = none), table layout
-    unsigned long long *stats;  // variant bit 3: per-launch decision statistics
-    uint64_t *dump;             // variant bit 3: presence words of the walking lanes
-    uint64_t dump_cap;
     uint64_t *queue;            // variant bit 4: lanes left for walk_kernel
     unsigned long long *qcount;
     double N;
@@ -256,7 +185,7 @@ __host__ __device__ inline LdsLayout lds_layout(int n, int nv, int S, int L, int
     l.work = align16(l.binom + 64 * kBinomK * 4);
     l.toff = align16(l.work + (nv + 1) * 8);
     l.stack = align16(l.toff + (nv * S + 1) * 8);
-    l.bits = align16(l.stack + ((V & 2) && !(V & 4) ? L * kBlock * 8 : 0));
+    l.bits = l.stack;
     const int W = bits_words(L);
     l.cmp = align16(l.bits + (W >= 4 ? 3 * W * kBlock * 8 : 0));
     l.total = l.cmp + ((V & 80) == 80 ? 16 + kBlock * kCmpEntryBytes : 0);
@@ -308,7 +237,6 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
     uint32_t *binom = reinterpret_cast<uint32_t *>(smem + lay.binom);
     uint64_t *work = reinterpret_cast<uint64_t *>(smem + lay.work);
     uint64_t *toff = reinterpret_cast<uint64_t *>(smem + lay.toff);
-    uint64_t *stk = reinterpret_cast<uint64_t *>(smem + lay.stack);
     for (int i = threadIdx.x; i < a.n * a.n; i += kBlock) g[i] = a.gram[i];
     for (int i = threadIdx.x; i < 64 * kBinomK; i += kBlock) binom[i] = a.binom[i];
     for (int i = threadIdx.x; i <= a.nv; i += kBlock) work[i] = a.work[i];
@@ -445,8 +373,6 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
 
     float out;
     bool queued = false;  // variant bit 4: left for walk_kernel
-    int cat = 1;          // variant bit 3 statistics: 1 ts >= 0, 2 no key >= -ts,
-    uint32_t steps = 0;   // 3 direct child >= -ts, 4 walk -> dominated, 5 walk -> stored
     if (ts >= 0.0f) {
         // returned -ts; the caller stores it iff it is < 0 (score_calculator.cpp:111)
         const float s = -ts;
@@ -459,7 +385,6 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         const uint64_t cpack = ls.cpack;
         const uint32_t Plocal = ls.Plocal;
         const uint32_t pvtop = ls.pvtop;
-        const bool v0inP = ls.v0inP;
         const uint64_t vbase = (uint64_t)vi * a.S;
 
         // presence of every candidate key in the cache as it stands now
@@ -468,7 +393,7 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         BS present = make_bits<BS>(lds_bits);
         BS hi = make_bits<BS>(lds_bits + (size_t)W * kBlock);
         present.clear();
-        if constexpr ((V & 20) != 0) hi.clear();
+        if constexpr ((V & 16) != 0) hi.clear();
         const float thr = -ts;
         gather_keys<L, PHASE, V>(present, hi, ls, thr, binom, z, a.table, toff + vbase);
 
@@ -477,45 +402,13 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
             const bool dom = settle_rules<L, PHASE>(present, hi, ls, queued);
             if (queued) queue_walk(present, hi, a.queue, a.qcount, toff[vbase + L] + rankP, ts);
             out = dom ? absent_f() : -ts;
-        } else if constexpr ((V & 4) != 0) {
-            // decision-only walk: no key >= -ts at all -> stored; a direct
-            // child >= -ts (always visited at the top level) -> not stored;
-            // otherwise walk until the first visited key >= -ts
-            bool any = false;
-#pragma unroll
-            for (int wj = 0; wj < W; ++wj) any |= hi.word(wj) != 0ull;
-            bool dom = false;
-            cat = 2;
-            if (any) {
-                cat = 3;
-#pragma unroll
-                for (int i = 0; i < L; ++i) dom |= hi.test(Plocal ^ (1u << ((pvtop >> (4 * i)) & 15u)));
-                if (!dom) {
-                    BS checked = make_bits<BS>(lds_bits + (size_t)2 * W * kBlock);
-                    checked.clear();
-                    checked.set(0u);
-                    dom = dominated<L, BS>(Plocal, pvtop, present, hi, checked, steps);
-                    cat = dom ? 4 : 5;
-                    if constexpr ((V & 8) != 0) {
-                        const uint64_t di = atomicAdd(&a.stats[9], 1ull);
-                        if (di < a.dump_cap) {
-                            for (int wj = 0; wj < W; ++wj) a.dump[di * (2 * W + 1) + wj] = present.word(wj);
-                            for (int wj = 0; wj < W; ++wj) a.dump[di * (2 * W + 1) + W + wj] = hi.word(wj);
-                            a.dump[di * (2 * W + 1) + 2 * W] = (uint64_t)dom | ((uint64_t)v0inP << 1) |
-                                                               ((uint64_t)steps << 8);
-                        }
-                    }
-                }
-            }
-            out = dom ? absent_f() : -ts;
         } else {
         BS checked = make_bits<BS>(lds_bits + (size_t)W * kBlock);
         BS visited = make_bits<BS>(lds_bits + (size_t)2 * W * kBlock);
         checked.clear();
         visited.clear();
         checked.set(0u);  // checked.insert(empty_set)
-        if constexpr ((V & 2) != 0) best_subset_stack<L, BS>(Plocal, pvtop, present, checked, visited, stk);
-        else best_subset<L, BS>(Plocal, pvtop, present, checked, visited);
+        best_subset<L, BS>(Plocal, pvtop, present, checked, visited);
 
         float best = 0.0f;
 #pragma unroll
@@ -553,26 +446,6 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
             for (int i = 0; i < L; ++i) hch = fmaxf(hch, a.hsub[toff[vbase + L - 1] + rc[i]]);
         }
         a.hsub[toff[vbase + L] + rankP] = fmaxf(out, hch);
-    }
-    if constexpr ((V & 8) != 0) {
-        // per wave: lanes per category, waves with any walking lane, walk
-        // steps summed over lanes and the wave's max (what the wave pays)
-        const int lane = threadIdx.x & 63;
-        uint32_t mx = steps;
-        for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-        uint32_t sum = steps;
-        for (int o = 32; o > 0; o >>= 1) sum += (uint32_t)__shfl_xor((int)sum, o);
-        const unsigned long long walkers = __ballot(cat >= 4);
-        for (int k = 1; k <= 5; ++k) {
-            const unsigned long long b = __ballot(cat == k);
-            if (lane == 0 && b) atomicAdd(&a.stats[k], (unsigned long long)__popcll(b));
-        }
-        if (lane == 0) {
-            atomicAdd(&a.stats[0], 1ull);
-            if (walkers) atomicAdd(&a.stats[6], 1ull);
-            atomicAdd(&a.stats[7], (unsigned long long)sum);
-            atomicAdd(&a.stats[8], (unsigned long long)mx);
-        }
     }
 }
 
@@ -1730,21 +1603,18 @@ template <int L, int V>
 KernelFn pick_phase(int phase) {
     return phase == 0 ? score_layer_kernel<L, 0, V> : score_layer_kernel<L, 1, V>;
 }
-// variants: bit 0 unrolled presence, bit 1 stack recursion, bit 2 decision-only
-// walk (takes precedence over bit 1).  An XCD-aware block order (each XCD a
-// contiguous eighth of the work, so a few variables' slabs per 4 MB L2) was
-// measured slower at C3 (3.20 vs 2.99 ms for layer 6) and is not kept.
+// variants (ulg_set_option "score_variant"): bit 0 unrolled presence gathers
+// (layers <= 6), bit 4 two-pass (settle, queue the rest for a walk launch),
+// bit 5 bit-sliced walk, bit 6 subset maxima.  1: one-pass; 65: one-pass with
+// the subset maxima (the small layers of 113); 17 / 49: two-pass with the
+// per-lane / bit-sliced walk; 81 / 113: the same with the subset maxima (113
+// is the default).  Round 1's other forms (loop gathers at every layer, a
+// stack-machine recursion, a decision-only per-lane walk, the statistics
+// build) were measured slower and are gone.
 template <int L>
 KernelFn pick(int phase, int variant) {
     switch (variant) {
-        case 0: return pick_phase<L, 0>(phase);
         case 1: return pick_phase<L, 1>(phase);
-        case 2: return pick_phase<L, 2>(phase);
-        case 3: return pick_phase<L, 3>(phase);
-        case 4: case 6: return pick_phase<L, 4>(phase);
-        case 5: case 7: return pick_phase<L, 5>(phase);
-        case 13: return pick_phase<L, 13>(phase);
-        case 16: case 48: return pick_phase<L, 16>(phase);
         case 17: case 49: return pick_phase<L, 17>(phase);
         case 65: return pick_phase<L, 65>(phase);
         case 81: case 113: return pick_phase<L, 81>(phase);
@@ -2477,9 +2347,6 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     sa.tbl_off = c->d_tbl_off.p;
     sa.table = c->table.p;
     sa.hsub = nullptr;
-    sa.stats = nullptr;
-    sa.dump = nullptr;
-    sa.dump_cap = 0;
     sa.queue = nullptr;
     sa.qcount = nullptr;
     sa.N = (double)c->N;
@@ -2513,7 +2380,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     // Variables never read each other's slabs, so they are striped over G
     // groups on concurrent streams: a group's latency-bound walk kernels
     // overlap the other groups' scoring kernels.  Diagnostics run on one.
-    const int G = ((variant & 16) && !(variant & 8) && !wck && !use_pipe) ? std::max(1, std::min(c->score_streams, nv)) : 1;
+    const int G = ((variant & 16) && !wck && !use_pipe) ? std::max(1, std::min(c->score_streams, nv)) : 1;
     while ((int)c->aux_streams.size() < G - 1) {
         hipStream_t st;
         ULG_HIP(c, hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -2604,7 +2471,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     // Small layers (L <= Ls, little work, latency-bound): one one-pass launch
     // per phase over all variables on the context stream -- no queue, no walk
     // launch, no stream groups.  The rest: per group, score + queued walk.
-    const int Ls = (variant & 16) && !(variant & 8) && !wck ? std::min(kmax, std::min(kMaxL, c->score_small_layers)) : 0;
+    const int Ls = (variant & 16) && !wck ? std::min(kmax, std::min(kMaxL, c->score_small_layers)) : 0;
     const int vsmall = variant & 65;  // the one-pass form (keeping the subset maxima under bit 6)
     bool forked = false;
     // The wide layers variable by variable (wide_pool 1) pay when the
@@ -2637,7 +2504,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     // events, the profiling events) and replayed, which removes the host
     // launch path of ~40 kernels per call (score_graph, default on).
     const bool use_graph =
-        c->score_graph && !c->prof && kmax <= kMaxL && c->time_limit_ms == 0 && !wck && !(variant & 8);
+        c->score_graph && !c->prof && kmax <= kMaxL && c->time_limit_ms == 0 && !wck;
     std::vector<uint64_t> gkey;
     // An early return between BeginCapture and EndCapture (a failed launch,
     // "layer too large") must not leave the context stream capturing: the
@@ -2756,14 +2623,6 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                 const KernelFn kfn = layer_kernel(L, ph, variant);
                 if (lay.total > 64 * 1024)
                     ULG_HIP(c, hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, lay.total));
-                if (variant & 8) {
-                    if ((rc = ensure(c, c->d_stats, 16))) return rc;
-                    ULG_HIP(c, hipMemsetAsync(c->d_stats.p, 0, 16 * 8, st));
-                    sa.stats = c->d_stats.p;
-                    sa.dump_cap = 4u << 20;
-                    if ((rc = ensure(c, c->d_dump, (size_t)sa.dump_cap * (2 * bits_words(L) + 1)))) return rc;
-                    sa.dump = c->d_dump.p;
-                }
                 prof_begin_s(c, kLayerNames[ph][L], st);
                 hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(kBlock), (size_t)lay.total, st, sa);
                 prof_end_s(c, st);
@@ -2817,27 +2676,6 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                                 std::fwrite(hw.data(), 8, hw.size(), f);
                                 std::fclose(f);
                             }
-                        }
-                    }
-                }
-                if (variant & 8) {
-                    unsigned long long stt[16];
-                    ULG_HIP(c, hipMemcpyAsync(stt, c->d_stats.p, sizeof stt, hipMemcpyDeviceToHost, st));
-                    ULG_HIP(c, hipStreamSynchronize(st));
-                    std::fprintf(stderr,
-                                 "score_stats L=%d phase=%d waves=%llu lanes: ts>=0 %llu, no-hi %llu, direct-hi %llu, "
-                                 "walk-dom %llu, walk-stored %llu; walking waves %llu; steps lane-sum %llu wave-max-sum %llu\n",
-                                 L, ph, stt[0], stt[1], stt[2], stt[3], stt[4], stt[5], stt[6], stt[7], stt[8]);
-                    if (const char *dd = std::getenv("ULG_DUMP_DIR")) {
-                        const uint64_t cntd = std::min<uint64_t>(stt[9], sa.dump_cap);
-                        std::vector<uint64_t> hd((size_t)cntd * (2 * bits_words(L) + 1));
-                        ULG_HIP(c, hipMemcpyAsync(hd.data(), c->d_dump.p, hd.size() * 8, hipMemcpyDeviceToHost, st));
-                        ULG_HIP(c, hipStreamSynchronize(st));
-                        char fn[512];
-                        std::snprintf(fn, sizeof fn, "%s/walk_L%d_p%d.bin", dd, L, ph);
-                        if (FILE *f = std::fopen(fn, "wb")) {
-                            std::fwrite(hd.data(), 8, hd.size(), f);
-                            std::fclose(f);
                         }
                     }
                 }
