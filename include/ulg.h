@@ -281,18 +281,24 @@ int ulg_sweep_shard_end(ulg_ctx *ctx, uint64_t *vpar, int *order, float *goal_co
                         int64_t *expanded);
 
 /* ---- tuning knobs -------------------------------------------------------
- * "score_variant" (0..7, 13, 16, 17, 48, 49, 81, 113; default 113): bit 0 =
- * fully unrolled presence gather in the scorer (layers <= 6), bit 1 =
- * stack-machine dominance recursion, bit 2 = decision-only walk (stops at the
- * first visited key >= -ts), bit 4 = two-pass layers: the scoring kernel
- * settles every set it can without a walk and queues the rest for a dense
- * walk kernel with the hi-cover prune (overrides bits 1-2), bit 5 = that walk
- * bit-sliced (64 x K sets per wave), bit 6 (with bits 0 and 4) = subset
- * maxima: a per-slot table of the largest stored value below each set settles
- * sets with 2L-3L reads before the block compacts the rest for the
- * 2^(L+1) presence gathers.  All variants store identical lists.  13 = bit 2 plus
- * per-launch decision statistics on stderr (and, with ULG_DUMP_DIR set, the
- * walking lanes' presence words); diagnostics only, it synchronises.
+ * "score_variant" (1, 17, 49, 65, 81, 113; default 113): bit 0 = fully
+ * unrolled presence gather (layers <= 6), bit 4 = two-pass layers (the
+ * scoring kernel settles every set it can without a walk and queues the rest
+ * for a dense walk kernel with the hi-cover prune), bit 5 = that walk
+ * bit-sliced (64 x K sets per wave), bit 6 = subset maxima (a per-slot table
+ * of the largest stored value below each set settles sets with 2L-3L reads
+ * before the rest are compacted for the 2^(L+1) presence gathers).  1 and 65
+ * are one-pass (every set decided in its lane).  All variants store
+ * identical lists.
+ * "score_pipe" (0/1, default 0): every layer unrolled (k <= 6) and variant
+ * 113: the whole call is one persistent launch (cbic_pipe.hip) whose waves
+ * claim score tiles and walk chunks from per-(variable, stage) device
+ * counters, a variable's next stage released as soon as its previous one is
+ * decided; "pipe_rounds" (1..64, default 2; at most 2 take effect): 64-set
+ * rounds per two-pass tile; "pipe_rounds_small" (1..64, default 1): per
+ * one-pass tile; "pipe_occ" (2/3, default 2): waves per SIMD the kernel is
+ * compiled for (3 spills a few registers).  A call with a time limit uses the
+ * layer launches.
  * "table_budget_kb" (KiB; default 0 = half the free HBM): memory for the dense
  * best-score tables (16 B per entry incl. the host cost copy).  Lists whose
  * tables over all variables exceed it (e.g. n = 32 with a full skeleton) are
@@ -317,12 +323,6 @@ int ulg_sweep_shard_end(ulg_ctx *ctx, uint64_t *vpar, int *order, float *goal_co
  * cached until the tables change) when that fits the free HBM; 0 reads the
  * binary-indexed lattice per predecessor instead; 2 uses the slices with
  * 64-bit index arithmetic (1 = 32-bit).
- * "exact_settled" (0/1, default 0): the exact-order A* (ULG_ASTAR_EXACT,
- * dense form, no ancestors) first computes on the GPU every node's smallest
- * reachable g (the same float sums, minimised over all predecessors) and
- * which in-edges attain it; a node whose g reaches that value can never be
- * improved (strict <), so later visits of it skip its record.  Same pops,
- * DAG and expansion count (C3: 47 % of the visits skipped, but no faster).
  * "wide_prune" (0/1, default 1): the wide-layer walks skip absent nodes
  * below which no present key reaches -ts (hi-cover tables per variable);
  * "wide_reduced" (0/1, default 1): they skip the recursion's re-tests that
@@ -330,15 +330,21 @@ int ulg_sweep_shard_end(ulg_ctx *ctx, uint64_t *vpar, int *order, float *goal_co
  * "wide_lds" (0/1/2, default 1): walks longer than 2^6 steps are replayed by
  * one workgroup each with their skip / hi bitsets in LDS (2^q <= 2^20 local
  * subsets; the hi bitset in HBM above 2^19); 2 replays every walk that way.
- * "wide_pool" (0/1, default 1): with score_streams > 1 the wide layers run
+ * "wide_pool" (0/1/2, default 2): with score_streams > 1 the wide layers run
  * variable by variable on score_streams host threads, largest candidate set
  * first (0: every group's part of a layer together, the slowest group
- * holding the next layer).
- * "wide_host" (iterations, default 4096, 0 = never): an LDS replay still
+ * holding the next layer; 1: always by variable; 2: by variable when the
+ * wide variables' candidate counts span at least 2).
+ * "wide_host" (iterations, default 1024, 0 = never): an LDS replay still
  * walking after that many iterations stops and is replayed from the start on
  * a host thread over the same bitsets (one wave issues at most one
  * instruction every 4 cycles; a host core runs the same sequential walk tens
- * of times faster).
+ * of times faster); "wide_host_max" (default 4096): only launches of at
+ * most this many LDS replays hand over; "wide_host_first" (default 0): launches
+ * of at most this many replays go to the host whole, without the LDS phase;
+ * "wide_host_q" (0..32, default 0 = off): ... as do launches of at most 128
+ * replays whose local bits q reach this; "wide_host_threads" (1..64,
+ * default 16): host threads for those replays.
  * All variants compute identical results; the knob exists for A/B timing. */
 int ulg_set_option(ulg_ctx *ctx, const char *name, int64_t value);
 /* Read-back of per-call state: "out_of_time" (1 if the last ulg_cbic_score,

@@ -2757,7 +2757,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
 launched:
     if (use_pipe) ULG_HIP(c, hipMemcpyAsync(c->pipe_stall_pinned, pargs.done + 1, 4, hipMemcpyDeviceToHost, c->stream));
     c->pipe_pending = use_pipe;
-    if (async && kmax <= kMaxL) {
+    if (async && kmax <= kMaxL && c->time_limit_ms == 0) {
         // no host sync on this path: the stored count is copied into pinned
         // memory behind the launches and collected by ulg_cbic_score_finish
         if (!c->async_pinned)

@@ -184,10 +184,8 @@ class ListExchange:
                     # low 32 bits of each set (little endian), on the device
                     lo = self.stage.view(torch.int32).view(-1, 2)[:, 0]
                     self.buf[self.hdr:self.hdr + 4 * self.cap].view(torch.int32).copy_(lo)
-            else:  # header only: the offsets, through buffers that hold the lists
-                tmp_sets = torch.empty(max(stored, 1), dtype=torch.int64, device=self.device)
-                tmp_scores = torch.empty(max(stored, 1), dtype=torch.float32, device=self.device)
-                ctx.fetch_device(tmp_sets.data_ptr(), tmp_scores.data_ptr(), self.offs_ptr)
+            else:  # header only: just the offsets (null sets / scores pointers skip those copies)
+                ctx.fetch_device(0, 0, self.offs_ptr)
             return
         offsets, sets, scores = a
         cnt = int(offsets[-1])
