@@ -50,6 +50,7 @@ struct PipeArgs {
     int Ls;       // layers <= Ls: one-pass tiles
     int R;        // rounds (x 64 sets) per two-pass tile
     int Rsmall;   // rounds per one-pass tile
+    int chain;    // the wave that releases a stage starts on it (pipe_chain)
     uint64_t timeout;  // wall-clock ticks a wave may stay idle before the call fails
 };
 

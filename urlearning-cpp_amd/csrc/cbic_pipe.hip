@@ -93,20 +93,27 @@ __device__ __forceinline__ void publish_next(const PipeArgs &a, int vi, int s) {
 }
 
 // this wave's stores are drained; add `delta` to the stage counter and, if
-// that completes the stage, release the variable's next stage
-__device__ __forceinline__ void stage_add(const PipeArgs &a, int vi, int s, uint64_t delta, int lane) {
+// that completes the stage, release the variable's next stage.  Returns
+// (wave-uniform) the stage this wave released, or -1.
+__device__ __forceinline__ int stage_add(const PipeArgs &a, int vi, int s, uint64_t delta, int lane) {
     drain();
+    int released = -1;
     if (lane == 0) {
         PipeCtr *ct = a.ctr + vi * a.NS + s;
         const uint64_t old = __hip_atomic_fetch_add((gu64 *)&ct->units, delta, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT);
-        if (old + delta == ((uint64_t)a.stages[vi * a.NS + s].ntiles << 32)) publish_next(a, vi, s);
+        if (old + delta == ((uint64_t)a.stages[vi * a.NS + s].ntiles << 32)) {
+            publish_next(a, vi, s);
+            const uint32_t nx = a.stages[vi * a.NS + s].next;
+            released = nx == kDone ? -1 : (int)nx;
+        }
     }
+    return __builtin_amdgcn_readfirstlane(released);
 }
 
 // ---- one-pass tile (layers <= Ls): every set decided in its lane -----------
 template <int L, int PH>
-__device__ __forceinline__ void tile_onepass(const PipeArgs &a, const PipeShared &sh, int vi, int s, uint32_t tile, int lane) {
+__device__ __forceinline__ int tile_onepass(const PipeArgs &a, const PipeShared &sh, int vi, int s, uint32_t tile, int lane) {
     const PipeStage &st = a.stages[vi * a.NS + s];
     const int v = sh.meta[vi * 4 + 0], m = sh.meta[vi * 4 + 1];
     const bool z = sh.meta[vi * 4 + 2] != 0;
@@ -182,7 +189,7 @@ __device__ __forceinline__ void tile_onepass(const PipeArgs &a, const PipeShared
         }
         stf(a.hsub + slot, fmaxf(out, hch));
     }
-    stage_add(a, vi, s, 1ull << 32, lane);
+    return stage_add(a, vi, s, 1ull << 32, lane);
 }
 
 // ---- two-pass tile (layers > Ls) --------------------------------------------
@@ -273,7 +280,7 @@ __device__ __forceinline__ void pool_drain(const PipeArgs &a, const PipeShared &
 }
 
 template <int L, int PH>
-__device__ __forceinline__ void tile_twopass(const PipeArgs &a, const PipeShared &sh, int vi, int s, uint32_t tile, int lane,
+__device__ __forceinline__ int tile_twopass(const PipeArgs &a, const PipeShared &sh, int vi, int s, uint32_t tile, int lane,
                              WavePool &P) {
     const PipeStage &st = a.stages[vi * a.NS + s];
     const int v = sh.meta[vi * 4 + 0], m = sh.meta[vi * 4 + 1];
@@ -360,12 +367,12 @@ __device__ __forceinline__ void tile_twopass(const PipeArgs &a, const PipeShared
     for (int off = 0; off < cnt; off += 64)
         pool_drain<L, PH>(a, sh, vi, s, P, off, cnt - off < 64 ? cnt - off : 64, lane, queued, hsub_on);
 
-    stage_add(a, vi, s, (1ull << 32) - (uint64_t)queued, lane);
+    return stage_add(a, vi, s, (1ull << 32) - (uint64_t)queued, lane);
 }
 
 // ---- walk chunk ----------------------------------------------------------------
 template <int L, int PH>
-__device__ __forceinline__ void walk_chunk(const PipeArgs &a, int vi, int s, uint32_t c, int lane) {
+__device__ __forceinline__ int walk_chunk(const PipeArgs &a, int vi, int s, uint32_t c, int lane) {
     constexpr int K = pipe_k(L);
     using SL = Sliced<L, K>;
     constexpr int W = bits_words(L);
@@ -432,7 +439,7 @@ __device__ __forceinline__ void walk_chunk(const PipeArgs &a, int vi, int s, uin
         stf(a.table + slot, d ? absent_f() : -ts);
         if (hsub_on) stf(a.hsub + slot, d ? hch : fmaxf(hch, -ts));
     }
-    stage_add(a, vi, s, (uint64_t)e, lane);
+    return stage_add(a, vi, s, (uint64_t)e, lane);
 }
 
 // ---- scheduling ------------------------------------------------------------------
@@ -523,25 +530,38 @@ __device__ __forceinline__ Item find_work(const PipeArgs &a, int rot, int lane, 
 }
 
 template <int L>
-__device__ __forceinline__ void run_item(const PipeArgs &a, const PipeShared &sh, const Item &it, int lane, WavePool &P) {
+__device__ __forceinline__ int run_item(const PipeArgs &a, const PipeShared &sh, const Item &it, int lane, WavePool &P) {
     const int ph = it.s & 1;
     if (it.kind == 2) {
         if constexpr (L >= 2) {
-            if (ph == 0) walk_chunk<L, 0>(a, it.vi, it.s, it.idx, lane);
-            else walk_chunk<L, 1>(a, it.vi, it.s, it.idx, lane);
+            if (ph == 0) return walk_chunk<L, 0>(a, it.vi, it.s, it.idx, lane);
+            return walk_chunk<L, 1>(a, it.vi, it.s, it.idx, lane);
         }
-        return;
+        return -1;
     }
     if (L <= a.Ls) {
         if constexpr (L <= kPipeMaxSmall) {
-            if (ph == 0) tile_onepass<L, 0>(a, sh, it.vi, it.s, it.idx, lane);
-            else tile_onepass<L, 1>(a, sh, it.vi, it.s, it.idx, lane);
+            if (ph == 0) return tile_onepass<L, 0>(a, sh, it.vi, it.s, it.idx, lane);
+            return tile_onepass<L, 1>(a, sh, it.vi, it.s, it.idx, lane);
         }
     } else {
         if constexpr (L >= 2) {
-            if (ph == 0) tile_twopass<L, 0>(a, sh, it.vi, it.s, it.idx, lane, P);
-            else tile_twopass<L, 1>(a, sh, it.vi, it.s, it.idx, lane, P);
+            if (ph == 0) return tile_twopass<L, 0>(a, sh, it.vi, it.s, it.idx, lane, P);
+            return tile_twopass<L, 1>(a, sh, it.vi, it.s, it.idx, lane, P);
         }
+    }
+    return -1;
+}
+
+__device__ __forceinline__ int run_any(const PipeArgs &a, const PipeShared &sh, const Item &it, int lane, WavePool &P) {
+    switch (it.s / 2 + 1) {
+        case 1: return run_item<1>(a, sh, it, lane, P);
+        case 2: return run_item<2>(a, sh, it, lane, P);
+        case 3: return run_item<3>(a, sh, it, lane, P);
+        case 4: return run_item<4>(a, sh, it, lane, P);
+        case 5: return run_item<5>(a, sh, it, lane, P);
+        case 6: return run_item<6>(a, sh, it, lane, P);
+        default: return -1;
     }
 }
 
@@ -587,14 +607,19 @@ __global__ void __launch_bounds__(kBlock, OCC) pipe_kernel(PipeArgs a) {
         it.idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)it.idx);
         if (it.kind > 0) {
             idle_since = 0;
-            switch (it.s / 2 + 1) {
-                case 1: run_item<1>(a, sh, it, lane, P); break;
-                case 2: run_item<2>(a, sh, it, lane, P); break;
-                case 3: run_item<3>(a, sh, it, lane, P); break;
-                case 4: run_item<4>(a, sh, it, lane, P); break;
-                case 5: run_item<5>(a, sh, it, lane, P); break;
-                case 6: run_item<6>(a, sh, it, lane, P); break;
-                default: break;
+            int nxt = run_any(a, sh, it, lane, P);
+            // The wave that released a variable's next stage starts on it
+            // at once (the chain's critical path, and its slabs are warm in
+            // this XCD's L2); other waves join through find_work.
+            while (nxt >= 0 && a.chain) {
+                uint32_t t = 0;
+                if (lane == 0)
+                    t = __hip_atomic_fetch_add((gu32 *)&a.ctr[it.vi * a.NS + nxt].claim, 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+                if (t >= a.stages[it.vi * a.NS + nxt].ntiles) break;
+                const Item nx{1, it.vi, nxt, t};
+                nxt = run_any(a, sh, nx, lane, P);
             }
             continue;
         }
@@ -692,6 +717,7 @@ int pipe_prepare(ulg_ctx *c, int nv, int S, int kmax, int max_parents, const std
     a.Ls = Ls;
     a.R = R;
     a.Rsmall = Rs;
+    a.chain = c->pipe_chain;
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0) khz = 100000;
     a.timeout = (uint64_t)khz * 1000ull * 10ull;  // 10 s idle

@@ -226,6 +226,11 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         c->pipe_occ = (int)value;
         return ULG_OK;
     }
+    if (std::strcmp(name, "pipe_chain") == 0) {
+        if (value < 0 || value > 1) return set_err(c, ULG_ERR_ARG, "pipe_chain must be 0 or 1");
+        c->pipe_chain = (int)value;
+        return ULG_OK;
+    }
     if (std::strcmp(name, "pipe_rounds") == 0) {
         if (value < 1 || value > 64) return set_err(c, ULG_ERR_ARG, "pipe_rounds must be 1..64");
         c->pipe_rounds = (int)value;

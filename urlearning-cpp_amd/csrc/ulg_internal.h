@@ -149,6 +149,7 @@ struct ulg_ctx {
     int score_pipe = 0;            // layers <= 6: one persistent launch with a device work queue
     int pipe_rounds = 2;           // 64-set rounds per two-pass score tile
     int pipe_rounds_small = 1;     // ... per one-pass tile
+    int pipe_chain = 1;            // the wave that releases a stage starts on it
     int pipe_occ = 2;              // waves per SIMD the pipeline kernel is compiled for (2 or 3)
     int pipe_cus = 0;              // compute units of the device (queried once)
     int pipe_nv = 0;
