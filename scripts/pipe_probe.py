@@ -50,7 +50,10 @@ def main():
     ap.add_argument("--cases", nargs="+", default=["small", "c2", "c3", "c5"])
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--options", default="")
+    ap.add_argument("--lib", default=None, help="another build of libulg.so (timing experiments)")
     a = ap.parse_args()
+    if a.lib:
+        ulg.LIB_PATH = os.path.abspath(a.lib)
     ctx = ulg.Context(0)
     for kv in filter(None, a.options.split(",")):
         k_, v_ = kv.split("=")

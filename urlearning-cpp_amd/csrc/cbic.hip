@@ -2504,7 +2504,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     // events, the profiling events) and replayed, which removes the host
     // launch path of ~40 kernels per call (score_graph, default on).
     const bool use_graph =
-        c->score_graph && !c->prof && kmax <= kMaxL && c->time_limit_ms == 0 && !wck;
+        c->score_graph && !c->prof && kmax <= kMaxL && c->time_limit_ms == 0 && !wck && !std::getenv("ULG_PIPE_STATS");
     std::vector<uint64_t> gkey;
     // An early return between BeginCapture and EndCapture (a failed launch,
     // "layer too large") must not leave the context stream capturing: the
@@ -2533,7 +2533,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                      (uint64_t)(uintptr_t)c->gram.p, (uint64_t)(uintptr_t)c->d_binom.p,
                      (uint64_t)(uintptr_t)c->d_binom64.p, (uint64_t)(uintptr_t)c->d_hsub.p, (uint64_t)total_slots,
                      (uint64_t)use_pipe, (uint64_t)c->pipe_rounds, (uint64_t)c->pipe_rounds_small,
-                     (uint64_t)c->score_small_layers, (uint64_t)c->pipe_occ, (uint64_t)c->pipe_chain, (uint64_t)(uintptr_t)c->d_pstate.p,
+                     (uint64_t)c->score_small_layers, (uint64_t)c->pipe_occ, (uint64_t)c->pipe_chain, (uint64_t)c->pipe_grid_max, (uint64_t)(uintptr_t)c->d_pstate.p,
                      (uint64_t)(uintptr_t)c->d_pqueue.p, (uint64_t)(uintptr_t)c->d_pstages.p,
                      (uint64_t)(uintptr_t)c->d_pinit.p});
         for (int i = 0; i < nv; ++i) gkey.push_back((uint64_t)vars[i]);
@@ -2784,6 +2784,7 @@ launched:
     if (c->pipe_pending) {
         c->pipe_pending = false;
         if ((rc = pipe_check(c))) return rc;
+        pipe_report(c);
     }
     if (wide_err)
         return set_err(c, ULG_ERR_UNSUPPORTED,

@@ -51,7 +51,9 @@ struct PipeArgs {
     int R;        // rounds (x 64 sets) per two-pass tile
     int Rsmall;   // rounds per one-pass tile
     int chain;    // the wave that releases a stage starts on it (pipe_chain)
+    uint32_t total_slots;  // table slots (a walk entry's slot is checked against it)
     uint64_t timeout;  // wall-clock ticks a wave may stay idle before the call fails
+    uint64_t *stats;   // ULG_PIPE_STATS: 10 counters summed over waves (nullptr: off)
 };
 
 // LDS of one workgroup: the shared read-only tables, then per wave its pool
@@ -84,5 +86,7 @@ int pipe_prepare(ulg_ctx *c, int nv, int S, int kmax, int max_parents, const std
 int pipe_launch(ulg_ctx *c, const PipeArgs &a, hipStream_t st);
 // After the call: 0, or ULG_ERR_HIP when a wave reported a stall.
 int pipe_check(ulg_ctx *c);
+// ULG_PIPE_STATS: print the last call's per-activity wave time on stderr
+void pipe_report(ulg_ctx *c);
 
 }  // namespace ulg

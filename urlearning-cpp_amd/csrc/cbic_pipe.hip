@@ -45,6 +45,7 @@
 // the error word and leaves, and the host reports the stall.
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -436,6 +437,10 @@ __device__ __forceinline__ int walk_chunk(const PipeArgs &a, int vi, int s, uint
         const float hch = __uint_as_float((uint32_t)ld64(en + 1));
         const bool d = (dom >> k) & 1u;
         const uint32_t slot = (uint32_t)e0;
+        if (slot >= a.total_slots) {  // never: an entry read before it was written (protocol bug)
+            st32(a.done + 1, 2u);
+            continue;
+        }
         stf(a.table + slot, d ? absent_f() : -ts);
         if (hsub_on) stf(a.hsub + slot, d ? hch : fmaxf(hch, -ts));
     }
@@ -596,8 +601,13 @@ __global__ void __launch_bounds__(kBlock, OCC) pipe_kernel(PipeArgs a) {
     const int rot = (int)((xcc_id() * (uint32_t)per + ((blockIdx.x >> 3) * 4u + (uint32_t)wid) % (uint32_t)per) %
                           (uint32_t)a.nv);
     uint64_t idle_since = 0;
+    int backoff = 1;
+    // ULG_PIPE_STATS: wall-clock ticks and counts per activity, summed over waves
+    uint64_t st_find = 0, st_idle = 0, st_t[3] = {0, 0, 0}, st_n[3] = {0, 0, 0}, st_polls = 0;
+    const bool stats = a.stats != nullptr;
     while (true) {
         bool any_left = true;
+        const uint64_t t0 = stats ? wall_clock64() : 0;
         Item it = find_work(a, rot, lane, any_left);
         // wave-uniform in SGPRs: the dispatch below then branches on scalars
         // and each item form keeps its own register allocation
@@ -605,21 +615,33 @@ __global__ void __launch_bounds__(kBlock, OCC) pipe_kernel(PipeArgs a) {
         it.vi = __builtin_amdgcn_readfirstlane(it.vi);
         it.s = __builtin_amdgcn_readfirstlane(it.s);
         it.idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)it.idx);
+        if (stats) {
+            st_find += wall_clock64() - t0;
+            ++st_polls;
+        }
         if (it.kind > 0) {
             idle_since = 0;
-            int nxt = run_any(a, sh, it, lane, P);
-            // The wave that released a variable's next stage starts on it
-            // at once (the chain's critical path, and its slabs are warm in
-            // this XCD's L2); other waves join through find_work.
-            while (nxt >= 0 && a.chain) {
+            backoff = 1;
+            Item cur = it;
+            while (true) {
+                const uint64_t t1 = stats ? wall_clock64() : 0;
+                const int nxt = run_any(a, sh, cur, lane, P);
+                if (stats) {
+                    const int kk = cur.kind == 2 ? 2 : ((cur.s / 2 + 1) <= a.Ls ? 0 : 1);
+                    st_t[kk] += wall_clock64() - t1;
+                    ++st_n[kk];
+                }
+                // The wave that released a variable's next stage starts on it
+                // at once (the chain's critical path, and its slabs are warm
+                // in this XCD's L2); other waves join through find_work.
+                if (nxt < 0 || !a.chain) break;
                 uint32_t t = 0;
                 if (lane == 0)
-                    t = __hip_atomic_fetch_add((gu32 *)&a.ctr[it.vi * a.NS + nxt].claim, 1u, __ATOMIC_RELAXED,
+                    t = __hip_atomic_fetch_add((gu32 *)&a.ctr[cur.vi * a.NS + nxt].claim, 1u, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT);
                 t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-                if (t >= a.stages[it.vi * a.NS + nxt].ntiles) break;
-                const Item nx{1, it.vi, nxt, t};
-                nxt = run_any(a, sh, nx, lane, P);
+                if (t >= a.stages[cur.vi * a.NS + nxt].ntiles) break;
+                cur = Item{1, cur.vi, nxt, t};
             }
             continue;
         }
@@ -632,7 +654,16 @@ __global__ void __launch_bounds__(kBlock, OCC) pipe_kernel(PipeArgs a) {
             break;
         }
         if (ld32(a.done + 1)) break;
-        __builtin_amdgcn_s_sleep(2);
+        // nothing to claim: back off (up to ~6 us) so idle waves do not
+        // flood the counters' lines while the others work
+        for (int b = 0; b < backoff; ++b) __builtin_amdgcn_s_sleep(8);
+        backoff = backoff < 32 ? 2 * backoff : 32;
+        if (stats) st_idle += wall_clock64() - now;
+    }
+    if (stats && lane == 0) {
+        const uint64_t v[10] = {st_find, st_idle, st_t[0], st_t[1], st_t[2], st_n[0], st_n[1], st_n[2], st_polls, 1};
+        for (int i = 0; i < 10; ++i)
+            __hip_atomic_fetch_add((gu64 *)(a.stats + i), v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -718,6 +749,12 @@ int pipe_prepare(ulg_ctx *c, int nv, int S, int kmax, int max_parents, const std
     a.R = R;
     a.Rsmall = Rs;
     a.chain = c->pipe_chain;
+    a.total_slots = (uint32_t)(c->table.cap < 0xFFFFFFFFull ? c->table.cap : 0xFFFFFFFFull);
+    a.stats = nullptr;
+    if (std::getenv("ULG_PIPE_STATS")) {
+        if ((rc = ensure(c, c->d_pstats, 16))) return rc;
+        a.stats = c->d_pstats.p;
+    }
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0) khz = 100000;
     a.timeout = (uint64_t)khz * 1000ull * 10ull;  // 10 s idle
@@ -727,6 +764,7 @@ int pipe_prepare(ulg_ctx *c, int nv, int S, int kmax, int max_parents, const std
 
 int pipe_launch(ulg_ctx *c, const PipeArgs &a, hipStream_t st) {
     ULG_HIP(c, hipMemsetAsync(c->d_pstate.p, 0, c->pipe_zero_bytes, st));
+    if (a.stats) ULG_HIP(c, hipMemsetAsync(a.stats, 0, 16 * 8, st));
     ULG_HIP(c, hipMemcpyAsync(a.stage_of, c->d_pinit.p, (size_t)a.nv * 4, hipMemcpyDeviceToDevice, st));
     const PipeLds lay = pipe_lds(a.n, a.nv, a.S);
     void (*kfn)(PipeArgs) = c->pipe_occ == 3 ? pipe_kernel<3> : pipe_kernel<2>;
@@ -741,7 +779,8 @@ int pipe_launch(ulg_ctx *c, const PipeArgs &a, hipStream_t st) {
         ULG_HIP(c, hipGetDeviceProperties(&pr, c->device));
         c->pipe_cus = pr.multiProcessorCount;
     }
-    const int grid = std::max(1, per_cu) * std::max(1, c->pipe_cus);
+    int grid = std::max(1, per_cu) * std::max(1, c->pipe_cus);
+    if (c->pipe_grid_max > 0) grid = std::min(grid, c->pipe_grid_max);  // A/B: fewer workers
     prof_begin_s(c, "score_pipe", st);
     hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kBlock), (size_t)lay.total, st, a);
     prof_end_s(c, st);
@@ -749,9 +788,25 @@ int pipe_launch(ulg_ctx *c, const PipeArgs &a, hipStream_t st) {
     return ULG_OK;
 }
 
+void pipe_report(ulg_ctx *c) {
+    if (!std::getenv("ULG_PIPE_STATS") || !c->d_pstats.p) return;
+    uint64_t v[16] = {0};
+    if (hipMemcpy(v, c->d_pstats.p, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return;
+    const double tick = 1e-2;  // wall clock 100 MHz: us per tick
+    std::fprintf(stderr,
+                 "pipe_stats waves=%llu polls=%llu find_us=%.0f idle_us=%.0f | onepass n=%llu us=%.0f | twopass n=%llu "
+                 "us=%.0f | walk n=%llu us=%.0f | per item us: onepass %.2f twopass %.2f walk %.2f find %.2f\n",
+                 (unsigned long long)v[9], (unsigned long long)v[8], v[0] * tick, v[1] * tick,
+                 (unsigned long long)v[5], v[2] * tick, (unsigned long long)v[6], v[3] * tick,
+                 (unsigned long long)v[7], v[4] * tick, v[5] ? v[2] * tick / v[5] : 0.0, v[6] ? v[3] * tick / v[6] : 0.0,
+                 v[7] ? v[4] * tick / v[7] : 0.0, v[8] ? v[0] * tick / v[8] : 0.0);
+}
+
 int pipe_check(ulg_ctx *c) {
     if (c->pipe_stall_pinned && *c->pipe_stall_pinned)
-        return set_err(c, ULG_ERR_HIP, "ulg_cbic_score: the scoring pipeline stalled (a wave waited 10 s for work)");
+        return set_err(c, ULG_ERR_HIP, *c->pipe_stall_pinned == 2
+                                           ? "ulg_cbic_score: the scoring pipeline read a walk entry before it was written"
+                                           : "ulg_cbic_score: the scoring pipeline stalled (a wave waited 10 s for work)");
     return ULG_OK;
 }
 

@@ -152,12 +152,14 @@ struct ulg_ctx {
     int pipe_chain = 1;            // the wave that releases a stage starts on it
     int pipe_occ = 2;              // waves per SIMD the pipeline kernel is compiled for (2 or 3)
     int pipe_cus = 0;              // compute units of the device (queried once)
+    int pipe_grid_max = 0;         // A/B: at most this many workgroups (0: every resident one)
     int pipe_nv = 0;
     size_t pipe_zero_bytes = 0;    // the per-call zeroed block at the start of d_pstate
     ulg::DevBuf<uint8_t> d_pstate;    // stage counters, chunk fill counters, done words, current stages
     ulg::DevBuf<uint64_t> d_pqueue;   // walk entries of every two-pass stage
     ulg::DevBuf<uint8_t> d_pstages;   // PipeStage table
     ulg::DevBuf<uint32_t> d_pinit;    // first stage of every variable
+    ulg::DevBuf<uint64_t> d_pstats;   // ULG_PIPE_STATS counters
     ulg::Mirror mir_pstages, mir_pinit;
     unsigned int *pipe_stall_pinned = nullptr;  // the stall word of the last call, copied behind it
     bool pipe_pending = false;     // the last call ran the pipeline: check its stall word after the sync
