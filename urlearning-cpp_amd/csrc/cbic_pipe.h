@@ -52,6 +52,7 @@ struct PipeArgs {
     int Rsmall;   // rounds per one-pass tile
     int chain;    // the wave that releases a stage starts on it (pipe_chain)
     uint32_t total_slots;  // table slots (a walk entry's slot is checked against it)
+    int plain;    // pipe_plain: plain slab stores + a release per item (A/B)
     uint64_t timeout;  // wall-clock ticks a wave may stay idle before the call fails
     uint64_t *stats;   // ULG_PIPE_STATS: 10 counters summed over waves (nullptr: off)
 };

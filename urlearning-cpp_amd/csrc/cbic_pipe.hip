@@ -71,6 +71,13 @@ __device__ __forceinline__ void st64(uint64_t *p, uint64_t v) {
 }
 __device__ __forceinline__ void stf(float *p, float v) { st32(reinterpret_cast<uint32_t *>(p), __float_as_uint(v)); }
 __device__ __forceinline__ float ldf(const float *p) { return LdSc1::ld(p); }
+// a decided value into the slabs: write-through (sc1) by default; with
+// pipe_plain a plain store that keeps the line in this XCD's L2, published by
+// the release fence in stage_add
+__device__ __forceinline__ void slab_st(const PipeArgs &a, float *p, float v) {
+    if (a.plain) *p = v;
+    else stf(p, v);
+}
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // sets per lane of a walk chunk (walk_sliced_kernel's defaults: 2 up to
@@ -98,6 +105,13 @@ __device__ __forceinline__ void publish_next(const PipeArgs &a, int vi, int s) {
 // (wave-uniform) the stage this wave released, or -1.
 __device__ __forceinline__ int stage_add(const PipeArgs &a, int vi, int s, uint64_t delta, int lane) {
     drain();
+    if (a.plain) {
+        // plain slab stores: write this XCD's dirty L2 lines back before the
+        // counter hands them over (Guideline 16 R1 producer; the asm wait
+        // after the fence, Pitfall 12)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        drain();
+    }
     int released = -1;
     if (lane == 0) {
         PipeCtr *ct = a.ctr + vi * a.NS + s;
@@ -179,7 +193,7 @@ __device__ __forceinline__ int tile_onepass(const PipeArgs &a, const PipeShared 
             out = ((double)best + 0.0 >= (double)(-ts)) ? absent_f() : -ts;
         }
         const uint64_t slot = sh.toff[vbase + L] + rankP;
-        stf(a.table + slot, out);
+        slab_st(a, a.table + slot, out);
         // subset maxima for the layers above (score_layer_kernel's one-pass form)
         uint64_t rc[L], rz[L];
         child_ranks<L, false>(cm, sh.binom, rc, rz);
@@ -188,7 +202,7 @@ __device__ __forceinline__ int tile_onepass(const PipeArgs &a, const PipeShared 
 #pragma unroll
             for (int i = 0; i < L; ++i) hch = fmaxf(hch, ldf(a.hsub + sh.toff[vbase + L - 1] + rc[i]));
         }
-        stf(a.hsub + slot, fmaxf(out, hch));
+        slab_st(a, a.hsub + slot, fmaxf(out, hch));
     }
     return stage_add(a, vi, s, 1ull << 32, lane);
 }
@@ -258,8 +272,8 @@ __device__ __forceinline__ void pool_drain(const PipeArgs &a, const PipeShared &
         for (int wj = 0; wj < W; ++wj) st64(e + 2 + W + wj, ow[wj]);
     } else if (act) {
         const float o = dom ? absent_f() : -ts;
-        stf(a.table + slot, o);
-        if (hsub_on) stf(a.hsub + slot, fmaxf(o, hch));
+        slab_st(a, a.table + slot, o);
+        if (hsub_on) slab_st(a, a.hsub + slot, fmaxf(o, hch));
     }
     if (nq) {
         // the entries are written: count them into their walk chunks
@@ -292,6 +306,7 @@ __device__ __forceinline__ int tile_twopass(const PipeArgs &a, const PipeShared 
     const bool hsub_on = !(L == a.kmax && PH == 1);
     int cnt = 0;
     uint32_t queued = 0;
+    const uint64_t tq0 = a.stats ? wall_clock64() : 0;
     for (int r = 0; r < a.R; ++r) {
         const uint32_t idx = (tile * (uint32_t)a.R + (uint32_t)r) * 64u + (uint32_t)lane;
         const bool valid = idx < st.nsets;
@@ -348,8 +363,8 @@ __device__ __forceinline__ int tile_twopass(const PipeArgs &a, const PipeShared 
                 }
             }
             if (!need) {
-                stf(a.table + slot, out);
-                if (hsub_on) stf(a.hsub + slot, fmaxf(out, hch));
+                slab_st(a, a.table + slot, out);
+                if (hsub_on) slab_st(a, a.hsub + slot, fmaxf(out, hch));
             }
         }
         // 2. pool the undecided sets; gather on dense lanes
@@ -364,9 +379,21 @@ __device__ __forceinline__ int tile_twopass(const PipeArgs &a, const PipeShared 
         cnt += __popcll(nm);
     }
     __builtin_amdgcn_wave_barrier();
+    const uint64_t tq1 = a.stats ? wall_clock64() : 0;
     // 3. the pooled sets on dense lanes, 64 at a time
     for (int off = 0; off < cnt; off += 64)
         pool_drain<L, PH>(a, sh, vi, s, P, off, cnt - off < 64 ? cnt - off : 64, lane, queued, hsub_on);
+    if (a.stats) {
+        const uint64_t tq2 = wall_clock64();
+        drain();
+        const uint64_t tq3 = wall_clock64();
+        if (lane == 0) {
+            __hip_atomic_fetch_add((gu64 *)(a.stats + 10), tq1 - tq0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add((gu64 *)(a.stats + 11), tq2 - tq1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add((gu64 *)(a.stats + 12), tq3 - tq2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add((gu64 *)(a.stats + 13), (uint64_t)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 
     return stage_add(a, vi, s, (1ull << 32) - (uint64_t)queued, lane);
 }
@@ -441,8 +468,8 @@ __device__ __forceinline__ int walk_chunk(const PipeArgs &a, int vi, int s, uint
             st32(a.done + 1, 2u);
             continue;
         }
-        stf(a.table + slot, d ? absent_f() : -ts);
-        if (hsub_on) stf(a.hsub + slot, d ? hch : fmaxf(hch, -ts));
+        slab_st(a, a.table + slot, d ? absent_f() : -ts);
+        if (hsub_on) slab_st(a, a.hsub + slot, d ? hch : fmaxf(hch, -ts));
     }
     return stage_add(a, vi, s, (uint64_t)e, lane);
 }
@@ -597,13 +624,14 @@ __global__ void __launch_bounds__(kBlock, OCC) pipe_kernel(PipeArgs a) {
     // Every XCD starts its search at its own run of variables (their slabs
     // then mostly stay in that XCD's L2), and the waves of one XCD spread over
     // that run.
-    const int per = (a.nv + 7) / 8;
-    const int rot = (int)((xcc_id() * (uint32_t)per + ((blockIdx.x >> 3) * 4u + (uint32_t)wid) % (uint32_t)per) %
-                          (uint32_t)a.nv);
+    const int xcc = (int)xcc_id();
+    const int vlo = xcc * a.nv / 8, vhi = (xcc + 1) * a.nv / 8;
+    const int own = vhi > vlo ? vhi - vlo : 1;
+    const int rot = (vlo + (int)(((blockIdx.x >> 3) * 4u + (uint32_t)wid) % (uint32_t)own)) % a.nv;
     uint64_t idle_since = 0;
     int backoff = 1;
     // ULG_PIPE_STATS: wall-clock ticks and counts per activity, summed over waves
-    uint64_t st_find = 0, st_idle = 0, st_t[3] = {0, 0, 0}, st_n[3] = {0, 0, 0}, st_polls = 0;
+    uint64_t st_find = 0, st_idle = 0, st_t[3] = {0, 0, 0}, st_n[3] = {0, 0, 0}, st_polls = 0, st_lost = 0;
     const bool stats = a.stats != nullptr;
     while (true) {
         bool any_left = true;
@@ -645,7 +673,10 @@ __global__ void __launch_bounds__(kBlock, OCC) pipe_kernel(PipeArgs a) {
             }
             continue;
         }
-        if (it.kind < 0) continue;
+        if (it.kind < 0) {
+            if (stats) ++st_lost;
+            continue;
+        }
         if (!any_left) break;  // every variable's last stage is published
         const uint64_t now = wall_clock64();
         if (idle_since == 0) idle_since = now;
@@ -661,9 +692,10 @@ __global__ void __launch_bounds__(kBlock, OCC) pipe_kernel(PipeArgs a) {
         if (stats) st_idle += wall_clock64() - now;
     }
     if (stats && lane == 0) {
-        const uint64_t v[10] = {st_find, st_idle, st_t[0], st_t[1], st_t[2], st_n[0], st_n[1], st_n[2], st_polls, 1};
+        const uint64_t v[11] = {st_find, st_idle, st_t[0], st_t[1], st_t[2], st_n[0], st_n[1], st_n[2], st_polls, 1, 0};
         for (int i = 0; i < 10; ++i)
             __hip_atomic_fetch_add((gu64 *)(a.stats + i), v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add((gu64 *)(a.stats + 14), st_lost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -749,6 +781,7 @@ int pipe_prepare(ulg_ctx *c, int nv, int S, int kmax, int max_parents, const std
     a.R = R;
     a.Rsmall = Rs;
     a.chain = c->pipe_chain;
+    a.plain = c->pipe_plain;
     a.total_slots = (uint32_t)(c->table.cap < 0xFFFFFFFFull ? c->table.cap : 0xFFFFFFFFull);
     a.stats = nullptr;
     if (std::getenv("ULG_PIPE_STATS")) {
@@ -800,6 +833,11 @@ void pipe_report(ulg_ctx *c) {
                  (unsigned long long)v[5], v[2] * tick, (unsigned long long)v[6], v[3] * tick,
                  (unsigned long long)v[7], v[4] * tick, v[5] ? v[2] * tick / v[5] : 0.0, v[6] ? v[3] * tick / v[6] : 0.0,
                  v[7] ? v[4] * tick / v[7] : 0.0, v[8] ? v[0] * tick / v[8] : 0.0);
+    std::fprintf(stderr,
+                 "pipe_stats twopass per tile us: score rounds %.2f, gathers+queue %.2f, final drain %.2f; pooled sets "
+                 "per tile %.1f; lost claims %llu\n",
+                 v[6] ? v[10] * tick / v[6] : 0.0, v[6] ? v[11] * tick / v[6] : 0.0, v[6] ? v[12] * tick / v[6] : 0.0,
+                 v[6] ? (double)v[13] / v[6] : 0.0, (unsigned long long)v[14]);
 }
 
 int pipe_check(ulg_ctx *c) {

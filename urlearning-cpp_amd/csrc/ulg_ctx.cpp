@@ -236,6 +236,11 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         c->pipe_grid_max = (int)value;
         return ULG_OK;
     }
+    if (std::strcmp(name, "pipe_plain") == 0) {
+        if (value < 0 || value > 1) return set_err(c, ULG_ERR_ARG, "pipe_plain must be 0 or 1");
+        c->pipe_plain = (int)value;
+        return ULG_OK;
+    }
     if (std::strcmp(name, "pipe_rounds") == 0) {
         if (value < 1 || value > 64) return set_err(c, ULG_ERR_ARG, "pipe_rounds must be 1..64");
         c->pipe_rounds = (int)value;

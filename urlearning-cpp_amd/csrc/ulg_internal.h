@@ -150,6 +150,7 @@ struct ulg_ctx {
     int pipe_rounds = 2;           // 64-set rounds per two-pass score tile
     int pipe_rounds_small = 1;     // ... per one-pass tile
     int pipe_chain = 1;            // the wave that releases a stage starts on it
+    int pipe_plain = 0;            // plain slab stores + a release per item instead of sc1 stores
     int pipe_occ = 2;              // waves per SIMD the pipeline kernel is compiled for (2 or 3)
     int pipe_cus = 0;              // compute units of the device (queried once)
     int pipe_grid_max = 0;         // A/B: at most this many workgroups (0: every resident one)
