@@ -77,6 +77,15 @@ def main():
                     ok = False
             same = all(np.asarray(x).tobytes() == np.asarray(y).tobytes() for x, y in zip(res[0], res[1]))
             ok &= same
+            if name == "c3":  # against the oracle command lines' digests too
+                import hashlib
+                ref = json.load(open(os.path.join(ROOT, "tests", "golden", "c3_oracle.json")))
+                offs, sets = res[1][0], res[1][1]
+                for v in range(n):
+                    srt = np.sort(np.asarray(sets[offs[v]:offs[v + 1]]).astype(np.uint64))
+                    if hashlib.sha256(srt.tobytes()).hexdigest() != ref["sets_sha256_per_variable"][v]:
+                        print(json.dumps({"case": name, "error": f"variable {v} differs from c3_oracle.json"}))
+                        ok = False
             print(json.dumps({"case": name, "n": n, "N": N, "k": k, "kind": kind, "identical": same,
                               "stored": int(res[1][0][-1]), "layers_ms": ms[0], "pipe_ms": ms[1]}), flush=True)
     ctx.close()

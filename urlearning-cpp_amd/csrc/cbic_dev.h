@@ -277,14 +277,37 @@ __device__ __forceinline__ void cover_words(uint64_t *w) {
             if (j & c) w[j] |= w[j ^ c];
 }
 
+// The candidate local subsets of presence_unrolled, in increasing order, as a
+// compile-time list: every nonempty t of the Q local bits with at most L
+// bits, except P itself, and the L-bit ones only for sets without variable 0
+// (PHASE 1) that hold variable 0 (local bit 0).
+constexpr int popc_c(uint32_t x) { return x ? (int)(x & 1u) + popc_c(x >> 1) : 0; }
+template <int L, int PHASE, int Q>
+struct PresList {
+    uint32_t t[1 << Q];
+    int n;
+    constexpr PresList() : t{}, n(0) {
+        const uint32_t Plocal = (Q == L) ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
+        for (uint32_t x = 1; x < (1u << Q); ++x) {
+            const int pc = popc_c(x);
+            if (pc > L || x == Plocal) continue;
+            if (pc == L && (PHASE == 0 || !(x & 1u))) continue;
+            t[n++] = x;
+        }
+    }
+};
+
 // Presence of every key with a fully unrolled subset loop: the rank of each
 // subset t of the Q local bits is a compile-time sum of per-(bit, position)
 // binomials preloaded into registers.  Q = L when variable 0 is in P (local
-// bits = P), Q = L + 1 otherwise (P plus variable 0).
-template <int L, int PHASE, int Q, int W, class LD = LdPlain>
+// bits = P), Q = L + 1 otherwise (P plus variable 0).  The loads go out in
+// batches of NB before any of their values is used: the gather is a chain of
+// independent loads, and issued one at a time (what the compiler makes of a
+// load-then-test loop) every load pays the full memory latency.
+template <int L, int PHASE, int Q, int W, class LD = LdPlain, int NB = 16>
 __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi, float thr, const uint32_t *binom,
                                                   uint64_t cpack, bool z, const float *table, const uint64_t *toffv) {
-    constexpr uint32_t Plocal = (Q == L) ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
+    constexpr PresList<L, PHASE, Q> PL{};
     uint32_t RB[Q][L + 1];
 #pragma unroll
     for (int lb = 0; lb < Q; ++lb) {
@@ -296,22 +319,44 @@ __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi,
 #pragma unroll
     for (int pc = 1; pc <= L; ++pc) off[pc] = toffv[pc];
 #pragma clang loop unroll(full)
-    for (uint32_t t = 1; t < (1u << Q); ++t) {
-        const int pc = __builtin_popcount(t);
-        if (pc > L || t == Plocal) continue;
-        if (pc == L && (PHASE == 0 || !(t & 1u))) continue;
-        if ((t & 1u) && !z) continue;
-        uint64_t rk = 0;
-        int jj = 0;
+    for (int b0 = 0; b0 < PL.n; b0 += NB) {
+        // opaque per batch: no rank partial sum is shared across batches, so
+        // the addresses of a batch are computed just before its loads
 #pragma unroll
-        for (int b = 0; b < Q; ++b)
-            if ((t >> b) & 1u) {
-                ++jj;
-                rk += RB[b][jj];
-            }
-        const float val = LD::ld(table + off[pc] + rk);
-        if (fbits(val) != kAbsentBits) present.set(t);
-        if (val >= thr) hi.set(t);  // the absent sentinel is a NaN: never >= thr
+        for (int lb = 0; lb < Q; ++lb)
+#pragma unroll
+            for (int p = 1; p <= L; ++p)
+                if (p <= lb + 1) asm volatile("" : "+v"(RB[lb][p]));
+        float v[NB];
+#pragma clang loop unroll(full)
+        for (int i = 0; i < NB; ++i) {
+            if (b0 + i >= PL.n) break;
+            const uint32_t t = PL.t[b0 + i];
+            const int pc = popc_c(t);
+            uint64_t rk = 0;
+            int jj = 0;
+#pragma unroll
+            for (int b = 0; b < Q; ++b)
+                if ((t >> b) & 1u) {
+                    ++jj;
+                    rk += RB[b][jj];
+                }
+            // a key with variable 0 exists only when variable 0 is a
+            // candidate (z); otherwise the lane loads slot 0 and ignores it
+            const bool ok = !(t & 1u) || z;
+            v[i] = LD::ld(table + (ok ? off[pc] + rk : 0ull));
+        }
+#pragma clang loop unroll(full)
+        for (int i = 0; i < NB; ++i) {
+            if (b0 + i >= PL.n) break;
+            const uint32_t t = PL.t[b0 + i];
+            const bool ok = !(t & 1u) || z;
+            if (ok && fbits(v[i]) != kAbsentBits) present.set(t);
+            if (ok && v[i] >= thr) hi.set(t);  // the absent sentinel is a NaN: never >= thr
+        }
+        // keep the batches apart: hoisting every load of the unrolled loop
+        // would hold all 2^Q values in registers at once
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
