@@ -2533,7 +2533,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                      (uint64_t)(uintptr_t)c->gram.p, (uint64_t)(uintptr_t)c->d_binom.p,
                      (uint64_t)(uintptr_t)c->d_binom64.p, (uint64_t)(uintptr_t)c->d_hsub.p, (uint64_t)total_slots,
                      (uint64_t)use_pipe, (uint64_t)c->pipe_rounds, (uint64_t)c->pipe_rounds_small,
-                     (uint64_t)c->score_small_layers, (uint64_t)c->pipe_occ, (uint64_t)c->pipe_chain, (uint64_t)c->pipe_grid_max, (uint64_t)c->pipe_plain, (uint64_t)(uintptr_t)c->d_pstate.p,
+                     (uint64_t)c->score_small_layers, (uint64_t)c->pipe_occ, (uint64_t)c->pipe_chain, (uint64_t)c->pipe_grid_max, (uint64_t)(uintptr_t)c->d_pwork.p, (uint64_t)(uintptr_t)c->d_pstate.p,
                      (uint64_t)(uintptr_t)c->d_pqueue.p, (uint64_t)(uintptr_t)c->d_pstages.p,
                      (uint64_t)(uintptr_t)c->d_pinit.p});
         for (int i = 0; i < nv; ++i) gkey.push_back((uint64_t)vars[i]);

@@ -18,6 +18,8 @@ struct PipeStage {
     uint32_t ntiles;  // score tiles (64 x rounds sets each)
     uint32_t foff;    // first walk-chunk fill counter
     uint32_t next;    // the variable's next stage with sets (0xFFFFFFFF: none)
+    uint32_t slab;    // first float of the stage's values in the work layout (a 128-byte line)
+    uint32_t pad;
     uint64_t qoff;    // first queue word of the stage's walk entries
 };
 
@@ -44,23 +46,25 @@ struct PipeArgs {
     uint32_t *done;           // [0] variables finished, [1] stall flag
     uint32_t *stage_of;       // [nv] each variable's current stage
     uint64_t *queue;
-    float *table, *hsub;
+    float *table;             // colex-ordered slabs (read by the compaction after the launch)
+    float *ptab, *phsub;      // work layout: values / subset maxima, one line-aligned slab per stage
     double N, lambda;
     int n, nv, S, NS, kmax;
     int Ls;       // layers <= Ls: one-pass tiles
     int R;        // rounds (x 64 sets) per two-pass tile
     int Rsmall;   // rounds per one-pass tile
     int chain;    // the wave that releases a stage starts on it (pipe_chain)
-    uint32_t total_slots;  // table slots (a walk entry's slot is checked against it)
-    int plain;    // pipe_plain: plain slab stores + a release per item (A/B)
+    uint32_t total_slots;  // table slots (a walk entry's slots are checked against them)
+    uint32_t work_slots;   // work-layout slots
     uint64_t timeout;  // wall-clock ticks a wave may stay idle before the call fails
     uint64_t *stats;   // ULG_PIPE_STATS: 10 counters summed over waves (nullptr: off)
 };
 
 // LDS of one workgroup: the shared read-only tables, then per wave its pool
-// of undecided sets (kPipePool entries: compact mask, slot, ts, children max)
+// of undecided sets (kPipePool entries: compact mask, work slot, ts, children
+// max, table slot)
 constexpr int kPipePool = 128;
-constexpr int kPipePoolBytes = kPipePool * (8 + 4 + 4 + 4);
+constexpr int kPipePoolBytes = kPipePool * (8 + 4 + 4 + 4 + 4);
 struct PipeLds {
     int gram, binom, toff, meta, pool, total;
 };

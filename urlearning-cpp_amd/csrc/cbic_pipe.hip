@@ -35,14 +35,18 @@
 // reaches that value publishes the variable's next stage.
 //
 // Visibility inside the launch (MI355X_MICROARCH.md, inter-workgroup
-// visibility; cdna_hip_programming.md Guideline 16): every slab value, subset
-// maximum and queue entry that another wave reads is stored write-through
-// (sc1) and loaded with sc1 loads (past the CU's L1, which other CUs' stores
-// never refresh); a wave drains its stores (s_waitcnt vmcnt(0)) before the
-// atomic that hands them over (chunk fill counters, the stage counter).
-// Read-only inputs (Gram matrix, binomials, offsets, stage table) are plain
-// loads.  Every spin is bounded: a wave idle for `timeout` clock ticks sets
-// the error word and leaves, and the host reports the stall.
+// visibility; cdna_hip_programming.md Guideline 16).  Decided values and
+// subset maxima live in the work layout below: plain stores, and every item
+// ends with s_waitcnt vmcnt(0) + an agent release (the XCD's dirty L2 lines
+// written back) before the stage-counter add that hands them over; readers use
+// plain loads, which is exact because no cache can hold a line of a stage
+// before the stage is complete (see "the work layout").  Walk entries, the
+// counters and the current-stage words are stored and loaded with sc1 (agent
+// atomics), and a wave drains its entry stores before the fill-counter add
+// that publishes them.  Read-only inputs (Gram matrix, binomials, offsets,
+// stage table) are plain loads.  Every spin is bounded: a wave idle for
+// `timeout` clock ticks sets the error word and leaves, and the host reports
+// the stall.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -69,21 +73,13 @@ __device__ __forceinline__ void st32(uint32_t *p, uint32_t v) {
 __device__ __forceinline__ void st64(uint64_t *p, uint64_t v) {
     __hip_atomic_store((gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void stf(float *p, float v) { st32(reinterpret_cast<uint32_t *>(p), __float_as_uint(v)); }
-__device__ __forceinline__ float ldf(const float *p) { return LdSc1::ld(p); }
-// a decided value into the slabs: write-through (sc1) by default; with
-// pipe_plain a plain store that keeps the line in this XCD's L2, published by
-// the release fence in stage_add
-__device__ __forceinline__ void slab_st(const PipeArgs &a, float *p, float v) {
-    if (a.plain) *p = v;
-    else stf(p, v);
-}
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // sets per lane of a walk chunk (walk_sliced_kernel's defaults: 2 up to
 // layer 5, 4 at layer 6)
 __host__ __device__ constexpr int pipe_k(int L) { return L <= 5 ? 2 : 4; }
-// queue entry words: slot | ts << 32, hch, then W hi and W open words
+// queue entry words: work slot | ts << 32, hch | table slot << 32, then W hi
+// and W open words
 __host__ __device__ constexpr int entry_words(int L) { return 2 + 2 * bits_words(L); }
 
 struct PipeShared {
@@ -105,13 +101,11 @@ __device__ __forceinline__ void publish_next(const PipeArgs &a, int vi, int s) {
 // (wave-uniform) the stage this wave released, or -1.
 __device__ __forceinline__ int stage_add(const PipeArgs &a, int vi, int s, uint64_t delta, int lane) {
     drain();
-    if (a.plain) {
-        // plain slab stores: write this XCD's dirty L2 lines back before the
-        // counter hands them over (Guideline 16 R1 producer; the asm wait
-        // after the fence, Pitfall 12)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        drain();
-    }
+    // the slab values are plain stores: write this XCD's dirty L2 lines back
+    // before the counter hands them over (Guideline 16 R1 producer; the asm
+    // wait after the fence, Pitfall 12)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    drain();
     int released = -1;
     if (lane == 0) {
         PipeCtr *ct = a.ctr + vi * a.NS + s;
@@ -126,6 +120,165 @@ __device__ __forceinline__ int stage_add(const PipeArgs &a, int vi, int s, uint6
     return __builtin_amdgcn_readfirstlane(released);
 }
 
+// ---- the work layout ------------------------------------------------------------
+// Inside the launch the decided values live in a layout of their own: every
+// (variable, layer, phase) stage has its own slab, starting on a 128-byte
+// line, indexed by the set's rank in its phase's enumeration (sets with
+// variable 0: colex rank of the other members among the candidates after
+// variable 0; the rest: colex rank among those candidates, or among all of
+// them when variable 0 is not one).  A cache line then holds values of one
+// stage only, and nothing reads a stage's lines before the stage is
+// complete -- so no L1 or L2 can hold a stale copy of a line, plain loads are
+// exact, and the lines a stage writes stay in its XCD's L2 for the stages
+// above (the layer kernels' slabs interleave both phases of a layer).  The
+// values also go to the colex-ordered table the compaction reads after the
+// launch.
+struct Slabs {
+    uint32_t o0[kPipeMaxL + 1], o1[kPipeMaxL + 1];  // per layer: phase 0 / phase 1 slab offsets
+};
+__device__ __forceinline__ void load_slabs(const PipeArgs &a, int vi, int L, Slabs &sl) {
+#pragma unroll
+    for (int p = 1; p <= kPipeMaxL; ++p) {
+        if (p > L) break;
+        sl.o0[p] = a.stages[vi * a.NS + 2 * (p - 1)].slab;
+        sl.o1[p] = a.stages[vi * a.NS + 2 * (p - 1) + 1].slab;
+    }
+}
+__device__ __forceinline__ float ldw(const float *p) { return *p; }
+
+// address in the work layout of the local subset t of a set whose local bit
+// lb is compact index (cpack >> 6 lb) & 63 (local bit 0: variable 0)
+__device__ __forceinline__ uint32_t work_addr(uint32_t t, uint64_t cpack, uint32_t zz, const uint32_t *binom,
+                                              const Slabs &sl) {
+    uint32_t rk = 0;
+    int k = 0;
+    for (uint32_t rem = t & ~1u; rem; rem &= rem - 1) {
+        const int lb = __builtin_ctz(rem);
+        ++k;
+        rk += B(binom, (int)((cpack >> (6 * lb)) & 63ull) - (int)zz, k);
+    }
+    const int pc = __builtin_popcount(t);
+    // a select chain, not an indexed load: a runtime index into the
+    // register array would put it in scratch
+    uint32_t o = 0;
+#pragma unroll
+    for (int p = 1; p <= kPipeMaxL; ++p)
+        if (p == pc) o = (t & 1u) ? sl.o0[p] : sl.o1[p];
+    return o + rk;
+}
+
+// presence_unrolled (cbic_dev.h) over the work layout: the same subsets and
+// batches; a subset's rank counts its members other than variable 0, their
+// compact indices shifted down by one when variable 0 is a candidate
+template <int L, int PHASE, int Q, int W, int NB = 16>
+__device__ __forceinline__ void presence_work(Bits<W> &present, Bits<W> &hi, float thr, const uint32_t *binom,
+                                              uint64_t cpack, bool z, const float *work, const Slabs &sl) {
+    constexpr PresList<L, PHASE, Q> PL{};
+    const uint32_t zz = z ? 1u : 0u;
+    uint32_t RB[Q][L + 1];
+#pragma unroll
+    for (int lb = 1; lb < Q; ++lb) {
+        const int ci = (int)((cpack >> (6 * lb)) & 63ull) - (int)zz;
+#pragma unroll
+        for (int p = 1; p <= L; ++p) RB[lb][p] = (p <= lb) ? B(binom, ci < 0 ? 0 : ci, p) : 0u;
+    }
+#pragma clang loop unroll(full)
+    for (int b0 = 0; b0 < PL.n; b0 += NB) {
+#pragma unroll
+        for (int lb = 1; lb < Q; ++lb)
+#pragma unroll
+            for (int p = 1; p <= L; ++p)
+                if (p <= lb) asm volatile("" : "+v"(RB[lb][p]));
+        float v[NB];
+#pragma clang loop unroll(full)
+        for (int i = 0; i < NB; ++i) {
+            if (b0 + i >= PL.n) break;
+            const uint32_t t = PL.t[b0 + i];
+            const int pc = popc_c(t);
+            uint32_t rk = 0;
+            int jj = 0;
+#pragma unroll
+            for (int b = 1; b < Q; ++b)
+                if ((t >> b) & 1u) {
+                    ++jj;
+                    rk += RB[b][jj];
+                }
+            const bool ok = !(t & 1u) || z;
+            v[i] = ldw(work + (ok ? ((t & 1u) ? sl.o0[pc] : sl.o1[pc]) + rk : 0u));
+        }
+#pragma clang loop unroll(full)
+        for (int i = 0; i < NB; ++i) {
+            if (b0 + i >= PL.n) break;
+            const uint32_t t = PL.t[b0 + i];
+            const bool ok = !(t & 1u) || z;
+            if (ok && fbits(v[i]) != kAbsentBits) present.set(t);
+            if (ok && v[i] >= thr) hi.set(t);  // the absent sentinel is a NaN: never >= thr
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// Work addresses of P's direct subsets (layer L - 1) and, for a set without
+// variable 0 when variable 0 is a candidate, of the layer-L keys P\a + {0}
+// (SURVEY N4), for P = compact mask cm.
+template <int L, int PH>
+__device__ __forceinline__ void work_children(uint64_t cm, bool z, const uint32_t *binom, const Slabs &sl,
+                                              uint32_t (&ca)[L], uint32_t (&za)[L]) {
+    const int zz = z ? 1 : 0;
+    if constexpr (PH == 1) {
+        uint32_t d0[L], dm1[L];
+        uint64_t rem = cm;
+#pragma unroll
+        for (int j = 0; j < L; ++j) {
+            const int e = __builtin_ctzll(rem) - zz;
+            rem &= rem - 1;
+            d0[j] = B(binom, e, j + 1);
+            dm1[j] = B(binom, e, j);
+        }
+        uint32_t pre = 0;
+#pragma unroll
+        for (int i = 0; i < L; ++i) {
+            uint32_t suf = 0;
+#pragma unroll
+            for (int j = i + 1; j < L; ++j) suf += dm1[j];
+            const uint32_t rk = pre + suf;
+            ca[i] = (L > 1 ? sl.o1[L - 1 > 0 ? L - 1 : 1] : 0u) + rk;
+            za[i] = sl.o0[L] + rk;
+            pre += d0[i];
+        }
+    } else {
+        // P = {var0} u {f_1 < ... < f_{L-1}} (f = compact index - 1)
+        uint32_t d0[L], dm1[L];
+        uint64_t rem = cm & ~1ull;
+#pragma unroll
+        for (int k = 0; k < L - 1; ++k) {
+            const int f = __builtin_ctzll(rem) - 1;
+            rem &= rem - 1;
+            d0[k] = B(binom, f, k + 1);
+            dm1[k] = B(binom, f, k);
+        }
+        if constexpr (L > 1) {
+            uint32_t all = 0;
+#pragma unroll
+            for (int k = 0; k < L - 1; ++k) all += d0[k];
+            ca[0] = sl.o1[L - 1] + all;  // P \ {var0}
+            uint32_t pre = 0;
+#pragma unroll
+            for (int i = 0; i < L - 1; ++i) {
+                uint32_t suf = 0;
+#pragma unroll
+                for (int k = i + 1; k < L - 1; ++k) suf += dm1[k];
+                ca[i + 1] = sl.o0[L - 1] + pre + suf;  // P \ {f_i}: still holds var0
+                pre += d0[i];
+            }
+        } else {
+            ca[0] = 0;
+        }
+#pragma unroll
+        for (int i = 0; i < L; ++i) za[i] = 0;
+    }
+}
+
 // ---- one-pass tile (layers <= Ls): every set decided in its lane -----------
 template <int L, int PH>
 __device__ __forceinline__ int tile_onepass(const PipeArgs &a, const PipeShared &sh, int vi, int s, uint32_t tile, int lane) {
@@ -135,6 +288,9 @@ __device__ __forceinline__ int tile_onepass(const PipeArgs &a, const PipeShared 
     const uint64_t vbase = (uint64_t)vi * a.S;
     const uint8_t *cl = a.cand + vi * 64;
     constexpr int W = bits_words(L);
+    Slabs sl;
+    load_slabs(a, vi, L, sl);
+    const uint32_t zz = z ? 1u : 0u;
     for (int r = 0; r < a.Rsmall; ++r) {
         const uint32_t idx = (tile * (uint32_t)a.Rsmall + (uint32_t)r) * 64u + (uint32_t)lane;
         if (!wave_any(idx < st.nsets)) break;
@@ -164,7 +320,7 @@ __device__ __forceinline__ int tile_onepass(const PipeArgs &a, const PipeShared 
             Bits<W> present, hi, checked, visited;
             present.clear();
             hi.clear();
-            gather_keys<L, PH, 1, Bits<W>, LdSc1>(present, hi, ls, -ts, sh.binom, z, a.table, sh.toff + vbase);
+            presence_work<L, PH, (PH == 0 ? L : L + 1), W>(present, hi, -ts, sh.binom, ls.cpack, z, a.ptab, sl);
             checked.clear();
             visited.clear();
             checked.set(0u);  // checked.insert(empty_set)
@@ -176,33 +332,25 @@ __device__ __forceinline__ int tile_onepass(const PipeArgs &a, const PipeShared 
                 while (x) {
                     const uint32_t t = (uint32_t)(wj * 64 + __builtin_ctzll(x));
                     x &= x - 1;
-                    uint64_t rk = 0;
-                    uint32_t rem = t;
-                    int j = 0;
-                    while (rem) {
-                        const int lb = __builtin_ctz(rem);
-                        rem &= rem - 1;
-                        ++j;
-                        rk += B(sh.binom, (int)((ls.cpack >> (6 * lb)) & 63ull), j);
-                    }
-                    const float val = ldf(a.table + sh.toff[vbase + __builtin_popcount(t)] + rk);
+                    const float val = ldw(a.ptab + work_addr(t, ls.cpack, zz, sh.binom, sl));
                     if (val > best) best = val;
                 }
             }
             // BIC_OLS.cpp:234: best_subset_score + bic_threshold >= -the_score
             out = ((double)best + 0.0 >= (double)(-ts)) ? absent_f() : -ts;
         }
-        const uint64_t slot = sh.toff[vbase + L] + rankP;
-        slab_st(a, a.table + slot, out);
+        const uint32_t wslot = (PH == 0 ? sl.o0[L] : sl.o1[L]) + idx;
+        a.table[sh.toff[vbase + L] + rankP] = out;  // for the compaction after the launch
+        a.ptab[wslot] = out;
         // subset maxima for the layers above (score_layer_kernel's one-pass form)
-        uint64_t rc[L], rz[L];
-        child_ranks<L, false>(cm, sh.binom, rc, rz);
+        uint32_t ca[L], za[L];
+        work_children<L, PH>(cm, z, sh.binom, sl, ca, za);
         float hch = absent_f();
         if constexpr (L > 1) {
 #pragma unroll
-            for (int i = 0; i < L; ++i) hch = fmaxf(hch, ldf(a.hsub + sh.toff[vbase + L - 1] + rc[i]));
+            for (int i = 0; i < L; ++i) hch = fmaxf(hch, ldw(a.phsub + ca[i]));
         }
-        slab_st(a, a.hsub + slot, fmaxf(out, hch));
+        a.phsub[wslot] = fmaxf(out, hch);
     }
     return stage_add(a, vi, s, 1ull << 32, lane);
 }
@@ -212,35 +360,36 @@ __device__ __forceinline__ int tile_onepass(const PipeArgs &a, const PipeShared 
 constexpr int kPool = kPipePool;
 struct WavePool {
     uint64_t cm[kPool];
-    uint32_t slot[kPool];
+    uint32_t slot[kPool];  // work-layout slot
     float ts[kPool];
     float hch[kPool];
+    uint32_t sslot[kPool];  // colex-table slot (the compaction's)
 };
 static_assert(sizeof(WavePool) == kPipePoolBytes, "pipe_lds sizes the pools");
 
 template <int L, int PH>
 __device__ __forceinline__ void pool_drain(const PipeArgs &a, const PipeShared &sh, int vi, int s, const WavePool &P, int off,
-                           int take, int lane, uint32_t &queued, bool hsub_on) {
+                           int take, int lane, uint32_t &queued, bool hsub_on, const Slabs &sl) {
     constexpr int W = bits_words(L);
     constexpr int EW = entry_words(L);
     constexpr uint32_t CH = 64u * pipe_k(L);
     const bool z = sh.meta[vi * 4 + 2] != 0;
-    const uint64_t vbase = (uint64_t)vi * a.S;
     const bool act = lane < take;
     bool q = false, dom = false;
     Bits<W> present, hib;
     uint64_t cm = 0;
-    uint32_t slot = 0;
+    uint32_t slot = 0, sslot = 0;
     float ts = 0.0f, hch = 0.0f;
     if (act) {
         cm = P.cm[off + lane];
         slot = P.slot[off + lane];
+        sslot = P.sslot[off + lane];
         ts = P.ts[off + lane];
         hch = P.hch[off + lane];
         const LocalSet<L> ls = local_set<L>(cm, z);
         present.clear();
         hib.clear();
-        gather_keys<L, PH, 1, Bits<W>, LdSc1>(present, hib, ls, -ts, sh.binom, z, a.table, sh.toff + vbase);
+        presence_work<L, PH, (PH == 0 ? L : L + 1), W>(present, hib, -ts, sh.binom, ls.cpack, z, a.ptab, sl);
         dom = settle_rules<L, PH>(present, hib, ls, q);
     }
     // queue the sets that still need the walk (one reservation per wave)
@@ -265,15 +414,16 @@ __device__ __forceinline__ void pool_drain(const PipeArgs &a, const PipeShared &
         }
         uint64_t *e = a.queue + a.stages[vi * a.NS + s].qoff + (uint64_t)pos * EW;
         st64(e, (uint64_t)slot | ((uint64_t)__float_as_uint(ts) << 32));
-        st64(e + 1, (uint64_t)__float_as_uint(hch));
+        st64(e + 1, (uint64_t)__float_as_uint(hch) | ((uint64_t)sslot << 32));
 #pragma unroll
         for (int wj = 0; wj < W; ++wj) st64(e + 2 + wj, hib.word(wj));
 #pragma unroll
         for (int wj = 0; wj < W; ++wj) st64(e + 2 + W + wj, ow[wj]);
     } else if (act) {
         const float o = dom ? absent_f() : -ts;
-        slab_st(a, a.table + slot, o);
-        if (hsub_on) slab_st(a, a.hsub + slot, fmaxf(o, hch));
+        a.table[sslot] = o;
+        a.ptab[slot] = o;
+        if (hsub_on) a.phsub[slot] = fmaxf(o, hch);
     }
     if (nq) {
         // the entries are written: count them into their walk chunks
@@ -304,6 +454,8 @@ __device__ __forceinline__ int tile_twopass(const PipeArgs &a, const PipeShared 
     const uint8_t *cl = a.cand + vi * 64;
     // the subset maxima of the top layer's phase 1 are never read
     const bool hsub_on = !(L == a.kmax && PH == 1);
+    Slabs sl;
+    load_slabs(a, vi, L, sl);
     int cnt = 0;
     uint32_t queued = 0;
     const uint64_t tq0 = a.stats ? wall_clock64() : 0;
@@ -312,7 +464,8 @@ __device__ __forceinline__ int tile_twopass(const PipeArgs &a, const PipeShared 
         const bool valid = idx < st.nsets;
         if (!wave_any(valid)) break;
         bool need = false;
-        uint64_t cm = 0, slot = 0;
+        uint64_t cm = 0;
+        uint32_t slot = 0, sslot = 0;
         float ts = 0.0f, hch = absent_f();
         if (valid) {
             if (PH == 0) cm = (unrank_colex(idx, L - 1, m - 1, sh.binom) << 1) | 1ull;
@@ -330,13 +483,14 @@ __device__ __forceinline__ int tile_twopass(const PipeArgs &a, const PipeShared 
                 }
             }
             ts = cbic_set_score<L>(sh.g, a.n, v, gv, a.N, a.lambda);
-            slot = sh.toff[vbase + L] + rankP;
+            slot = (PH == 0 ? sl.o0[L] : sl.o1[L]) + idx;
+            sslot = (uint32_t)(sh.toff[vbase + L] + rankP);
             // 1. settle by the subset maxima (score_layer_kernel, variant 113)
-            uint64_t rc[L], rz[L];
-            child_ranks<L, PH == 1>(cm, sh.binom, rc, rz);
+            uint32_t ca[L], za[L];
+            work_children<L, PH>(cm, z, sh.binom, sl, ca, za);
             if constexpr (L > 1) {
 #pragma unroll
-                for (int i = 0; i < L; ++i) hch = fmaxf(hch, ldf(a.hsub + sh.toff[vbase + L - 1] + rc[i]));
+                for (int i = 0; i < L; ++i) hch = fmaxf(hch, ldw(a.phsub + ca[i]));
             }
             float out;
             if (ts >= 0.0f) {
@@ -348,7 +502,7 @@ __device__ __forceinline__ int tile_twopass(const PipeArgs &a, const PipeShared 
                 if constexpr (PH == 1) {
                     if (z) {
 #pragma unroll
-                        for (int i = 0; i < L; ++i) hu = fmaxf(hu, ldf(a.hsub + sh.toff[vbase + L] + rz[i]));
+                        for (int i = 0; i < L; ++i) hu = fmaxf(hu, ldw(a.phsub + za[i]));
                     }
                 }
                 out = -ts;
@@ -356,15 +510,16 @@ __device__ __forceinline__ int tile_twopass(const PipeArgs &a, const PipeShared 
                     bool dh = false;
                     if constexpr (L > 1) {
 #pragma unroll
-                        for (int i = 0; i < L; ++i) dh |= ldf(a.table + sh.toff[vbase + L - 1] + rc[i]) >= thr;
+                        for (int i = 0; i < L; ++i) dh |= ldw(a.ptab + ca[i]) >= thr;
                     }
                     out = absent_f();
                     need = !dh;
                 }
             }
             if (!need) {
-                slab_st(a, a.table + slot, out);
-                if (hsub_on) slab_st(a, a.hsub + slot, fmaxf(out, hch));
+                a.table[sslot] = out;
+                a.ptab[slot] = out;
+                if (hsub_on) a.phsub[slot] = fmaxf(out, hch);
             }
         }
         // 2. pool the undecided sets; gather on dense lanes
@@ -372,7 +527,8 @@ __device__ __forceinline__ int tile_twopass(const PipeArgs &a, const PipeShared 
         if (valid && need) {
             const int pos = cnt + __popcll(nm & ((1ull << lane) - 1ull));
             P.cm[pos] = cm;
-            P.slot[pos] = (uint32_t)slot;
+            P.slot[pos] = slot;
+            P.sslot[pos] = sslot;
             P.ts[pos] = ts;
             P.hch[pos] = hch;
         }
@@ -382,7 +538,7 @@ __device__ __forceinline__ int tile_twopass(const PipeArgs &a, const PipeShared 
     const uint64_t tq1 = a.stats ? wall_clock64() : 0;
     // 3. the pooled sets on dense lanes, 64 at a time
     for (int off = 0; off < cnt; off += 64)
-        pool_drain<L, PH>(a, sh, vi, s, P, off, cnt - off < 64 ? cnt - off : 64, lane, queued, hsub_on);
+        pool_drain<L, PH>(a, sh, vi, s, P, off, cnt - off < 64 ? cnt - off : 64, lane, queued, hsub_on, sl);
     if (a.stats) {
         const uint64_t tq2 = wall_clock64();
         drain();
@@ -459,17 +615,18 @@ __device__ __forceinline__ int walk_chunk(const PipeArgs &a, int vi, int s, uint
     for (int k = 0; k < K; ++k) {
         if (mine + k >= endq) break;
         const uint64_t *en = q0 + (uint64_t)(mine + k) * EW;
-        const uint64_t e0 = ld64(en);
+        const uint64_t e0 = ld64(en), e1 = ld64(en + 1);
         const float ts = __uint_as_float((uint32_t)(e0 >> 32));
-        const float hch = __uint_as_float((uint32_t)ld64(en + 1));
+        const float hch = __uint_as_float((uint32_t)e1);
         const bool d = (dom >> k) & 1u;
-        const uint32_t slot = (uint32_t)e0;
-        if (slot >= a.total_slots) {  // never: an entry read before it was written (protocol bug)
+        const uint32_t slot = (uint32_t)e0, sslot = (uint32_t)(e1 >> 32);
+        if (slot >= a.work_slots || sslot >= a.total_slots) {  // never: an entry read before it was written
             st32(a.done + 1, 2u);
             continue;
         }
-        slab_st(a, a.table + slot, d ? absent_f() : -ts);
-        if (hsub_on) slab_st(a, a.hsub + slot, d ? hch : fmaxf(hch, -ts));
+        a.table[sslot] = d ? absent_f() : -ts;
+        a.ptab[slot] = d ? absent_f() : -ts;
+        if (hsub_on) a.phsub[slot] = d ? hch : fmaxf(hch, -ts);
     }
     return stage_add(a, vi, s, (uint64_t)e, lane);
 }
@@ -714,6 +871,7 @@ int pipe_prepare(ulg_ctx *c, int nv, int S, int kmax, int max_parents, const std
     std::vector<PipeStage> stages((size_t)nv * NS);
     std::vector<uint32_t> first(nv, kDone);
     uint64_t qwords = 0, fills = 0;
+    uint64_t wslots = 32;  // line 0: never written (the gathers' masked lanes load it)
     for (int vi = 0; vi < nv; ++vi) {
         const int m = mv[vi];
         const bool z = meta[vi * 4 + 2] != 0;
@@ -728,6 +886,9 @@ int pipe_prepare(ulg_ctx *c, int nv, int S, int kmax, int max_parents, const std
             st.ntiles = (uint32_t)((cnt + per - 1) / per);
             st.qoff = qwords;
             st.foff = (uint32_t)fills;
+            st.slab = (uint32_t)wslots;
+            st.pad = 0;
+            wslots += (cnt + 31) / 32 * 32;  // whole 128-byte lines per stage
             st.next = kDone;
             if (L > Ls && cnt > 0) {
                 qwords += cnt * (uint64_t)pipe_entry_words(L);
@@ -752,6 +913,8 @@ int pipe_prepare(ulg_ctx *c, int nv, int S, int kmax, int max_parents, const std
     if ((rc = ensure(c, c->d_pstate, state_bytes)) || (rc = ensure(c, c->d_pqueue, (size_t)std::max<uint64_t>(qwords, 1))) ||
         (rc = ensure(c, c->d_pinit, (size_t)nv)))
         return rc;
+    if (2 * wslots >= 0xFFFFFFFFull) return set_err(c, ULG_ERR_UNSUPPORTED, "pipe: work layout too large");
+    if ((rc = ensure(c, c->d_pwork, (size_t)(2 * wslots)))) return rc;
     std::vector<uint8_t> sbytes(stages.size() * sizeof(PipeStage));
     std::memcpy(sbytes.data(), stages.data(), sbytes.size());
     if ((rc = upload(c, c->d_pstages, c->mir_pstages, sbytes))) return rc;
@@ -769,7 +932,8 @@ int pipe_prepare(ulg_ctx *c, int nv, int S, int kmax, int max_parents, const std
     a.meta = c->d_meta.p;
     a.tbl_off = c->d_tbl_off.p;
     a.table = c->table.p;
-    a.hsub = c->d_hsub.p;
+    a.ptab = c->d_pwork.p;
+    a.phsub = c->d_pwork.p + wslots;
     a.N = (double)c->N;
     a.lambda = c->lambda;
     a.n = c->n;
@@ -781,8 +945,8 @@ int pipe_prepare(ulg_ctx *c, int nv, int S, int kmax, int max_parents, const std
     a.R = R;
     a.Rsmall = Rs;
     a.chain = c->pipe_chain;
-    a.plain = c->pipe_plain;
     a.total_slots = (uint32_t)(c->table.cap < 0xFFFFFFFFull ? c->table.cap : 0xFFFFFFFFull);
+    a.work_slots = (uint32_t)wslots;
     a.stats = nullptr;
     if (std::getenv("ULG_PIPE_STATS")) {
         if ((rc = ensure(c, c->d_pstats, 16))) return rc;

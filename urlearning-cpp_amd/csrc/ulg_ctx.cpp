@@ -167,7 +167,7 @@ void ulg_destroy(ulg_ctx *c) {
     release(c->raw); release(c->z); release(c->gram); release(c->partials); release(c->colstat);
     release(c->table); release(c->d_tbl_off); release(c->d_work); release(c->d_blk);
     release(c->d_cand); release(c->d_meta); release(c->d_binom); release(c->d_binom64); release(c->d_wqueue); release(c->d_wbits); release(c->d_stats); release(c->d_dump); release(c->d_queue); release(c->d_qcount); release(c->d_workg); release(c->d_vwork); release(c->d_hq); release(c->d_hqc); release(c->d_hmax); release(c->d_hoff); release(c->d_hmeta); release(c->d_scount); release(c->d_hsub);
-    release(c->d_pstate); release(c->d_pqueue); release(c->d_pstages); release(c->d_pinit); release(c->d_pstats);
+    release(c->d_pstate); release(c->d_pqueue); release(c->d_pstages); release(c->d_pinit); release(c->d_pstats); release(c->d_pwork);
     release(c->out_sets); release(c->out_scores); release(c->out_offsets);
     release(c->qbuf_in); release(c->qbuf_out);
     pss_release(c);
@@ -234,11 +234,6 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
     if (std::strcmp(name, "pipe_grid_max") == 0) {
         if (value < 0 || value > (1 << 20)) return set_err(c, ULG_ERR_ARG, "pipe_grid_max must be 0..2^20");
         c->pipe_grid_max = (int)value;
-        return ULG_OK;
-    }
-    if (std::strcmp(name, "pipe_plain") == 0) {
-        if (value < 0 || value > 1) return set_err(c, ULG_ERR_ARG, "pipe_plain must be 0 or 1");
-        c->pipe_plain = (int)value;
         return ULG_OK;
     }
     if (std::strcmp(name, "pipe_rounds") == 0) {
