@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--options", default="")
     ap.add_argument("--lib", default=None, help="another build of libulg.so (timing experiments)")
+    ap.add_argument("--modes", type=int, nargs="+", default=[0, 1], help="score_pipe values to run (0: layers only)")
     a = ap.parse_args()
     if a.lib:
         ulg.LIB_PATH = os.path.abspath(a.lib)
@@ -65,7 +66,7 @@ def main():
             ctx.load(X, 2.0)
             variables, cands = cands_for(n, kind, n)
             res, ms = {}, {}
-            for pipe in (0, 1):  # the context default is whatever ulg_internal.h says
+            for pipe in a.modes:  # the context default is whatever ulg_internal.h says
                 ctx.set_option("score_pipe", pipe)
                 st, _ = ctx.score(variables, cands, k)
                 res[pipe] = ctx.fetch(st)
@@ -75,19 +76,21 @@ def main():
                 if any(np.asarray(x).tobytes() != np.asarray(y).tobytes() for x, y in zip(res[pipe], again)):
                     print(json.dumps({"case": name, "n": n, "pipe": pipe, "error": "not deterministic"}), flush=True)
                     ok = False
-            same = all(np.asarray(x).tobytes() == np.asarray(y).tobytes() for x, y in zip(res[0], res[1]))
+            m0, m1 = a.modes[0], a.modes[-1]
+            same = all(np.asarray(x).tobytes() == np.asarray(y).tobytes() for x, y in zip(res[m0], res[m1]))
             ok &= same
             if name == "c3":  # against the oracle command lines' digests too
                 import hashlib
                 ref = json.load(open(os.path.join(ROOT, "tests", "golden", "c3_oracle.json")))
-                offs, sets = res[1][0], res[1][1]
+                offs, sets = res[m1][0], res[m1][1]
                 for v in range(n):
                     srt = np.sort(np.asarray(sets[offs[v]:offs[v + 1]]).astype(np.uint64))
                     if hashlib.sha256(srt.tobytes()).hexdigest() != ref["sets_sha256_per_variable"][v]:
                         print(json.dumps({"case": name, "error": f"variable {v} differs from c3_oracle.json"}))
                         ok = False
             print(json.dumps({"case": name, "n": n, "N": N, "k": k, "kind": kind, "identical": same,
-                              "stored": int(res[1][0][-1]), "layers_ms": ms[0], "pipe_ms": ms[1]}), flush=True)
+                              "stored": int(res[m1][0][-1]), "layers_ms": ms.get(0), "pipe_ms": ms.get(1),
+                              "options": a.options, "sliced_k": os.environ.get("ULG_SLICED_K")}), flush=True)
     ctx.close()
     sys.exit(0 if ok else 1)
 

@@ -1670,7 +1670,7 @@ SlicedFn sliced_fn_wide(int L, int phase) {
 // waves to hide the walk's latency
 // sets per lane of the bit-sliced walk: 2 up to layer 5 (more, smaller
 // unions), 4 above (C3: layer 5 0.58 -> 0.54 ms, layer 6 best at 4 or 8);
-// ULG_SLICED_K=2|4|8 overrides for A/B
+// ULG_SLICED_K=1|2|4|8 overrides for A/B
 constexpr int kSlicedKSmall = 2;  // default sets per lane up to layer 5
 int sliced_k(int L) {
     if (L >= 7) return L == 7 ? 2 : 1;
@@ -1681,13 +1681,14 @@ int sliced_k(int L) {
         const char *comma = std::strchr(e, ',');
         k = (L <= 5 || !comma) ? std::atoi(e) : std::atoi(comma + 1);
     }
-    return (k == 2 || k == 8) ? k : 4;
+    return (k == 1 || k == 2 || k == 8) ? k : 4;
 }
 // queued sets per walk wave
 uint64_t walk_sets_per_wave(int L) { return 64ull * (uint64_t)sliced_k(L); }
 SlicedFn sliced_fn(int L, int phase) {
     if (L >= 7) return sliced_fn_wide(L, phase);
     switch (sliced_k(L)) {
+        case 1: return sliced_fn_k<1>(L, phase);
         case 2: return sliced_fn_k<2>(L, phase);
         case 4: return sliced_fn_k<4>(L, phase);
         default: return sliced_fn_k<8>(L, phase);
@@ -2355,9 +2356,9 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     sa.nv = nv;
     sa.S = S;
     sa.xcd = c->score_xcd;
-    // queue entries address the table with 32 bits; beyond that the one-pass
-    // form (identical results) is used
-    const int variant = (c->score_variant & 16) && (total_slots >> 32) ? 1 : c->score_variant;
+    // tables of 2^30 slots or more: the one-pass form with 64-bit slots (the
+    // others keep 32-bit byte offsets in their gathers and slots in entries)
+    const int variant = (total_slots >> 30) ? 1 : c->score_variant;
     if (variant & 64) {
         if ((rc = ensure(c, c->d_hsub, total_slots))) return rc;
         sa.hsub = c->d_hsub.p;

@@ -304,10 +304,17 @@ struct PresList {
 // batches of NB before any of their values is used: the gather is a chain of
 // independent loads, and issued one at a time (what the compiler makes of a
 // load-then-test loop) every load pays the full memory latency.
-template <int L, int PHASE, int Q, int W, class LD = LdPlain, int NB = 16>
+//
+// B32: every slot below 2^30, so a key's byte offset fits 32 bits: the rank
+// sums stay in 32-bit registers and each load is a global_load with the
+// table base in SGPRs and a 32-bit VGPR offset (one address register per
+// pending load instead of a 64-bit pair).  !B32 (tables of 2^30 slots or
+// more, the one-pass variant 1 only): 64-bit slot arithmetic.
+template <int L, int PHASE, int Q, int W, class LD = LdPlain, int NB = 16, bool B32 = true>
 __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi, float thr, const uint32_t *binom,
                                                   uint64_t cpack, bool z, const float *table, const uint64_t *toffv) {
     constexpr PresList<L, PHASE, Q> PL{};
+    using Slot = std::conditional_t<B32, uint32_t, uint64_t>;
     uint32_t RB[Q][L + 1];
 #pragma unroll
     for (int lb = 0; lb < Q; ++lb) {
@@ -315,9 +322,12 @@ __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi,
 #pragma unroll
         for (int p = 1; p <= L; ++p) RB[lb][p] = (p <= lb + 1) ? B(binom, ci, p) : 0u;
     }
-    uint64_t off[L + 1];
+    Slot off[L + 1];
 #pragma unroll
-    for (int pc = 1; pc <= L; ++pc) off[pc] = toffv[pc];
+    for (int pc = 1; pc <= L; ++pc) off[pc] = (Slot)toffv[pc];
+    uint32_t pw[2 * W], hw[2 * W];  // the bitsets as 32-bit halves: a constant bit touches one
+#pragma unroll
+    for (int j = 0; j < 2 * W; ++j) pw[j] = hw[j] = 0u;
 #pragma clang loop unroll(full)
     for (int b0 = 0; b0 < PL.n; b0 += NB) {
         // opaque per batch: no rank partial sum is shared across batches, so
@@ -333,7 +343,7 @@ __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi,
             if (b0 + i >= PL.n) break;
             const uint32_t t = PL.t[b0 + i];
             const int pc = popc_c(t);
-            uint64_t rk = 0;
+            Slot rk = off[pc];
             int jj = 0;
 #pragma unroll
             for (int b = 0; b < Q; ++b)
@@ -342,21 +352,36 @@ __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi,
                     rk += RB[b][jj];
                 }
             // a key with variable 0 exists only when variable 0 is a
-            // candidate (z); otherwise the lane loads slot 0 and ignores it
-            const bool ok = !(t & 1u) || z;
-            v[i] = LD::ld(table + (ok ? off[pc] + rk : 0ull));
+            // candidate (z); otherwise the lane loads slot 0 and reads it as
+            // absent
+            if (t & 1u) rk = z ? rk : (Slot)0;
+            if constexpr (B32)
+                v[i] = LD::ld(reinterpret_cast<const float *>(reinterpret_cast<const char *>(table) + (rk << 2)));
+            else
+                v[i] = LD::ld(table + rk);
         }
 #pragma clang loop unroll(full)
         for (int i = 0; i < NB; ++i) {
             if (b0 + i >= PL.n) break;
             const uint32_t t = PL.t[b0 + i];
-            const bool ok = !(t & 1u) || z;
-            if (ok && fbits(v[i]) != kAbsentBits) present.set(t);
-            if (ok && v[i] >= thr) hi.set(t);  // the absent sentinel is a NaN: never >= thr
+            float x = v[i];
+            if (t & 1u) x = z ? x : absent_f();
+            const uint32_t bit = 1u << (t & 31u);
+            pw[t >> 5] |= (fbits(x) != kAbsentBits) ? bit : 0u;
+            hw[t >> 5] |= (x >= thr) ? bit : 0u;  // the absent sentinel is a NaN: never >= thr
         }
+        // pinned here: the IR passes would otherwise sink every test below
+        // the last batch and hold all the loaded values at once
+#pragma unroll
+        for (int j = 0; j < 2 * W; ++j) asm volatile("" : "+v"(pw[j]), "+v"(hw[j]));
         // keep the batches apart: hoisting every load of the unrolled loop
         // would hold all 2^Q values in registers at once
         __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+        present.w[j] |= (uint64_t)pw[2 * j] | ((uint64_t)pw[2 * j + 1] << 32);
+        hi.w[j] |= (uint64_t)hw[2 * j] | ((uint64_t)hw[2 * j + 1] << 32);
     }
 }
 
@@ -407,13 +432,14 @@ __device__ __forceinline__ LocalSet<L> local_set(uint64_t cm, bool z) {
 
 // Presence of every candidate key below P u {var 0} in the cache as it
 // stands now (`present`), and which of them hold a value >= thr (`hi`).
+// V == 1 is the form kept for tables of 2^30 slots or more (64-bit slots)
 template <int L, int PHASE, int V, class BS, class LD = LdPlain>
 __device__ __forceinline__ void gather_keys(BS &present, BS &hi, const LocalSet<L> &ls, float thr,
                                             const uint32_t *binom, bool z, const float *table,
                                             const uint64_t *toffv) {
     constexpr int W = BS::kWords;
     if constexpr (L <= 6 && (V & 1)) {
-        presence_unrolled<L, PHASE, (PHASE == 0 ? L : L + 1), W, LD>(present, hi, thr, binom, ls.cpack, z, table,
+        presence_unrolled<L, PHASE, (PHASE == 0 ? L : L + 1), W, LD, 8, (V != 1)>(present, hi, thr, binom, ls.cpack, z, table,
                                                                       toffv);
     } else {
         const int q = ls.v0inP ? L : L + 1;
