@@ -168,13 +168,14 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, int on) {
 }
 
 
-// LDS carve: gram | binom | work | tbl_off | recursion stack (variant bit 1)
+// LDS carve: gram | binom | work | tbl_off | meta | candidate lists |
+// recursion stack (variant bit 1)
 // | LDS bitsets (3 per lane when they have >= 4 words) | the block's
 // undecided sets after the subset-maxima test (variant bits 4 + 6: a count,
 // then per entry compact mask, slot, ts, children maximum, variable) (16-B
 // aligned)
 struct LdsLayout {
-    int gram, binom, work, toff, stack, bits, cmp, total;
+    int gram, binom, work, toff, meta, cand, stack, bits, cmp, total;
 };
 constexpr int kCmpEntryBytes = 8 + 4 + 4 + 4 + 4;
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
@@ -184,7 +185,9 @@ __host__ __device__ inline LdsLayout lds_layout(int n, int nv, int S, int L, int
     l.binom = align16(l.gram + n * n * 8);
     l.work = align16(l.binom + 64 * kBinomK * 4);
     l.toff = align16(l.work + (nv + 1) * 8);
-    l.stack = align16(l.toff + (nv * S + 1) * 8);
+    l.meta = align16(l.toff + (nv * S + 1) * 8);
+    l.cand = align16(l.meta + nv * 4 * 4);
+    l.stack = align16(l.cand + nv * 64);
     l.bits = l.stack;
     const int W = bits_words(L);
     l.cmp = align16(l.bits + (W >= 4 ? 3 * W * kBlock * 8 : 0));
@@ -226,11 +229,22 @@ __device__ __forceinline__ void queue_walk(const BS &present, const BS &hi, uint
 }
 
 
+#ifdef ULG_LAYER_STATS
+// timing diagnostics of the two-pass layer kernels (A/B builds only): per
+// (layer, phase) the wave-time sums of init, score, settle, compact, gather
+// and the wave / gather-lane counts, in 100 MHz wall-clock ticks
+__device__ unsigned long long g_lstat[64][2][kMaxL + 1][8];  // 64 copies: few atomics per address
+#define LSTAT_T(x) const uint64_t x = wall_clock64()
+#else
+#define LSTAT_T(x)
+#endif
+
 // PHASE 0: sets containing variable 0; 1: the rest.  V = variant bits (see
 // ulg_set_option "score_variant"), compile-time so each form gets its own
 // register allocation.
 template <int L, int PHASE, int V>
 __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
+    LSTAT_T(t0);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const LdsLayout lay = lds_layout(a.n, a.nv, a.S, L, V);
     double *g = reinterpret_cast<double *>(smem + lay.gram);
@@ -241,10 +255,20 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
     for (int i = threadIdx.x; i < 64 * kBinomK; i += kBlock) binom[i] = a.binom[i];
     for (int i = threadIdx.x; i <= a.nv; i += kBlock) work[i] = a.work[i];
     for (int i = threadIdx.x; i <= a.nv * a.S; i += kBlock) toff[i] = a.tbl_off[i];
+    // the per-variable metadata and candidate lists too: every lane reads
+    // them right after its variable is known, and from global memory those
+    // would be two more dependent round trips per lane
+    int *smeta = reinterpret_cast<int *>(smem + lay.meta);
+    uint8_t *scand = reinterpret_cast<uint8_t *>(smem + lay.cand);
+    for (int i = threadIdx.x; i < a.nv * 4; i += kBlock) smeta[i] = a.meta[i];
+    for (int i = threadIdx.x; i < a.nv * 16; i += kBlock)
+        reinterpret_cast<uint32_t *>(scand)[i] = reinterpret_cast<const uint32_t *>(a.cand)[i];
     __syncthreads();
+    LSTAT_T(t1);
 
     constexpr bool HM = (V & 64) != 0;           // subset maxima kept up to date
     constexpr bool CMP = HM && (V & 16) != 0;     // ... and the sets settled by them first
+    constexpr bool FUSE = CMP && (V & 128) != 0 && L <= 6;  // ... and the open sets walked in this kernel
     const uint64_t gid0 = (uint64_t)xcd_block(blockIdx.x, gridDim.x, a.xcd) * kBlock + threadIdx.x;
     const bool valid = gid0 < work[a.nv];
     if (!CMP && !valid) return;
@@ -257,9 +281,9 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         if (work[mid] <= gid) lo = mid; else hi = mid;
     }
     const int vi = lo;
-    const int v = a.meta[vi * 4 + 0];
-    const int m = a.meta[vi * 4 + 1];
-    const bool z = a.meta[vi * 4 + 2] != 0;
+    const int v = smeta[vi * 4 + 0];
+    const int m = smeta[vi * 4 + 1];
+    const bool z = smeta[vi * 4 + 2] != 0;
     const uint64_t r = gid - work[vi];
 
     uint64_t cm;  // compact mask of P over the variable's candidate list
@@ -269,7 +293,7 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
     const uint64_t rankP = rank_colex(cm, binom);
 
     // parent variables in ascending order (== BIC_OLS parent_vec order)
-    const uint8_t *cl = a.cand + vi * 64;
+    const uint8_t *cl = scand + vi * 64;
     int gv[L];
     {
         uint64_t rem = cm;
@@ -282,7 +306,20 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
     }
 
     const float ts = cbic_set_score<L>(g, a.n, v, gv, a.N, a.lambda);
+#ifdef ULG_AB_SCORE2
+    {  // timing A/B only: the score computed twice (the copy kept alive by an asm use)
+        int gv2[L];
+#pragma unroll
+        for (int i = 0; i < L; ++i) {
+            gv2[i] = gv[i];
+            asm volatile("" : "+v"(gv2[i]));
+        }
+        const float t2 = cbic_set_score<L>(g, a.n, v, gv2, a.N, a.lambda);
+        asm volatile("" ::"v"(t2));
+    }
+#endif
 
+    LSTAT_T(t2);
     if constexpr (CMP) {
         // 1. settle by the subset maxima: ts >= 0, no key >= -ts in U(P), or a
         //    present direct child >= -ts (always visited at the top level)
@@ -290,10 +327,33 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         const uint64_t slot = toff[vbase + L] + rankP;
         uint64_t rc[L], rz[L];
         child_ranks<L, PHASE == 1>(cm, binom, rc, rz);
+        // every load of the settle issued at once (the children's maxima and
+        // values, the var-0 toggles' maxima): one memory round trip instead
+        // of up to three dependent ones
         float hch = absent_f();  // max over the proper nonempty subsets of P
-        if constexpr (L > 1) {
+        float hz = absent_f();   // ... and over the toggles P\a + {0}
+        bool dh = false;         // a direct child >= -ts
+        {
+            float ch[L], cv[L], zv[L];
+            const uint32_t o1 = (uint32_t)toff[vbase + L - 1], o0 = (uint32_t)toff[vbase + L];
 #pragma unroll
-            for (int i = 0; i < L; ++i) hch = fmaxf(hch, a.hsub[toff[vbase + L - 1] + rc[i]]);
+            for (int i = 0; i < L; ++i) {
+                if constexpr (L > 1) {
+                    ch[i] = a.hsub[o1 + (uint32_t)rc[i]];
+                    cv[i] = a.table[o1 + (uint32_t)rc[i]];
+                }
+                if constexpr (PHASE == 1) zv[i] = a.hsub[(z ? o0 : 0u) + (z ? (uint32_t)rz[i] : 0u)];
+            }
+            const float thr = -ts;
+#pragma unroll
+            for (int i = 0; i < L; ++i) {
+                if constexpr (L > 1) {
+                    hch = fmaxf(hch, ch[i]);
+                    dh |= cv[i] >= thr;
+                }
+                if constexpr (PHASE == 1) hz = fmaxf(hz, zv[i]);
+            }
+            if (!z) hz = absent_f();
         }
         bool need = false;
         float out;
@@ -302,20 +362,9 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
             out = (s < 0.0f) ? s : absent_f();
         } else {
             const float thr = -ts;
-            float hu = hch;
-            if constexpr (PHASE == 1) {
-                if (z) {
-#pragma unroll
-                    for (int i = 0; i < L; ++i) hu = fmaxf(hu, a.hsub[toff[vbase + L] + rz[i]]);
-                }
-            }
+            const float hu = fmaxf(hch, hz);
             out = -ts;
             if (hu >= thr) {
-                bool dh = false;
-                if constexpr (L > 1) {
-#pragma unroll
-                    for (int i = 0; i < L; ++i) dh |= a.table[toff[vbase + L - 1] + rc[i]] >= thr;
-                }
                 out = absent_f();
                 need = !dh;
             }
@@ -324,6 +373,7 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
             a.table[slot] = out;
             a.hsub[slot] = fmaxf(out, hch);
         }
+        LSTAT_T(t3);
         // 2. the rest of the block's sets, compacted in LDS, so the presence
         //    gathers (2^(L+1) reads each) run on dense waves
         unsigned int *cnt = reinterpret_cast<unsigned int *>(smem + lay.cmp);
@@ -343,10 +393,32 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
             evi[k] = vi;
         }
         __syncthreads();
+        LSTAT_T(t4);
+#ifdef ULG_LAYER_STATS
+        const bool gl = threadIdx.x < *cnt;
+        auto lstat = [&](uint64_t t5) {
+            if ((threadIdx.x & 63) == 0) {
+                unsigned long long *st = g_lstat[blockIdx.x & 63][PHASE][L];
+                atomicAdd(st + 0, (unsigned long long)(t1 - t0));
+                atomicAdd(st + 1, (unsigned long long)(t2 - t1));
+                atomicAdd(st + 2, (unsigned long long)(t3 - t2));
+                atomicAdd(st + 3, (unsigned long long)(t4 - t3));
+                atomicAdd(st + 4, (unsigned long long)(t5 - t4));
+                atomicAdd(st + 5, 1ull);
+            }
+            const unsigned long long ng = (unsigned long long)__popcll(__ballot(gl));
+            if ((threadIdx.x & 63) == 0) atomicAdd(g_lstat[blockIdx.x & 63][PHASE][L] + 6, ng);
+        };
+        if (!gl) {
+            lstat(t4);
+            return;
+        }
+#else
         if (threadIdx.x >= *cnt) return;
+#endif
         const int k = threadIdx.x;
         const int vk = evi[k];
-        const bool zk = a.meta[vk * 4 + 2] != 0;
+        const bool zk = smeta[vk * 4 + 2] != 0;
         const float tk = ets[k];
         const uint64_t sk = eslot[k];
         constexpr int W = bits_words(L);
@@ -358,9 +430,53 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         present.clear();
         hib.clear();
         gather_keys<L, PHASE, V>(present, hib, ls, -tk, binom, zk, a.table, toff + (uint64_t)vk * a.S);
+#ifdef ULG_AB_GATHER2
+        if constexpr (W < 4) {  // timing A/B only: the gathers run twice (kept alive by asm uses)
+            LocalSet<L> ls2 = ls;
+            asm volatile("" : "+v"(ls2.cpack));
+            BS p2, h2;
+            p2.clear();
+            h2.clear();
+            gather_keys<L, PHASE, V>(p2, h2, ls2, -tk, binom, zk, a.table, toff + (uint64_t)vk * a.S);
+#pragma unroll
+            for (int j = 0; j < W; ++j) asm volatile("" ::"v"(p2.w[j]), "v"(h2.w[j]));
+        }
+#endif
         bool q;
         const bool dom = settle_rules<L, PHASE>(present, hib, ls, q);
-        if (q) {
+        if constexpr (FUSE) {
+            // variant bit 7: the sets the rules leave open are walked right
+            // here, by this wave's lanes (the bit-sliced walk with one set per
+            // lane: each lane's own bitsets are its registers), instead of
+            // through the queue and a walk launch
+            using SK = Sliced<L, 1>;
+            typename SK::Vec hiV, openV;
+            uint64_t ow[W];
+#pragma unroll
+            for (int wj = 0; wj < W; ++wj) ow[wj] = hib.word(wj);
+            cover_words<W>(ow);
+#pragma unroll
+            for (int wj = 0; wj < W; ++wj) {
+                const uint64_t ce = ow[wj] & 0x5555555555555555ull;
+                ow[wj] = (ce | (ce << 1)) & ~present.word(wj) & (wj == 0 ? ~1ull : ~0ull);
+            }
+#pragma unroll
+            for (int r = 0; r < SK::NV; ++r) {
+                hiV[r] = r < SK::NV0 ? (uint32_t)(hib.word(r >> 1) >> (32 * (r & 1))) : 0u;
+                openV[r] = r < SK::NV0 ? (uint32_t)(ow[r >> 1] >> (32 * (r & 1))) : 0u;
+            }
+            constexpr bool v0inP = PHASE == 0;
+            constexpr uint32_t Plocal = v0inP ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
+            uint32_t pvtop = 0;
+#pragma unroll
+            for (int i = 0; i < L; ++i) pvtop |= (uint32_t)(i + (v0inP ? 0 : 1)) << (4 * i);
+            uint32_t alive = q ? 1u : 0u, wd = 0u, pts = 0u;
+            walk_sliced<L, 1, L>(Plocal, pvtop, alive, hiV, openV, alive, wd, pts);
+            const bool dd = q ? (wd & 1u) != 0u : dom;
+            const float o = dd ? absent_f() : -tk;
+            a.table[sk] = o;
+            a.hsub[sk] = fmaxf(o, ehch[k]);
+        } else if (q) {
             queue_walk(present, hib, a.queue, a.qcount, sk, tk);
             a.hsub[sk] = ehch[k];  // the walk raises it to -ts if it stores P
         } else {
@@ -368,6 +484,9 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
             a.table[sk] = o;
             a.hsub[sk] = fmaxf(o, ehch[k]);
         }
+#ifdef ULG_LAYER_STATS
+        lstat(wall_clock64());
+#endif
         return;
     }
 
@@ -1608,7 +1727,8 @@ KernelFn pick_phase(int phase) {
 // bit 5 bit-sliced walk, bit 6 subset maxima.  1: one-pass; 65: one-pass with
 // the subset maxima (the small layers of 113); 17 / 49: two-pass with the
 // per-lane / bit-sliced walk; 81 / 113: the same with the subset maxima (113
-// is the default).  Round 1's other forms (loop gathers at every layer, a
+// is the default); 241: 113 with bit 7, the open sets of layers <= 6 walked
+// in the scoring kernel itself (one set per lane, no queue, no walk launch).  Round 1's other forms (loop gathers at every layer, a
 // stack-machine recursion, a decision-only per-lane walk, the statistics
 // build) were measured slower and are gone.
 template <int L>
@@ -1618,6 +1738,7 @@ KernelFn pick(int phase, int variant) {
         case 17: case 49: return pick_phase<L, 17>(phase);
         case 65: return pick_phase<L, 65>(phase);
         case 81: case 113: return pick_phase<L, 81>(phase);
+        case 241: return L <= 6 ? pick_phase<L, 209>(phase) : pick_phase<L, 81>(phase);
         default: return nullptr;
     }
 }
@@ -2627,7 +2748,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                 prof_begin_s(c, kLayerNames[ph][L], st);
                 hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(kBlock), (size_t)lay.total, st, sa);
                 prof_end_s(c, st);
-                if (variant & 16) {
+                if ((variant & 16) && !((variant & 128) && L <= 6)) {
                     // the undecided lanes of this launch, densely packed
                     if ((variant & 32) && sliced_fn(L, ph)) {
                         const uint64_t per = walk_sets_per_wave(L);
@@ -2787,6 +2908,27 @@ launched:
         if ((rc = pipe_check(c))) return rc;
         pipe_report(c);
     }
+#ifdef ULG_LAYER_STATS
+    {
+        static unsigned long long h[64][2][kMaxL + 1][8];
+        if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_lstat), sizeof h) == hipSuccess) {
+            for (int L = 1; L <= kMaxL; ++L)
+                for (int ph = 0; ph < 2; ++ph) {
+                    unsigned long long x[8] = {0};
+                    for (int cp = 0; cp < 64; ++cp)
+                        for (int i = 0; i < 8; ++i) x[i] += h[cp][ph][L][i];
+                    if (!x[5]) continue;
+                    const double w = (double)x[5] * 100.0;  // ticks (100 MHz) -> us, per wave
+                    std::fprintf(stderr,
+                                 "layer_stats L%d p%d waves=%llu gather_lanes/wave=%.1f per-wave us: init %.2f score %.2f "
+                                 "settle %.2f compact %.2f gather %.2f\n",
+                                 L, ph, x[5], (double)x[6] / x[5], x[0] / w, x[1] / w, x[2] / w, x[3] / w, x[4] / w);
+                }
+            std::memset(h, 0, sizeof h);
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lstat), h, sizeof h);
+        }
+    }
+#endif
     if (wide_err)
         return set_err(c, ULG_ERR_UNSUPPORTED,
                        "ulg_cbic_score: a find_best_subset_score walk in a wide layer exceeded its cap (2^30 steps "
