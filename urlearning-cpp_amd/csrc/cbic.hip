@@ -155,6 +155,7 @@ struct ScoreArgs {
     double lambda;
     int n, nv, S;
     int xcd;                    // remap blocks so each XCD takes a contiguous run of sets
+    int hsub_out;               // write the subset maxima (0: the top layer's phase 1, never read)
 };
 
 // Blocks are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8),
@@ -371,7 +372,7 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         }
         if (valid && !need) {
             a.table[slot] = out;
-            a.hsub[slot] = fmaxf(out, hch);
+            if (a.hsub_out) a.hsub[slot] = fmaxf(out, hch);
         }
         LSTAT_T(t3);
         // 2. the rest of the block's sets, compacted in LDS, so the presence
@@ -475,14 +476,14 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
             const bool dd = q ? (wd & 1u) != 0u : dom;
             const float o = dd ? absent_f() : -tk;
             a.table[sk] = o;
-            a.hsub[sk] = fmaxf(o, ehch[k]);
+            if (a.hsub_out) a.hsub[sk] = fmaxf(o, ehch[k]);
         } else if (q) {
             queue_walk(present, hib, a.queue, a.qcount, sk, tk);
-            a.hsub[sk] = ehch[k];  // the walk raises it to -ts if it stores P
+            if (a.hsub_out) a.hsub[sk] = ehch[k];  // the walk raises it to -ts if it stores P
         } else {
             const float o = dom ? absent_f() : -tk;
             a.table[sk] = o;
-            a.hsub[sk] = fmaxf(o, ehch[k]);
+            if (a.hsub_out) a.hsub[sk] = fmaxf(o, ehch[k]);
         }
 #ifdef ULG_LAYER_STATS
         lstat(wall_clock64());
@@ -564,7 +565,7 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
 #pragma unroll
             for (int i = 0; i < L; ++i) hch = fmaxf(hch, a.hsub[toff[vbase + L - 1] + rc[i]]);
         }
-        a.hsub[toff[vbase + L] + rankP] = fmaxf(out, hch);
+        if (a.hsub_out) a.hsub[toff[vbase + L] + rankP] = fmaxf(out, hch);
     }
 }
 
@@ -2462,6 +2463,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     empty_set_kernel<<<(nv + 63) / 64, 64, 0, c->stream>>>(c->d_tbl_off.p, nv, S, c->table.p);
     prof_end(c);
     ScoreArgs sa;
+    sa.hsub_out = 1;
     sa.gram = c->gram.p;
     sa.binom = c->d_binom.p;
     sa.cand = c->d_cand.p;
@@ -2684,6 +2686,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                 ss.work = c->d_work.p + wo;
                 ss.queue = nullptr;
                 ss.qcount = nullptr;
+                ss.hsub_out = !(L == kmax && ph == 1);
                 const LdsLayout lay = lds_layout(n, nv, S, L, vsmall);
                 const KernelFn kfn = layer_kernel(L, ph, vsmall);
                 if (lay.total > 64 * 1024)
@@ -2723,6 +2726,8 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                 unsigned long long *qc = (variant & 16) ? c->d_qcount.p + (size_t)g * 2 * (kmax + 1) + (L * 2 + ph) : nullptr;
                 sa.queue = (variant & 16) ? c->d_queue.p + (size_t)g * qwords : nullptr;
                 sa.qcount = qc;
+                // nothing reads the subset maxima of the top layer's second phase
+                sa.hsub_out = !(L == kmax && ph == 1);
                 const uint64_t blocks = (cnt + kBlock - 1) / kBlock;
                 if (blocks > 0x7fffffffull) return set_err(c, ULG_ERR_UNSUPPORTED, "ulg_cbic_score: layer too large");
                 if (L > kMaxL) {
@@ -2757,7 +2762,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                         if (wck) ULG_HIP(c, hipMemsetAsync(c->d_dump.p, 0, 24 * sb, st));
                         prof_begin_s(c, kWalkNames[ph][L], st);
                         hipLaunchKernelGGL(sliced_fn(L, ph), dim3((unsigned)sb), dim3(64), 0, st, sa.queue, qc,
-                                           c->table.p, sa.hsub, wck ? c->d_dump.p : nullptr);
+                                           c->table.p, sa.hsub_out ? sa.hsub : nullptr, wck ? c->d_dump.p : nullptr);
                         prof_end_s(c, st);
                         if (wck) {
                             std::vector<uint64_t> hw((size_t)3 * sb);
@@ -2783,7 +2788,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                         if (wck) ULG_HIP(c, hipMemsetAsync(c->d_dump.p, 0, 8 * wck_words, st));
                         prof_begin_s(c, kWalkNames[ph][L], st);
                         hipLaunchKernelGGL(wfn, dim3((unsigned)blocks), dim3(kBlock), wl, st, sa.queue, qc, c->table.p,
-                                           sa.hsub, wck ? c->d_dump.p : nullptr);
+                                           sa.hsub_out ? sa.hsub : nullptr, wck ? c->d_dump.p : nullptr);
                         prof_end_s(c, st);
                         if (wck) {
                             std::vector<uint64_t> hw(wck_words);
