@@ -281,16 +281,14 @@ int ulg_sweep_shard_end(ulg_ctx *ctx, uint64_t *vpar, int *order, float *goal_co
                         int64_t *expanded);
 
 /* ---- tuning knobs -------------------------------------------------------
- * "score_variant" (1, 17, 49, 65, 81, 113, 241; default 113): bit 0 = fully
+ * "score_variant" (1, 17, 49, 65, 81, 113; default 113): bit 0 = fully
  * unrolled presence gather (layers <= 6), bit 4 = two-pass layers (the
  * scoring kernel settles every set it can without a walk and queues the rest
  * for a dense walk kernel with the hi-cover prune), bit 5 = that walk
  * bit-sliced (64 x K sets per wave), bit 6 = subset maxima (a per-slot table
  * of the largest stored value below each set settles sets with 2L-3L reads
  * before the rest are compacted for the 2^(L+1) presence gathers).  1 and 65
- * are one-pass (every set decided in its lane).  241 = 113 + bit 7: the
- * sets the scoring kernel leaves open at layers <= 6 are walked in that
- * kernel by their own lanes (no queue, no walk launch).  All variants store
+ * are one-pass (every set decided in its lane).  All variants store
  * identical lists.
  * "score_pipe" (0/1, default 0): every layer unrolled (k <= 6) and variant
  * 113: the whole call is one persistent launch (cbic_pipe.hip) whose waves

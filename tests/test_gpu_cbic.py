@@ -191,7 +191,7 @@ def test_rescoring_is_deterministic(ulg_ctx):
         assert x.tobytes() == y.tobytes()
 
 
-@pytest.mark.parametrize("variant", [1, 17, 49, 65, 81, 113, 241])
+@pytest.mark.parametrize("variant", [1, 17, 49, 65, 81, 113])
 def test_scorer_variants_identical(ulg_ctx, oracle_built, variant):
     """Every scorer variant (presence gather x recursion form x decision-only
     walk x subset-maxima settling) stores exactly the oracle's sets (k=6
@@ -229,9 +229,9 @@ def test_walk_forms_identical(ulg_ctx, oracle_built, monkeypatch, sets_per_lane)
 
 
 def test_subset_maxima_identical_c3_and_without_var0(ulg_ctx):
-    """Variants 113 (subset maxima settle sets before the presence gathers)
-    and 241 (113 with the open sets walked in the scoring kernel) against 49
-    (every set gathered): identical lists at C3 and on candidate
+    """Variant 113 (subset maxima settle sets before the presence gathers,
+    the rule keys gathered before the rest) against 49 (every set gathered in
+    full): identical lists at C3 and on candidate
     lists without variable 0 (phase 1 then has no P\\a+{0} keys)."""
     n = 25
     X, _ = synth.gaussian_sem(n, 10000, 9200)
@@ -241,10 +241,10 @@ def test_subset_maxima_identical_c3_and_without_var0(ulg_ctx):
     try:
         for variables, cands, k in cases:
             res = {}
-            for variant in (49, 113, 241):
+            for variant in (49, 113):
                 ulg_ctx.set_option("score_variant", variant)
                 res[variant] = ulg_ctx.score_all(variables, cands, k)
-            for other in (113, 241):
+            for other in (113,):
                 for a, b in zip(res[49], res[other]):
                     assert np.asarray(a).tobytes() == np.asarray(b).tobytes(), (len(variables), k, other)
     finally:

@@ -198,6 +198,9 @@ __host__ __device__ inline LdsLayout lds_layout(int n, int nv, int S, int L, int
 
 
 
+#ifdef ULG_AB_ATOMIC2
+__device__ unsigned long long g_abdummy;
+#endif
 // Append a set to the walk queue (wave-aggregated: one atomic per wave):
 // table slot | ts bits << 32, the hi words, then the open words
 // (open = absent & cover(T without var 0) & not checked; checked = {empty}).
@@ -210,6 +213,9 @@ __device__ __forceinline__ void queue_walk(const BS &present, const BS &hi, uint
     const int leader = __ffsll((long long)act) - 1;
     unsigned long long base = 0;
     if (lane == leader) base = atomicAdd(qcount, (unsigned long long)__popcll(act));
+#ifdef ULG_AB_ATOMIC2
+    if (lane == leader) atomicAdd(&g_abdummy, 1ull);  // timing A/B only: a second hot-spot atomic
+#endif
     base = __shfl(base, leader);
     const uint64_t pos = base + (uint64_t)__popcll(act & ((1ull << lane) - 1ull));
     uint64_t ow[W];
@@ -269,7 +275,6 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
 
     constexpr bool HM = (V & 64) != 0;           // subset maxima kept up to date
     constexpr bool CMP = HM && (V & 16) != 0;     // ... and the sets settled by them first
-    constexpr bool FUSE = CMP && (V & 128) != 0 && L <= 6;  // ... and the open sets walked in this kernel
     const uint64_t gid0 = (uint64_t)xcd_block(blockIdx.x, gridDim.x, a.xcd) * kBlock + threadIdx.x;
     const bool valid = gid0 < work[a.nv];
     if (!CMP && !valid) return;
@@ -430,7 +435,10 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         BS hib = make_bits<BS>(lds_bits + (size_t)W * kBlock);
         present.clear();
         hib.clear();
-        gather_keys<L, PHASE, V>(present, hib, ls, -tk, binom, zk, a.table, toff + (uint64_t)vk * a.S);
+        // the keys the two-level rules read first; the rest only for the sets
+        // the rules leave to the walk (the subset maxima already showed a
+        // key >= -ts is present, so the rules need no "any key" test)
+        gather_keys<L, PHASE, V, BS, LdPlain, 1>(present, hib, ls, -tk, binom, zk, a.table, toff + (uint64_t)vk * a.S);
 #ifdef ULG_AB_GATHER2
         if constexpr (W < 4) {  // timing A/B only: the gathers run twice (kept alive by asm uses)
             LocalSet<L> ls2 = ls;
@@ -444,40 +452,10 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         }
 #endif
         bool q;
-        const bool dom = settle_rules<L, PHASE>(present, hib, ls, q);
-        if constexpr (FUSE) {
-            // variant bit 7: the sets the rules leave open are walked right
-            // here, by this wave's lanes (the bit-sliced walk with one set per
-            // lane: each lane's own bitsets are its registers), instead of
-            // through the queue and a walk launch
-            using SK = Sliced<L, 1>;
-            typename SK::Vec hiV, openV;
-            uint64_t ow[W];
-#pragma unroll
-            for (int wj = 0; wj < W; ++wj) ow[wj] = hib.word(wj);
-            cover_words<W>(ow);
-#pragma unroll
-            for (int wj = 0; wj < W; ++wj) {
-                const uint64_t ce = ow[wj] & 0x5555555555555555ull;
-                ow[wj] = (ce | (ce << 1)) & ~present.word(wj) & (wj == 0 ? ~1ull : ~0ull);
-            }
-#pragma unroll
-            for (int r = 0; r < SK::NV; ++r) {
-                hiV[r] = r < SK::NV0 ? (uint32_t)(hib.word(r >> 1) >> (32 * (r & 1))) : 0u;
-                openV[r] = r < SK::NV0 ? (uint32_t)(ow[r >> 1] >> (32 * (r & 1))) : 0u;
-            }
-            constexpr bool v0inP = PHASE == 0;
-            constexpr uint32_t Plocal = v0inP ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
-            uint32_t pvtop = 0;
-#pragma unroll
-            for (int i = 0; i < L; ++i) pvtop |= (uint32_t)(i + (v0inP ? 0 : 1)) << (4 * i);
-            uint32_t alive = q ? 1u : 0u, wd = 0u, pts = 0u;
-            walk_sliced<L, 1, L>(Plocal, pvtop, alive, hiV, openV, alive, wd, pts);
-            const bool dd = q ? (wd & 1u) != 0u : dom;
-            const float o = dd ? absent_f() : -tk;
-            a.table[sk] = o;
-            if (a.hsub_out) a.hsub[sk] = fmaxf(o, ehch[k]);
-        } else if (q) {
+        const bool dom = settle_rules<L, PHASE, BS, true>(present, hib, ls, q);
+        if (q) {
+            gather_keys<L, PHASE, V, BS, LdPlain, 2>(present, hib, ls, -tk, binom, zk, a.table,
+                                                    toff + (uint64_t)vk * a.S);
             queue_walk(present, hib, a.queue, a.qcount, sk, tk);
             if (a.hsub_out) a.hsub[sk] = ehch[k];  // the walk raises it to -ts if it stores P
         } else {
@@ -1728,8 +1706,9 @@ KernelFn pick_phase(int phase) {
 // bit 5 bit-sliced walk, bit 6 subset maxima.  1: one-pass; 65: one-pass with
 // the subset maxima (the small layers of 113); 17 / 49: two-pass with the
 // per-lane / bit-sliced walk; 81 / 113: the same with the subset maxima (113
-// is the default); 241: 113 with bit 7, the open sets of layers <= 6 walked
-// in the scoring kernel itself (one set per lane, no queue, no walk launch).  Round 1's other forms (loop gathers at every layer, a
+// is the default).  Round 4's variant 241 (the open sets walked in the
+// scoring kernel by their own lanes, no queue) was slower at C5 (5.05 against
+// 3.59 ms: a 64-set union tree repeats work a 256-set one shares) and is gone.  Round 1's other forms (loop gathers at every layer, a
 // stack-machine recursion, a decision-only per-lane walk, the statistics
 // build) were measured slower and are gone.
 template <int L>
@@ -1739,7 +1718,6 @@ KernelFn pick(int phase, int variant) {
         case 17: case 49: return pick_phase<L, 17>(phase);
         case 65: return pick_phase<L, 65>(phase);
         case 81: case 113: return pick_phase<L, 81>(phase);
-        case 241: return L <= 6 ? pick_phase<L, 209>(phase) : pick_phase<L, 81>(phase);
         default: return nullptr;
     }
 }
@@ -2753,7 +2731,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                 prof_begin_s(c, kLayerNames[ph][L], st);
                 hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(kBlock), (size_t)lay.total, st, sa);
                 prof_end_s(c, st);
-                if ((variant & 16) && !((variant & 128) && L <= 6)) {
+                if (variant & 16) {
                     // the undecided lanes of this launch, densely packed
                     if ((variant & 32) && sliced_fn(L, ph)) {
                         const uint64_t per = walk_sets_per_wave(L);

@@ -282,7 +282,27 @@ __device__ __forceinline__ void cover_words(uint64_t *w) {
 // bits, except P itself, and the L-bit ones only for sets without variable 0
 // (PHASE 1) that hold variable 0 (local bit 0).
 constexpr int popc_c(uint32_t x) { return x ? (int)(x & 1u) + popc_c(x >> 1) : 0; }
-template <int L, int PHASE, int Q>
+// The keys settle_rules reads (below): P's direct children, and for a set
+// without variable 0 its grandchildren, great-grandchildren and their var-0
+// toggles; for a set with variable 0, P\{0} and P\{0,c}.
+template <int L, int PHASE>
+constexpr bool rule_key(uint32_t x) {
+    if (PHASE == 1) {
+        const uint32_t P1 = ((1u << L) - 1u) << 1;
+        const uint32_t r = P1 & ~x;  // removed members
+        if ((x & ~1u & ~P1) != 0u) return false;
+        const int k = popc_c(r);
+        if (x & 1u) return k >= 1 && k <= 2;  // P\{a}+{0}, P\{a,b}+{0}
+        return k >= 1 && k <= 3;              // P\{a}, P\{a,b}, P\{a,b,c}
+    } else {
+        const uint32_t P0 = (1u << L) - 1u;
+        const uint32_t r = P0 & ~x;
+        if (popc_c(r) == 1) return true;      // the children
+        return popc_c(r) == 2 && (r & 1u);    // P\{0,c}
+    }
+}
+// PART 0: every key; 1: the rule keys only; 2: the rest
+template <int L, int PHASE, int Q, int PART = 0>
 struct PresList {
     uint32_t t[1 << Q];
     int n;
@@ -292,6 +312,8 @@ struct PresList {
             const int pc = popc_c(x);
             if (pc > L || x == Plocal) continue;
             if (pc == L && (PHASE == 0 || !(x & 1u))) continue;
+            if (PART == 1 && !rule_key<L, PHASE>(x)) continue;
+            if (PART == 2 && rule_key<L, PHASE>(x)) continue;
             t[n++] = x;
         }
     }
@@ -310,10 +332,10 @@ struct PresList {
 // table base in SGPRs and a 32-bit VGPR offset (one address register per
 // pending load instead of a 64-bit pair).  !B32 (tables of 2^30 slots or
 // more, the one-pass variant 1 only): 64-bit slot arithmetic.
-template <int L, int PHASE, int Q, int W, class LD = LdPlain, int NB = 16, bool B32 = true>
+template <int L, int PHASE, int Q, int W, class LD = LdPlain, int NB = 16, bool B32 = true, int PART = 0>
 __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi, float thr, const uint32_t *binom,
                                                   uint64_t cpack, bool z, const float *table, const uint64_t *toffv) {
-    constexpr PresList<L, PHASE, Q> PL{};
+    constexpr PresList<L, PHASE, Q, PART> PL{};
     using Slot = std::conditional_t<B32, uint32_t, uint64_t>;
 #ifdef ULG_AB_RBLDS
     // A/B: the per-(bit, position) binomials read from the LDS table inside
@@ -450,15 +472,19 @@ __device__ __forceinline__ LocalSet<L> local_set(uint64_t cm, bool z) {
 
 // Presence of every candidate key below P u {var 0} in the cache as it
 // stands now (`present`), and which of them hold a value >= thr (`hi`).
-// V == 1 is the form kept for tables of 2^30 slots or more (64-bit slots)
-template <int L, int PHASE, int V, class BS, class LD = LdPlain>
+// V == 1 is the form kept for tables of 2^30 slots or more (64-bit slots).
+// PART (unrolled layers only): 0 every key, 1 the keys settle_rules reads, 2
+// the rest (the loop form gathers every key under PART 0 and 1, none under 2).
+template <int L, int PHASE, int V, class BS, class LD = LdPlain, int PART = 0>
 __device__ __forceinline__ void gather_keys(BS &present, BS &hi, const LocalSet<L> &ls, float thr,
                                             const uint32_t *binom, bool z, const float *table,
                                             const uint64_t *toffv) {
     constexpr int W = BS::kWords;
     if constexpr (L <= 6 && (V & 1)) {
-        presence_unrolled<L, PHASE, (PHASE == 0 ? L : L + 1), W, LD, 8, (V != 1)>(present, hi, thr, binom, ls.cpack, z, table,
-                                                                      toffv);
+        presence_unrolled<L, PHASE, (PHASE == 0 ? L : L + 1), W, LD, 8, (V != 1), PART>(present, hi, thr, binom,
+                                                                                        ls.cpack, z, table, toffv);
+    } else if constexpr (PART == 2) {
+        return;
     } else {
         const int q = ls.v0inP ? L : L + 1;
         const uint32_t full = 1u << q;
@@ -495,10 +521,12 @@ __device__ __forceinline__ void gather_keys(BS &present, BS &hi, const LocalSet<
 //    is expanded with the full list, and its j = L-1 call tests
 //    every P\{a,b}, its j = 1 call (L >= 3) the toggle of var 0.
 //    Present keys never enter `checked`, so those are visited.
-template <int L, int PHASE, class BS>
+// ANY_KNOWN: the caller knows some key >= -ts is present (the subset maxima
+// said so), so the rules may run on the rule keys alone.
+template <int L, int PHASE, class BS, bool ANY_KNOWN = false>
 __device__ __forceinline__ bool settle_rules(const BS &present, const BS &hi, const LocalSet<L> &ls, bool &queued) {
     constexpr int W = BS::kWords;
-    bool any = false;
+    bool any = ANY_KNOWN;
 #pragma unroll
     for (int wj = 0; wj < W; ++wj) any |= hi.word(wj) != 0ull;
     bool dom = false;
