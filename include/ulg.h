@@ -290,6 +290,9 @@ int ulg_sweep_shard_end(ulg_ctx *ctx, uint64_t *vpar, int *order, float *goal_co
  * before the rest are compacted for the 2^(L+1) presence gathers).  1 and 65
  * are one-pass (every set decided in its lane).  All variants store
  * identical lists.
+ * "walk_small_sets" (>= 0, default 200000): a layer-6 launch of fewer sets
+ * walks one set per lane instead of four (the small launches of 4- and
+ * 8-rank shares end with their longest walk wave).
  * "score_pipe" (0/1, default 0): every layer unrolled (k <= 6) and variant
  * 113: the whole call is one persistent launch (cbic_pipe.hip) whose waves
  * claim score tiles and walk chunks from per-(variable, stage) device

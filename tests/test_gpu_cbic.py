@@ -211,9 +211,9 @@ def test_scorer_variants_identical(ulg_ctx, oracle_built, variant):
         ulg_ctx.set_option("score_variant", DEFAULT_VARIANT)
 
 
-@pytest.mark.parametrize("sets_per_lane", ["2", "4", "8"])
+@pytest.mark.parametrize("sets_per_lane", ["1", "2", "4", "8"])
 def test_walk_forms_identical(ulg_ctx, oracle_built, monkeypatch, sets_per_lane):
-    """The bit-sliced walk with 2, 4 or 8 sets per lane (ULG_SLICED_K) stores
+    """The bit-sliced walk with 1, 2, 4 or 8 sets per lane (ULG_SLICED_K) stores
     exactly the oracle's sets, with and without variable 0 among the
     candidates (both N4 phases)."""
     monkeypatch.setenv("ULG_SLICED_K", sets_per_lane)

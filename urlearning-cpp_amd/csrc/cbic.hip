@@ -198,9 +198,6 @@ __host__ __device__ inline LdsLayout lds_layout(int n, int nv, int S, int L, int
 
 
 
-#ifdef ULG_AB_ATOMIC2
-__device__ unsigned long long g_abdummy;
-#endif
 // Append a set to the walk queue (wave-aggregated: one atomic per wave):
 // table slot | ts bits << 32, the hi words, then the open words
 // (open = absent & cover(T without var 0) & not checked; checked = {empty}).
@@ -213,9 +210,6 @@ __device__ __forceinline__ void queue_walk(const BS &present, const BS &hi, uint
     const int leader = __ffsll((long long)act) - 1;
     unsigned long long base = 0;
     if (lane == leader) base = atomicAdd(qcount, (unsigned long long)__popcll(act));
-#ifdef ULG_AB_ATOMIC2
-    if (lane == leader) atomicAdd(&g_abdummy, 1ull);  // timing A/B only: a second hot-spot atomic
-#endif
     base = __shfl(base, leader);
     const uint64_t pos = base + (uint64_t)__popcll(act & ((1ull << lane) - 1ull));
     uint64_t ow[W];
@@ -312,18 +306,6 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
     }
 
     const float ts = cbic_set_score<L>(g, a.n, v, gv, a.N, a.lambda);
-#ifdef ULG_AB_SCORE2
-    {  // timing A/B only: the score computed twice (the copy kept alive by an asm use)
-        int gv2[L];
-#pragma unroll
-        for (int i = 0; i < L; ++i) {
-            gv2[i] = gv[i];
-            asm volatile("" : "+v"(gv2[i]));
-        }
-        const float t2 = cbic_set_score<L>(g, a.n, v, gv2, a.N, a.lambda);
-        asm volatile("" ::"v"(t2));
-    }
-#endif
 
     LSTAT_T(t2);
     if constexpr (CMP) {
@@ -439,18 +421,6 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         // the rules leave to the walk (the subset maxima already showed a
         // key >= -ts is present, so the rules need no "any key" test)
         gather_keys<L, PHASE, V, BS, LdPlain, 1>(present, hib, ls, -tk, binom, zk, a.table, toff + (uint64_t)vk * a.S);
-#ifdef ULG_AB_GATHER2
-        if constexpr (W < 4) {  // timing A/B only: the gathers run twice (kept alive by asm uses)
-            LocalSet<L> ls2 = ls;
-            asm volatile("" : "+v"(ls2.cpack));
-            BS p2, h2;
-            p2.clear();
-            h2.clear();
-            gather_keys<L, PHASE, V>(p2, h2, ls2, -tk, binom, zk, a.table, toff + (uint64_t)vk * a.S);
-#pragma unroll
-            for (int j = 0; j < W; ++j) asm volatile("" ::"v"(p2.w[j]), "v"(h2.w[j]));
-        }
-#endif
         bool q;
         const bool dom = settle_rules<L, PHASE, BS, true>(present, hib, ls, q);
         if (q) {
@@ -1772,11 +1742,16 @@ SlicedFn sliced_fn_wide(int L, int phase) {
 // unions), 4 above (C3: layer 5 0.58 -> 0.54 ms, layer 6 best at 4 or 8);
 // ULG_SLICED_K=1|2|4|8 overrides for A/B
 constexpr int kSlicedKSmall = 2;  // default sets per lane up to layer 5
-int sliced_k(int L) {
+// A layer-6 launch of fewer than `small` sets (the shares of 4 and 8 ranks,
+// where a stream group holds one or two variables) walks one set per lane:
+// its few waves then each walk a quarter of the union tree, and the launch
+// ends with its longest wave (C3 8-rank share 0.80 -> 0.73 ms; the one-GPU
+// launches keep 4, best there, `profiles/r4/`).
+int sliced_k(int L, uint64_t cnt = ~0ull, uint64_t small = 0) {
     if (L >= 7) return L == 7 ? 2 : 1;
     // ULG_SLICED_K=a (every layer) or a,b (layers <= 5, layer 6): A/B only
     const char *e = std::getenv("ULG_SLICED_K");
-    int k = L <= 5 ? kSlicedKSmall : 4;
+    int k = L <= 5 ? kSlicedKSmall : (cnt < small ? 1 : 4);
     if (e) {
         const char *comma = std::strchr(e, ',');
         k = (L <= 5 || !comma) ? std::atoi(e) : std::atoi(comma + 1);
@@ -1784,10 +1759,9 @@ int sliced_k(int L) {
     return (k == 1 || k == 2 || k == 8) ? k : 4;
 }
 // queued sets per walk wave
-uint64_t walk_sets_per_wave(int L) { return 64ull * (uint64_t)sliced_k(L); }
-SlicedFn sliced_fn(int L, int phase) {
+SlicedFn sliced_fn(int L, int phase, int k) {
     if (L >= 7) return sliced_fn_wide(L, phase);
-    switch (sliced_k(L)) {
+    switch (k) {
         case 1: return sliced_fn_k<1>(L, phase);
         case 2: return sliced_fn_k<2>(L, phase);
         case 4: return sliced_fn_k<4>(L, phase);
@@ -2626,6 +2600,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     if (use_graph) {
         gkey.assign({(uint64_t)nv, (uint64_t)max_parents, (uint64_t)variant, (uint64_t)G, (uint64_t)Ls,
                      (uint64_t)c->score_xcd, (uint64_t)n, (uint64_t)c->N, dbits(c->lambda), (uint64_t)c->prof,
+                     (uint64_t)c->walk_small_sets,
                      (uint64_t)(uintptr_t)c->table.p, (uint64_t)(uintptr_t)c->d_work.p,
                      (uint64_t)(uintptr_t)c->d_workg.p, (uint64_t)(uintptr_t)c->d_queue.p,
                      (uint64_t)(uintptr_t)c->d_qcount.p, (uint64_t)(uintptr_t)c->d_cand.p,
@@ -2733,13 +2708,14 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                 prof_end_s(c, st);
                 if (variant & 16) {
                     // the undecided lanes of this launch, densely packed
-                    if ((variant & 32) && sliced_fn(L, ph)) {
-                        const uint64_t per = walk_sets_per_wave(L);
+                    const int wk = sliced_k(L, cnt, (uint64_t)c->walk_small_sets);
+                    if ((variant & 32) && sliced_fn(L, ph, wk)) {
+                        const uint64_t per = 64ull * (uint64_t)wk;
                         const uint64_t sb = (cnt + per - 1) / per;
                         if (wck && (rc = ensure(c, c->d_dump, (size_t)3 * sb))) return rc;
                         if (wck) ULG_HIP(c, hipMemsetAsync(c->d_dump.p, 0, 24 * sb, st));
                         prof_begin_s(c, kWalkNames[ph][L], st);
-                        hipLaunchKernelGGL(sliced_fn(L, ph), dim3((unsigned)sb), dim3(64), 0, st, sa.queue, qc,
+                        hipLaunchKernelGGL(sliced_fn(L, ph, wk), dim3((unsigned)sb), dim3(64), 0, st, sa.queue, qc,
                                            c->table.p, sa.hsub_out ? sa.hsub : nullptr, wck ? c->d_dump.p : nullptr);
                         prof_end_s(c, st);
                         if (wck) {

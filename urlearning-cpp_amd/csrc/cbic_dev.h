@@ -337,14 +337,6 @@ __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi,
                                                   uint64_t cpack, bool z, const float *table, const uint64_t *toffv) {
     constexpr PresList<L, PHASE, Q, PART> PL{};
     using Slot = std::conditional_t<B32, uint32_t, uint64_t>;
-#ifdef ULG_AB_RBLDS
-    // A/B: the per-(bit, position) binomials read from the LDS table inside
-    // each batch instead of held in registers (Q row offsets live, not the
-    // whole triangle)
-    uint32_t RO[Q];
-#pragma unroll
-    for (int lb = 0; lb < Q; ++lb) RO[lb] = (uint32_t)((cpack >> (6 * lb)) & 63ull) * kBinomK;
-#else
     uint32_t RB[Q][L + 1];
 #pragma unroll
     for (int lb = 0; lb < Q; ++lb) {
@@ -352,7 +344,6 @@ __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi,
 #pragma unroll
         for (int p = 1; p <= L; ++p) RB[lb][p] = (p <= lb + 1) ? B(binom, ci, p) : 0u;
     }
-#endif
     Slot off[L + 1];
 #pragma unroll
     for (int pc = 1; pc <= L; ++pc) off[pc] = (Slot)toffv[pc];
@@ -363,16 +354,11 @@ __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi,
     for (int b0 = 0; b0 < PL.n; b0 += NB) {
         // opaque per batch: no rank partial sum is shared across batches, so
         // the addresses of a batch are computed just before its loads
-#ifdef ULG_AB_RBLDS
-#pragma unroll
-        for (int lb = 0; lb < Q; ++lb) asm volatile("" : "+v"(RO[lb]));
-#else
 #pragma unroll
         for (int lb = 0; lb < Q; ++lb)
 #pragma unroll
             for (int p = 1; p <= L; ++p)
                 if (p <= lb + 1) asm volatile("" : "+v"(RB[lb][p]));
-#endif
         float v[NB];
 #pragma clang loop unroll(full)
         for (int i = 0; i < NB; ++i) {
@@ -385,11 +371,7 @@ __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi,
             for (int b = 0; b < Q; ++b)
                 if ((t >> b) & 1u) {
                     ++jj;
-#ifdef ULG_AB_RBLDS
-                    rk += binom[RO[b] + jj];
-#else
                     rk += RB[b][jj];
-#endif
                 }
             // a key with variable 0 exists only when variable 0 is a
             // candidate (z); otherwise the lane loads slot 0 and reads it as

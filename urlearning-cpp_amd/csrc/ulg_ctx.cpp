@@ -231,6 +231,11 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         c->pipe_chain = (int)value;
         return ULG_OK;
     }
+    if (std::strcmp(name, "walk_small_sets") == 0) {
+        if (value < 0) return set_err(c, ULG_ERR_ARG, "walk_small_sets must be >= 0");
+        c->walk_small_sets = value;
+        return ULG_OK;
+    }
     if (std::strcmp(name, "pipe_grid_max") == 0) {
         if (value < 0 || value > (1 << 20)) return set_err(c, ULG_ERR_ARG, "pipe_grid_max must be 0..2^20");
         c->pipe_grid_max = (int)value;

@@ -147,6 +147,7 @@ struct ulg_ctx {
 
     // ---- persistent scoring pipeline (cbic_pipe.hip) ----
     int score_pipe = 0;            // layers <= 6: one persistent launch with a device work queue
+    int64_t walk_small_sets = 200000;  // layer-6 launches below this many sets walk one set per lane
     int pipe_rounds = 2;           // 64-set rounds per two-pass score tile
     int pipe_rounds_small = 1;     // ... per one-pass tile
     int pipe_chain = 1;            // the wave that releases a stage starts on it
