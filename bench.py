@@ -95,9 +95,9 @@ def cpu_baseline(cfg, X, target_s=15.0):
 
 
 PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r2")
-# the scorer's passes were re-taken in round 3 (score_variant 113); the
+# the scorer's passes were re-taken in round 4 (the kernels timed now); the
 # sweep's kernel is unchanged since round 2
-PMC_TRAFFIC = os.path.join(os.path.dirname(PROFILES), "r3", "pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(os.path.dirname(PROFILES), "r4", "pmc_traffic.json")
 
 
 def step_sets_by_layer(cfg):
@@ -116,7 +116,7 @@ def pmc_traffic(cfg, sets, label):
     if (t.get("config_id") != cfg["id"] or round(t.get("sets_per_launch", -1)) != round(sets)
             or t.get("label") != label):
         return None, None
-    return t["traffic_bytes_per_launch"], "profiles/r3/pmc_traffic.json"
+    return t["traffic_bytes_per_launch"], "profiles/r4/pmc_traffic.json"
 
 
 ROOF_KERNELS = ["score_pipe", "score_layer_{k}_rest", "walk_{k}_rest"]
