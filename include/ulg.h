@@ -281,7 +281,7 @@ int ulg_sweep_shard_end(ulg_ctx *ctx, uint64_t *vpar, int *order, float *goal_co
                         int64_t *expanded);
 
 /* ---- tuning knobs -------------------------------------------------------
- * "score_variant" (1, 17, 49, 65, 81, 113; default 113): bit 0 = fully
+ * "score_variant" (1, 49, 65, 113; default 113): bit 0 = fully
  * unrolled presence gather (layers <= 6), bit 4 = two-pass layers (the
  * scoring kernel settles every set it can without a walk and queues the rest
  * for a dense walk kernel with the hi-cover prune), bit 5 = that walk

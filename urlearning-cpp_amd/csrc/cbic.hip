@@ -149,7 +149,7 @@ struct ScoreArgs {
     float *table;
     float *hsub;                // variant bit 6: per slot, the maximum stored value over the set's
                                 // nonempty subsets (the set included; NaN = none), table layout
-    uint64_t *queue;            // variant bit 4: lanes left for walk_kernel
+    uint64_t *queue;            // variant bit 4: lanes left for the walk launch
     unsigned long long *qcount;
     double N;
     double lambda;
@@ -440,7 +440,7 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
     }
 
     float out;
-    bool queued = false;  // variant bit 4: left for walk_kernel
+    bool queued = false;  // variant bit 4: left for the walk launch
     if (ts >= 0.0f) {
         // returned -ts; the caller stores it iff it is < 0 (score_calculator.cpp:111)
         const float s = -ts;
@@ -517,69 +517,9 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
     }
 }
 
-// Second half of a queued layer (variant bit 4): one lane per parent set the
-// score kernel could not decide, packed densely so a wave's lanes all walk.
-// Entry: table slot (low 32 bits) | ts bits (high 32) , W presence words, W
-// `hi` words.
-template <int L, int PHASE>
-__global__ void __launch_bounds__(kBlock) walk_kernel(const uint64_t *queue, const unsigned long long *qcount,
-                                                      float *table, float *hsub, uint64_t *wclock) {
-    const uint64_t t_start = wclock ? wall_clock64() : 0;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int W = bits_words(L);
-    using BS = std::conditional_t<(W >= 4), BitsLds<W>, Bits<W>>;
-    const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (gid >= *qcount) return;
-    const uint64_t q = gid;
-    const uint64_t *e = queue + q * (uint64_t)(1 + 2 * W);
-    uint64_t *lds_bits = reinterpret_cast<uint64_t *>(smem) + threadIdx.x;
-    BS hi = make_bits<BS>(lds_bits);
-    BS open = make_bits<BS>(lds_bits + (size_t)W * kBlock);
-    if constexpr (W >= 4) {
-#pragma unroll
-        for (int wj = 0; wj < W; ++wj) {
-            lds_bits[wj * kBlock] = e[1 + wj];
-            lds_bits[(W + wj) * kBlock] = e[1 + W + wj];
-        }
-    } else {
-#pragma unroll
-        for (int wj = 0; wj < W; ++wj) {
-            hi.w[wj] = e[1 + wj];
-            open.w[wj] = e[1 + W + wj];
-        }
-    }
-    const float ts = __uint_as_float((uint32_t)(e[0] >> 32));
-    constexpr bool v0inP = PHASE == 0;
-    constexpr uint32_t Plocal = v0inP ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
-    uint32_t pvtop = 0;
-#pragma unroll
-    for (int i = 0; i < L; ++i) pvtop |= (uint32_t)(i + (v0inP ? 0 : 1)) << (4 * i);
-    uint32_t steps = 0;
-    bool dom;
-    if (wclock) dom = walk_open<L, BS, true>(Plocal, pvtop, hi, open, steps);
-    else dom = walk_open<L, BS>(Plocal, pvtop, hi, open, steps);
-    table[(uint32_t)e[0]] = dom ? absent_f() : -ts;
-    if (hsub && !dom) hsub[(uint32_t)e[0]] = fmaxf(hsub[(uint32_t)e[0]], -ts);  // subset maxima (variant bit 6)
-    if (wclock) {
-        // per lane: steps | dom << 31 | open count << 32 (at the queue index)
-        int pc = 0;
-#pragma unroll
-        for (int wj = 0; wj < W; ++wj) pc += __popcll(e[1 + W + wj]);
-        wclock[2 * ((uint64_t)gridDim.x * kBlock / 64 + 1) + q] =
-            (uint64_t)steps | ((uint64_t)dom << 31) | ((uint64_t)pc << 32);
-        // diagnostics (ULG_WALK_CLOCK): per wave start / end wall clock
-        const uint64_t t_end = wall_clock64();
-        const uint64_t w = gid >> 6;
-        if ((threadIdx.x & 63) == 0) {
-            wclock[2 * w] = t_start;
-        }
-        __syncthreads();
-        if ((threadIdx.x & 63) == 0) wclock[2 * w + 1] = t_end;
-    }
-}
-
-
-// one wave (64 threads) per 64*K queued sets; entries as walk_kernel's
+// Second half of a queued layer (variant bit 4): one wave (64 threads) per
+// 64*K queued sets.  Entry: table slot (low 32 bits) | ts bits (high 32), W
+// `hi` words, W open words (queue_walk).
 template <int L, int PHASE, int K>
 __global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, const unsigned long long *qcount,
                                                          float *table, float *hsub, uint64_t *wclock) {
@@ -1673,39 +1613,22 @@ KernelFn pick_phase(int phase) {
 }
 // variants (ulg_set_option "score_variant"): bit 0 unrolled presence gathers
 // (layers <= 6), bit 4 two-pass (settle, queue the rest for a walk launch),
-// bit 5 bit-sliced walk, bit 6 subset maxima.  1: one-pass; 65: one-pass with
-// the subset maxima (the small layers of 113); 17 / 49: two-pass with the
-// per-lane / bit-sliced walk; 81 / 113: the same with the subset maxima (113
-// is the default).  Round 4's variant 241 (the open sets walked in the
-// scoring kernel by their own lanes, no queue) was slower at C5 (5.05 against
-// 3.59 ms: a 64-set union tree repeats work a 256-set one shares) and is gone.  Round 1's other forms (loop gathers at every layer, a
-// stack-machine recursion, a decision-only per-lane walk, the statistics
-// build) were measured slower and are gone.
+// bit 5 bit-sliced walk, bit 6 subset maxima.  1: one-pass (also the form for
+// tables of 2^30 slots or more); 65: one-pass with the subset maxima (the
+// small layers of 113); 49: two-pass with the bit-sliced walk (the tests'
+// every-set-gathered reference); 113: the same with the subset maxima (the
+// default).  Gone after measurement: round 4's per-lane walk forms 17 / 81
+// and a variant that walked the open sets inside the scoring kernel (C5 5.05
+// against 3.59 ms: a 64-set union tree repeats work a 256-set one shares);
+// round 1's loop gathers at every layer, stack-machine recursion,
+// decision-only per-lane walk and statistics build.
 template <int L>
 KernelFn pick(int phase, int variant) {
     switch (variant) {
         case 1: return pick_phase<L, 1>(phase);
-        case 17: case 49: return pick_phase<L, 17>(phase);
+        case 49: return pick_phase<L, 17>(phase);
         case 65: return pick_phase<L, 65>(phase);
-        case 81: case 113: return pick_phase<L, 81>(phase);
-        default: return nullptr;
-    }
-}
-using WalkFn = void (*)(const uint64_t *, const unsigned long long *, float *, float *, uint64_t *);
-template <int L>
-WalkFn walk_pick(int phase) {
-    return phase == 0 ? walk_kernel<L, 0> : walk_kernel<L, 1>;
-}
-WalkFn walk_fn(int L, int phase) {
-    switch (L) {
-        case 1: return walk_pick<1>(phase);
-        case 2: return walk_pick<2>(phase);
-        case 3: return walk_pick<3>(phase);
-        case 4: return walk_pick<4>(phase);
-        case 5: return walk_pick<5>(phase);
-        case 6: return walk_pick<6>(phase);
-        case 7: return walk_pick<7>(phase);
-        case 8: return walk_pick<8>(phase);
+        case 113: return pick_phase<L, 81>(phase);
         default: return nullptr;
     }
 }
@@ -2725,35 +2648,6 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                             char fn[512];
                             std::snprintf(fn, sizeof fn, "%s/sliced_L%d_p%d.bin", wck, L, ph);
                             if (FILE *f = std::fopen(fn, "wb")) {
-                                std::fwrite(hw.data(), 8, hw.size(), f);
-                                std::fclose(f);
-                            }
-                        }
-                    } else {
-                        const WalkFn wfn = walk_fn(L, ph);
-                        const int W = bits_words(L);
-                        const size_t wl = W >= 4 ? (size_t)2 * W * kBlock * 8 : 0;
-                        if (wl > 64 * 1024)
-                            ULG_HIP(c, hipFuncSetAttribute((const void *)wfn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                           (int)wl));
-                        // per wave start/end (2 words x waves+1), then one record per queued lane
-                        const size_t wck_words = (size_t)2 * (blocks * kBlock / 64 + 1) + (size_t)blocks * kBlock;
-                        if (wck && (rc = ensure(c, c->d_dump, wck_words))) return rc;
-                        if (wck) ULG_HIP(c, hipMemsetAsync(c->d_dump.p, 0, 8 * wck_words, st));
-                        prof_begin_s(c, kWalkNames[ph][L], st);
-                        hipLaunchKernelGGL(wfn, dim3((unsigned)blocks), dim3(kBlock), wl, st, sa.queue, qc, c->table.p,
-                                           sa.hsub_out ? sa.hsub : nullptr, wck ? c->d_dump.p : nullptr);
-                        prof_end_s(c, st);
-                        if (wck) {
-                            std::vector<uint64_t> hw(wck_words);
-                            unsigned long long qn = 0;
-                            ULG_HIP(c, hipMemcpyAsync(hw.data(), c->d_dump.p, hw.size() * 8, hipMemcpyDeviceToHost, st));
-                            ULG_HIP(c, hipMemcpyAsync(&qn, qc, 8, hipMemcpyDeviceToHost, st));
-                            ULG_HIP(c, hipStreamSynchronize(st));
-                            char fn[512];
-                            std::snprintf(fn, sizeof fn, "%s/wclock_L%d_p%d.bin", wck, L, ph);
-                            if (FILE *f = std::fopen(fn, "wb")) {
-                                std::fwrite(&qn, 8, 1, f);
                                 std::fwrite(hw.data(), 8, hw.size(), f);
                                 std::fclose(f);
                             }

@@ -146,117 +146,6 @@ __device__ __forceinline__ void best_subset(uint32_t T, uint32_t pv, const BS &p
     }
 }
 
-// The same traversal with the decision folded in (variant bit 2).  The caller
-// only needs "is some visited key's value >= -ts" (BIC_OLS.cpp:234 with
-// bic_threshold 0 and best_score starting at 0 < -ts): `hi` marks the present
-// keys with value >= -ts, and the walk stops at the first one it visits.
-// Present keys never enter `checked` (only recursed, absent keys do), so a
-// present key is visited exactly when the walk tests it -- stopping early
-// cannot change the answer, and no value is reloaded afterwards.
-// Measured at C3 layer 6: 3.1 ms vs 2.8 ms for the full walk (bit 2 clear) --
-// a wave only leaves the walk when all its lanes do, so the early exit buys
-// little, while the extra exits cost issue slots.  An equivalent walk without
-// the reference's redundant re-tests (2.2x fewer union points per wave in a
-// host simulation) measured 5.6 ms: heavier control flow, occupancy 2.
-template <int M, class BS>
-__device__ __forceinline__ bool dominated(uint32_t T, uint32_t pv, const BS &present, const BS &hi, BS &checked,
-                                          uint32_t &steps) {
-#pragma nounroll
-    for (int idx = 0; idx < M; ++idx) {
-        ++steps;
-        const uint32_t u = (pv >> (4 * idx)) & 15u;
-        const uint32_t T2 = T ^ (1u << u);
-        if (checked.test(T2)) continue;
-        if (present.test(T2)) {
-            if (hi.test(T2)) return true;
-            continue;
-        }
-        if constexpr (M > 1) {
-            uint32_t npv = 0;
-            int j = 0;
-#pragma nounroll
-            for (int i = 0; i < M; ++i) {
-                const uint32_t pi = (pv >> (4 * i)) & 15u;
-                if (pi == u) continue;
-                npv |= pi << (4 * j);
-                ++j;
-                if (dominated<M - 1, BS>(T2, npv, present, hi, checked, steps)) return true;
-                checked.set(T2);
-            }
-        }
-    }
-    return false;
-}
-
-// dominated() with the hi-cover prune: an absent node T2 is expanded only if
-// some key >= -ts lies in U(T2) = subsets of T2 u {var 0} (`cover`, tested at
-// T2 without var 0).  Skipping an expansion changes `checked` only inside
-// U(T2); a later test that sees the difference expands a node of U(T2), whose
-// own expansion again stays inside U(T2) -- so every difference stays within
-// keys none of which is >= -ts, and the first such key the walk visits, if
-// any, is the same.  (The queued lanes of C3 layer 6 walk 13 steps instead of
-// 220 when stored, 113 instead of 194 when pruned.)
-template <int M, class BS>
-__device__ __forceinline__ bool dominated_cov(uint32_t T, uint32_t pv, const BS &present, const BS &hi,
-                                              const BS &cover, BS &checked) {
-#pragma nounroll
-    for (int idx = 0; idx < M; ++idx) {
-        const uint32_t u = (pv >> (4 * idx)) & 15u;
-        const uint32_t T2 = T ^ (1u << u);
-        if (checked.test(T2)) continue;
-        if (present.test(T2)) {
-            if (hi.test(T2)) return true;
-            continue;
-        }
-        if constexpr (M > 1) {
-            if (!cover.test(T2 & ~1u)) continue;
-            uint32_t npv = 0;
-            int j = 0;
-#pragma nounroll
-            for (int i = 0; i < M; ++i) {
-                const uint32_t pi = (pv >> (4 * i)) & 15u;
-                if (pi == u) continue;
-                npv |= pi << (4 * j);
-                ++j;
-                if (dominated_cov<M - 1, BS>(T2, npv, present, hi, cover, checked)) return true;
-                checked.set(T2);
-            }
-        }
-    }
-    return false;
-}
-
-// dominated_cov() with its three per-node tests folded into one: `open` =
-// absent & hi-cover & not yet checked, so a tested node is a hit (hi), an
-// expansion (open) or nothing; clearing its open bit after the first call
-// returns is the reference's checked.insert (present nodes never enter
-// `checked`, so testing hi before `checked` changes nothing).
-template <int M, class BS, bool DIAG = false>
-__device__ __forceinline__ bool walk_open(uint32_t T, uint32_t pv, const BS &hi, BS &open, uint32_t &steps) {
-#pragma nounroll
-    for (int idx = 0; idx < M; ++idx) {
-        if constexpr (DIAG) ++steps;
-        const uint32_t u = (pv >> (4 * idx)) & 15u;
-        const uint32_t T2 = T ^ (1u << u);
-        if (hi.test(T2)) return true;
-        if constexpr (M > 1) {
-            if (!open.test(T2)) continue;
-            uint32_t npv = 0;
-            int j = 0;
-#pragma nounroll
-            for (int i = 0; i < M; ++i) {
-                const uint32_t pi = (pv >> (4 * i)) & 15u;
-                if (pi == u) continue;
-                npv |= pi << (4 * j);
-                ++j;
-                if (walk_open<M - 1, BS, DIAG>(T2, npv, hi, open, steps)) return true;
-                open.reset(T2);
-            }
-        }
-    }
-    return false;
-}
-
 // cover = { T : some key of hi, without var 0, is a subset of T }: drop bit 0
 // of every key, then close upwards over bits 1 .. q-1 (in-word shifts for
 // bits 1..5, word ORs for the bits that index words).

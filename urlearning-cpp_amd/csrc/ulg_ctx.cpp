@@ -196,8 +196,8 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         return ULG_OK;
     }
     if (std::strcmp(name, "score_variant") == 0) {
-        if (value != 1 && value != 17 && value != 49 && value != 65 && value != 81 && value != 113)
-            return set_err(c, ULG_ERR_ARG, "score_variant must be 1, 17, 49, 65, 81 or 113");
+        if (value != 1 && value != 49 && value != 65 && value != 113)
+            return set_err(c, ULG_ERR_ARG, "score_variant must be 1, 49, 65 or 113");
         c->score_variant = (int)value;
         return ULG_OK;
     }
