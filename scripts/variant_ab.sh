@@ -11,7 +11,7 @@ if [ "${TESTS:-1}" = "1" ]; then
   timeout -k 10 400 python -u -m pytest tests/test_gpu_cbic.py -x -q --timeout 200 --timeout-method thread > ${OUT}/pytest.log 2>&1
   echo "tests: $(tail -1 ${OUT}/pytest.log)"
 fi
-for v in ${VARIANTS:-113 241}; do
+for v in ${VARIANTS:-49 113}; do
   timeout -k 10 200 python -u scripts/pipe_probe.py --cases c3 c5 small --modes 0 --reps 10 --options score_variant=$v > ${OUT}/probe_$v.log 2>&1
   timeout -k 10 150 python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-search --no-c4 --option score_variant=$v > ${OUT}/bench_$v.json 2> ${OUT}/bench_$v.err
   if [ -f ab/libulg_LAYER_STATS.so ]; then
