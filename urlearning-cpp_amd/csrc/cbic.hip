@@ -578,8 +578,13 @@ __global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, 
 #pragma unroll
     for (int i = 0; i < L; ++i) pvtop |= (uint32_t)(i + (v0inP ? 0 : 1)) << (4 * i);
     uint32_t dom = 0u, pts = 0u;
-    if (wclock) walk_sliced<L, K, L, true>(Plocal, pvtop, alive, hiV, openV, alive, dom, pts);
-    else walk_sliced<L, K, L>(Plocal, pvtop, alive, hiV, openV, alive, dom, pts);
+    // the open bits in LDS (OpenLds): no vector copies per recursion level
+    __shared__ uint32_t open_lds[S::NV * 64];
+    OpenLds<L, K> ol{open_lds + threadIdx.x};
+#pragma unroll
+    for (int r = 0; r < S::NV; ++r) ol.base[r * 64] = openV[r];
+    if (wclock) walk_sliced<L, K, L, true>(Plocal, pvtop, alive, hiV, ol, alive, dom, pts);
+    else walk_sliced<L, K, L>(Plocal, pvtop, alive, hiV, ol, alive, dom, pts);
     if (wclock && threadIdx.x == 0) {
         // diagnostics (ULG_WALK_CLOCK): start, end, union points of this wave
         wclock[3 * blockIdx.x] = t_start;

@@ -535,16 +535,37 @@ __device__ __forceinline__ void sl_clear(typename Sliced<L, K>::Vec &v, uint32_t
 }
 __device__ __forceinline__ bool wave_any(uint32_t x) { return __ballot(x != 0u) != 0ull; }
 
+// The walk's open bits in LDS instead of registers: register r of the bit-
+// sliced vector is word r * 64 + lane.  A test is one ds_read at a uniform
+// offset and a clear one ds_and, where the register form's indexed write
+// makes the compiler copy the whole vector at every recursion level (16
+// v_mov_b64 per expanded node at layer 6).
+template <int L, int K>
+struct OpenLds {
+    uint32_t *base;  // this lane's word 0
+};
+template <int L, int K>
+__device__ __forceinline__ uint32_t sl_get(const OpenLds<L, K> &v, uint32_t t) {
+    using S = Sliced<L, K>;
+    return (v.base[(t / S::E) * 64] >> (S::K * (t % S::E))) & S::KM;
+}
+template <int L, int K>
+__device__ __forceinline__ void sl_clear(OpenLds<L, K> &v, uint32_t t, uint32_t m) {
+    using S = Sliced<L, K>;
+    __hip_atomic_fetch_and(v.base + (t / S::E) * 64, ~(m << (S::K * (t % S::E))), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
 // [idx_lo, idx_hi): the positions this call can change anything at.  The
 // j-th call fb(T2, npv) of a node's inner loop sees the positions below j-1
 // already tested by its earlier calls (closed, or present below -ts) and zeros
 // from j on, whose child T2 ^ {0} call 1 tested at its position 1 -- so call 1
 // walks positions 0..1 and call j >= 2 position j-1 only (the reference's
 // remaining re-tests are no-ops; the same tests in the same order).
-template <int L, int K, int M, bool DIAG = false>
+template <int L, int K, int M, bool DIAG = false, class OV = typename Sliced<L, K>::Vec>
 __device__ __forceinline__ void walk_sliced(uint32_t T, uint32_t pv, uint32_t act, const typename Sliced<L, K>::Vec &hiV,
-                                            typename Sliced<L, K>::Vec &openV, uint32_t &alive, uint32_t &dom,
-                                            uint32_t &pts, int idx_lo = 0, int idx_hi = M) {
+                                            OV &openV, uint32_t &alive, uint32_t &dom, uint32_t &pts, int idx_lo = 0,
+                                            int idx_hi = M) {
 #pragma nounroll
     for (int idx = idx_lo; idx < idx_hi; ++idx) {
         act &= alive;
@@ -568,8 +589,10 @@ __device__ __forceinline__ void walk_sliced(uint32_t T, uint32_t pv, uint32_t ac
                 if (pi == u) continue;
                 npv |= pi << (4 * j);
                 ++j;
-                if (j == 1) walk_sliced<L, K, M - 1, DIAG>(T2, npv, x, hiV, openV, alive, dom, pts, 0, M - 1 < 2 ? M - 1 : 2);
-                else walk_sliced<L, K, M - 1, DIAG>(T2, npv, x, hiV, openV, alive, dom, pts, j - 1, j);
+                if (j == 1)
+                    walk_sliced<L, K, M - 1, DIAG, OV>(T2, npv, x, hiV, openV, alive, dom, pts, 0, M - 1 < 2 ? M - 1 : 2);
+                else
+                    walk_sliced<L, K, M - 1, DIAG, OV>(T2, npv, x, hiV, openV, alive, dom, pts, j - 1, j);
                 sl_clear<L, K>(openV, T2, x);  // checked.insert(T2) for the sets that ran the call
                 x &= alive;
                 if (!wave_any(x)) break;
