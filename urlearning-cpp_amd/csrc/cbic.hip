@@ -1666,20 +1666,23 @@ SlicedFn sliced_fn_wide(int L, int phase) {
 }
 // sets per lane: more sets share one walk of the union tree, fewer give more
 // waves to hide the walk's latency
-// sets per lane of the bit-sliced walk: 2 up to layer 5 (more, smaller
-// unions), 4 above (C3: layer 5 0.58 -> 0.54 ms, layer 6 best at 4 or 8);
-// ULG_SLICED_K=1|2|4|8 overrides for A/B
-constexpr int kSlicedKSmall = 2;  // default sets per lane up to layer 5
+// sets per lane of the bit-sliced walk: 4 up to layer 5, 8 at layer 6 since
+// the open bits moved to LDS (round 4, bench step 0.550 -> 0.540 ms, C5 call
+// 3.36 -> 3.15 ms against 2 / 4; before it, 2 / 4 was best: a wider union
+// then cost a larger register copy per node); ULG_SLICED_K=1|2|4|8 (every
+// layer) or a,b (layers <= 5, layer 6) overrides for A/B
+constexpr int kSlicedKSmall = 4;  // default sets per lane up to layer 5
+constexpr int kSlicedK6 = 8;      // ... at layer 6
 // A layer-6 launch of fewer than `small` sets (the shares of 4 and 8 ranks,
 // where a stream group holds one or two variables) walks one set per lane:
 // its few waves then each walk a quarter of the union tree, and the launch
 // ends with its longest wave (C3 8-rank share 0.80 -> 0.73 ms; the one-GPU
-// launches keep 4, best there, `profiles/r4/`).
+// launches keep the wide union, best there, `profiles/r4/`).
 int sliced_k(int L, uint64_t cnt = ~0ull, uint64_t small = 0) {
     if (L >= 7) return L == 7 ? 2 : 1;
     // ULG_SLICED_K=a (every layer) or a,b (layers <= 5, layer 6): A/B only
     const char *e = std::getenv("ULG_SLICED_K");
-    int k = L <= 5 ? kSlicedKSmall : (cnt < small ? 1 : 4);
+    int k = L <= 5 ? kSlicedKSmall : (cnt < small ? 1 : kSlicedK6);
     if (e) {
         const char *comma = std::strchr(e, ',');
         k = (L <= 5 || !comma) ? std::atoi(e) : std::atoi(comma + 1);
