@@ -164,6 +164,11 @@ class ListExchange:
             self.sets_ptr = self.stage.data_ptr()
         else:
             self.sets_ptr = base + self.hdr
+        if self.device.type == "cuda":
+            # the zero fills run on torch's stream and libulg writes these
+            # blocks on its own: without this wait a fill could land after the
+            # scorer's copy and zero the lists (seen once in ~10 two-rank runs)
+            torch.cuda.current_stream(self.device).synchronize()
 
     def _sets_view(self, blocks):
         """[ws, cap] int64 sets of gathered blocks [ws, block] (uint8)."""
