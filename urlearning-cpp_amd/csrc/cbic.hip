@@ -1666,13 +1666,13 @@ SlicedFn sliced_fn_wide(int L, int phase) {
 }
 // sets per lane: more sets share one walk of the union tree, fewer give more
 // waves to hide the walk's latency
-// sets per lane of the bit-sliced walk: 4 up to layer 5, 8 at layer 6 since
-// the open bits moved to LDS (round 4, bench step 0.550 -> 0.540 ms, C5 call
-// 3.36 -> 3.15 ms against 2 / 4; before it, 2 / 4 was best: a wider union
-// then cost a larger register copy per node); ULG_SLICED_K=1|2|4|8 (every
+// sets per lane of the bit-sliced walk: 2 up to layer 5, 4 at layer 6
+// (rounds 2-4: with the open bits in LDS, 4 / 8 measured 0.558 against 0.547
+// ms per C3 bench step over three alternating runs, 4 / 4 0.556, though C5
+// calls prefer 4 / 8: 3.15 against 3.36 ms); ULG_SLICED_K=1|2|4|8 (every
 // layer) or a,b (layers <= 5, layer 6) overrides for A/B
-constexpr int kSlicedKSmall = 4;  // default sets per lane up to layer 5
-constexpr int kSlicedK6 = 8;      // ... at layer 6
+constexpr int kSlicedKSmall = 2;  // default sets per lane up to layer 5
+constexpr int kSlicedK6 = 4;      // ... at layer 6
 // A layer-6 launch of fewer than `small` sets (the shares of 4 and 8 ranks,
 // where a stream group holds one or two variables) walks one set per lane:
 // its few waves then each walk a quarter of the union tree, and the launch
