@@ -1471,9 +1471,12 @@ __global__ void __launch_bounds__(kBlock) write_kernel(WriteArgs a) {
     __shared__ uint32_t pre[kBlock / 64];
     __shared__ uint32_t binom[64 * kBinomK];
     __shared__ uint64_t toff_s[kWriteLdsSegs + 1];
+    __shared__ uint32_t cand_s[64 * 16];  // the candidate lists (64 bytes per variable, nv <= 64)
     const int nseg = a.nv * a.S;
     const bool lds_off = nseg <= kWriteLdsSegs;
     for (int i = threadIdx.x; i < 64 * kBinomK; i += kBlock) binom[i] = a.binom[i];
+    for (int i = threadIdx.x; i < a.nv * 16; i += kBlock) cand_s[i] = reinterpret_cast<const uint32_t *>(a.cand)[i];
+    const uint8_t *cand = reinterpret_cast<const uint8_t *>(cand_s);
     if (lds_off)
         for (int i = threadIdx.x; i <= nseg; i += kBlock) toff_s[i] = a.tbl_off[i];
     const uint64_t *toff = lds_off ? toff_s : a.tbl_off;
@@ -1529,7 +1532,7 @@ __global__ void __launch_bounds__(kBlock) write_kernel(WriteArgs a) {
         while (rem) {
             const int b = __builtin_ctzll(rem);
             rem &= rem - 1;
-            gs |= 1ull << a.cand[vi * 64 + b];
+            gs |= 1ull << cand[vi * 64 + b];
         }
         a.sets[pos] = gs;
         a.scores[pos] = vals[j];
