@@ -230,22 +230,12 @@ __device__ __forceinline__ void queue_walk(const BS &present, const BS &hi, uint
 }
 
 
-#ifdef ULG_LAYER_STATS
-// timing diagnostics of the two-pass layer kernels (A/B builds only): per
-// (layer, phase) the wave-time sums of init, score, settle, compact, gather
-// and the wave / gather-lane counts, in 100 MHz wall-clock ticks
-__device__ unsigned long long g_lstat[64][2][kMaxL + 1][8];  // 64 copies: few atomics per address
-#define LSTAT_T(x) const uint64_t x = wall_clock64()
-#else
-#define LSTAT_T(x)
-#endif
 
 // PHASE 0: sets containing variable 0; 1: the rest.  V = variant bits (see
 // ulg_set_option "score_variant"), compile-time so each form gets its own
 // register allocation.
 template <int L, int PHASE, int V>
 __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
-    LSTAT_T(t0);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const LdsLayout lay = lds_layout(a.n, a.nv, a.S, L, V);
     double *g = reinterpret_cast<double *>(smem + lay.gram);
@@ -265,7 +255,6 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
     for (int i = threadIdx.x; i < a.nv * 16; i += kBlock)
         reinterpret_cast<uint32_t *>(scand)[i] = reinterpret_cast<const uint32_t *>(a.cand)[i];
     __syncthreads();
-    LSTAT_T(t1);
 
     constexpr bool HM = (V & 64) != 0;           // subset maxima kept up to date
     constexpr bool CMP = HM && (V & 16) != 0;     // ... and the sets settled by them first
@@ -307,7 +296,6 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
 
     const float ts = cbic_set_score<L>(g, a.n, v, gv, a.N, a.lambda);
 
-    LSTAT_T(t2);
     if constexpr (CMP) {
         // 1. settle by the subset maxima: ts >= 0, no key >= -ts in U(P), or a
         //    present direct child >= -ts (always visited at the top level)
@@ -361,7 +349,6 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
             a.table[slot] = out;
             if (a.hsub_out) a.hsub[slot] = fmaxf(out, hch);
         }
-        LSTAT_T(t3);
         // 2. the rest of the block's sets, compacted in LDS, so the presence
         //    gathers (2^(L+1) reads each) run on dense waves
         unsigned int *cnt = reinterpret_cast<unsigned int *>(smem + lay.cmp);
@@ -381,29 +368,7 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
             evi[k] = vi;
         }
         __syncthreads();
-        LSTAT_T(t4);
-#ifdef ULG_LAYER_STATS
-        const bool gl = threadIdx.x < *cnt;
-        auto lstat = [&](uint64_t t5) {
-            if ((threadIdx.x & 63) == 0) {
-                unsigned long long *st = g_lstat[blockIdx.x & 63][PHASE][L];
-                atomicAdd(st + 0, (unsigned long long)(t1 - t0));
-                atomicAdd(st + 1, (unsigned long long)(t2 - t1));
-                atomicAdd(st + 2, (unsigned long long)(t3 - t2));
-                atomicAdd(st + 3, (unsigned long long)(t4 - t3));
-                atomicAdd(st + 4, (unsigned long long)(t5 - t4));
-                atomicAdd(st + 5, 1ull);
-            }
-            const unsigned long long ng = (unsigned long long)__popcll(__ballot(gl));
-            if ((threadIdx.x & 63) == 0) atomicAdd(g_lstat[blockIdx.x & 63][PHASE][L] + 6, ng);
-        };
-        if (!gl) {
-            lstat(t4);
-            return;
-        }
-#else
         if (threadIdx.x >= *cnt) return;
-#endif
         const int k = threadIdx.x;
         const int vk = evi[k];
         const bool zk = smeta[vk * 4 + 2] != 0;
@@ -433,9 +398,6 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
             a.table[sk] = o;
             if (a.hsub_out) a.hsub[sk] = fmaxf(o, ehch[k]);
         }
-#ifdef ULG_LAYER_STATS
-        lstat(wall_clock64());
-#endif
         return;
     }
 
@@ -2772,27 +2734,6 @@ launched:
         if ((rc = pipe_check(c))) return rc;
         pipe_report(c);
     }
-#ifdef ULG_LAYER_STATS
-    {
-        static unsigned long long h[64][2][kMaxL + 1][8];
-        if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_lstat), sizeof h) == hipSuccess) {
-            for (int L = 1; L <= kMaxL; ++L)
-                for (int ph = 0; ph < 2; ++ph) {
-                    unsigned long long x[8] = {0};
-                    for (int cp = 0; cp < 64; ++cp)
-                        for (int i = 0; i < 8; ++i) x[i] += h[cp][ph][L][i];
-                    if (!x[5]) continue;
-                    const double w = (double)x[5] * 100.0;  // ticks (100 MHz) -> us, per wave
-                    std::fprintf(stderr,
-                                 "layer_stats L%d p%d waves=%llu gather_lanes/wave=%.1f per-wave us: init %.2f score %.2f "
-                                 "settle %.2f compact %.2f gather %.2f\n",
-                                 L, ph, x[5], (double)x[6] / x[5], x[0] / w, x[1] / w, x[2] / w, x[3] / w, x[4] / w);
-                }
-            std::memset(h, 0, sizeof h);
-            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lstat), h, sizeof h);
-        }
-    }
-#endif
     if (wide_err)
         return set_err(c, ULG_ERR_UNSUPPORTED,
                        "ulg_cbic_score: a find_best_subset_score walk in a wide layer exceeded its cap (2^30 steps "
