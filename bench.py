@@ -172,6 +172,24 @@ def roofline(ctx, cfg, per_layer_sets, steps, step_sets=None, step_bytes=None):
              "fp64_tflops": sets * flops_per_set / (p["avg_ms"] * 1e-3) / 1e12}, p)
 
 
+def host_pmu(ctx, expanded):
+    """The exact replay's host counters (ulg_get_info exact_*: perf_event_open
+    on the replay thread, user space): cycles, instructions and the kernel's
+    generic cache-miss event per expansion -- the replay's floor as numbers.
+    None where the host does not grant the counters."""
+    try:
+        cyc, ins, mis = (ctx.info(k) for k in ("exact_cycles", "exact_instructions", "exact_cache_misses"))
+    except Exception:  # noqa: BLE001 -- an older library
+        return None
+    e = max(int(expanded), 1)
+    out = {"event": "PERF_COUNT_HW_CPU_CYCLES / _INSTRUCTIONS / _CACHE_MISSES, user space, replay thread"}
+    out["cycles_per_expansion"] = cyc / e if cyc >= 0 else None
+    out["instructions_per_expansion"] = ins / e if ins >= 0 else None
+    out["ipc"] = ins / cyc if cyc > 0 and ins >= 0 else None
+    out["cache_misses_per_expansion"] = mis / e if mis >= 0 else None
+    return out if any(out[k] is not None for k in ("cycles_per_expansion", "cache_misses_per_expansion")) else None
+
+
 PMC_SEARCH = os.path.join(PROFILES, "pmc_search_traffic.json")
 
 
@@ -292,6 +310,7 @@ def exact_astar_legs(ctx, cfg, skel, lists, oracle_budget_s=15.0):
                     "expansions": e["expanded"], "ms": 1e3 * dt, "expansions_per_s": e["expanded"] / dt,
                     "ns_per_expansion": 1e9 * dt / max(e["expanded"], 1),
                     "goal_cost": e["cost"],
+                    "host_pmu": host_pmu(ctx, e["expanded"]),
                     "same_netfile_cost_expansions_as_oracle_fixture": same,
                     "oracle_fixture": os.path.relpath(fx, ROOT) if os.path.exists(fx) else None,
                     "note": "reference pop order replayed on the host over GPU-built O(1) tables; the time "

@@ -353,7 +353,10 @@ int ulg_set_option(ulg_ctx *ctx, const char *name, int64_t value);
 /* Read-back of per-call state: "out_of_time" (1 if the last ulg_cbic_score,
  * ulg_astar* or ulg_triplet_astar ran out of time_limit_ms), "highest_completed_layer" (the
  * reference's ScoreCalculator::highestCompletedLayer of the last scoring call,
- * score_calculator.h:45). */
+ * score_calculator.h:45), "exact_cycles" / "exact_instructions" /
+ * "exact_cache_misses" (the last exact-order A*'s user-space host counters on
+ * the calling thread, perf_event_open; -1 where the host does not grant
+ * them). */
 int ulg_get_info(ulg_ctx *ctx, const char *name, int64_t *value);
 
 /* ---- profiling (per-kernel HIP-event timing on the context stream) ---- */

@@ -19,6 +19,10 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <linux/perf_event.h>
+#include <sys/ioctl.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include "search_exact.h"
 
@@ -558,6 +562,48 @@ int ulg_pdb_query(ulg_ctx *c, int64_t count, const uint64_t *S, float *h, int *c
     return search_pdb_query(c, count, S, h, complete);
 }
 
+namespace {
+// The replay's host counters (perf_event_open on the calling thread, user
+// space only): cycles, instructions and the kernel's generic cache-miss event
+// (the last-level misses a pop or successor visit waits on).  A counter the
+// host does not grant (containers, perf_event_paranoid) reads as -1.
+struct HostPmu {
+    int fd[3] = {-1, -1, -1};
+    HostPmu() {
+        const uint64_t cfg[3] = {PERF_COUNT_HW_CPU_CYCLES, PERF_COUNT_HW_INSTRUCTIONS, PERF_COUNT_HW_CACHE_MISSES};
+        for (int i = 0; i < 3; ++i) {
+            perf_event_attr pe;
+            std::memset(&pe, 0, sizeof pe);
+            pe.type = PERF_TYPE_HARDWARE;
+            pe.size = sizeof pe;
+            pe.config = cfg[i];
+            pe.disabled = 1;
+            pe.exclude_kernel = 1;
+            pe.exclude_hv = 1;
+            fd[i] = (int)syscall(SYS_perf_event_open, &pe, 0, -1, -1, 0);
+            if (fd[i] >= 0) {
+                ioctl(fd[i], PERF_EVENT_IOC_RESET, 0);
+                ioctl(fd[i], PERF_EVENT_IOC_ENABLE, 0);
+            }
+        }
+    }
+    void stop(int64_t (&acc)[3]) {
+        for (int i = 0; i < 3; ++i) {
+            if (fd[i] < 0) {
+                acc[i] = -1;
+                continue;
+            }
+            ioctl(fd[i], PERF_EVENT_IOC_DISABLE, 0);
+            uint64_t v = 0;
+            if (read(fd[i], &v, sizeof v) == (ssize_t)sizeof v && acc[i] >= 0) acc[i] += (int64_t)v;
+            else acc[i] = -1;
+            close(fd[i]);
+            fd[i] = -1;
+        }
+    }
+};
+}  // namespace
+
 int ulg_astar(ulg_ctx *c, const uint64_t *edges, int pd_count, int mode, uint64_t *vpar, int *order,
               float *goal_cost, int64_t *expanded, char *net_text, int64_t net_cap) {
     if (!c) return ULG_ERR_ARG;
@@ -596,6 +642,7 @@ int ulg_astar_scc(ulg_ctx *c, const uint64_t *edges, int pd_count, int mode, uin
     if (net_text && net_cap > 0) net_text[0] = 0;
     if (mode == ULG_ASTAR_GPU) return astar_gpu(c, edges, vpar, order, goal_cost, expanded);
     if (mode != ULG_ASTAR_EXACT) return set_err(c, ULG_ERR_ARG, "ulg_astar: unknown mode");
+    c->exact_pmu[0] = c->exact_pmu[1] = c->exact_pmu[2] = 0;
     std::vector<uint64_t> comps;
     const bool good = edges != nullptr;
     if (good) components(edges, n, comps);
@@ -622,9 +669,11 @@ int ulg_astar_scc(ulg_ctx *c, const uint64_t *edges, int pd_count, int mode, uin
         HostTables T;
         host_tables(s, T);
         const Clock::time_point *dl = c->time_limit_ms > 0 ? &deadline : nullptr;
-        if ((rc = dense ? astar_dense(c, T, edges, good, ancestors, comp, expanded, &hang, r, dl)
-                        : astar_one(c, T, edges, good, ancestors, comp, expanded, &hang, r, dl)))
-            return rc;
+        HostPmu pmu;
+        rc = dense ? astar_dense(c, T, edges, good, ancestors, comp, expanded, &hang, r, dl)
+                   : astar_one(c, T, edges, good, ancestors, comp, expanded, &hang, r, dl);
+        pmu.stop(c->exact_pmu);
+        if (rc) return rc;
         if (!r.found) { fail = true; continue; }
         // each component rewrites netFile and netFile.csv (astar_main.cpp:470,519)
         for (int v = 0; v < n; ++v) vpar[v] = 0;

@@ -325,6 +325,19 @@ int ulg_get_info(ulg_ctx *c, const char *name, int64_t *value) {
         *value = c->completed_layer;
         return ULG_OK;
     }
+    // the last exact A*'s host counters (user space, the calling thread; -1: not granted)
+    if (std::strcmp(name, "exact_cycles") == 0) {
+        *value = c->exact_pmu[0];
+        return ULG_OK;
+    }
+    if (std::strcmp(name, "exact_instructions") == 0) {
+        *value = c->exact_pmu[1];
+        return ULG_OK;
+    }
+    if (std::strcmp(name, "exact_cache_misses") == 0) {
+        *value = c->exact_pmu[2];
+        return ULG_OK;
+    }
     return set_err(c, ULG_ERR_ARG, std::string("unknown info: ") + name);
 }
 

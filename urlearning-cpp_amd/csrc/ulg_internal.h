@@ -77,6 +77,7 @@ struct ulg_ctx {
     int64_t time_limit_ms = 0;     // -r: wall-clock budget per scoring call / search (0 = none)
     int out_of_time = 0;           // the last scoring call or search ran out of its budget
     int completed_layer = -1;      // highest fully scored layer of the last scoring call
+    int64_t exact_pmu[3] = {-1, -1, -1};  // last exact A*: user-space cycles, instructions, cache misses (-1: n/a)
     uint64_t table_budget_kb = 0;  // best-score table budget in KiB (0 = half the free HBM)
     int sweep_table = 1;
     int wide_prune = 1;            // wide walks: skip absent nodes whose subsets hold no key >= -ts

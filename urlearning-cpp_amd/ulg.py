@@ -364,7 +364,8 @@ class Context:
         self._check(lib().ulg_set_option(self._h, name.encode(), int(value)), "ulg_set_option")
 
     def info(self, name: str) -> int:
-        """ulg_get_info: "out_of_time", "highest_completed_layer"."""
+        """ulg_get_info: "out_of_time", "highest_completed_layer", "exact_cycles",
+        "exact_instructions", "exact_cache_misses"."""
         v = C.c_int64()
         self._check(lib().ulg_get_info(self._h, name.encode(), C.byref(v)), "ulg_get_info")
         return v.value
