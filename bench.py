@@ -73,8 +73,14 @@ def cpu_baseline(cfg, X, target_s=15.0):
     import oracle
     oracle.build()
     n, k, lam = cfg["n"], cfg["k"], cfg["lam"]
-    # T = nproc: the CPUs this process may run on
-    threads = max(1, len(os.sched_getaffinity(0)))
+    # the CPUs this process may actually use: its affinity mask, capped by the
+    # cgroup CPU quota (on the GPU box 16 of 256 visible CPUs); more threads
+    # than that only time-share them
+    cores = max(1, len(os.sched_getaffinity(0)))
+    q = cpu_quota()
+    if q is not None:
+        cores = max(1, min(cores, int(q)))
+    threads = cores
     nvars = min(n, threads)
     variables = list(range(nvars))
     cands = [(1 << n) - 1] * n
@@ -87,8 +93,8 @@ def cpu_baseline(cfg, X, target_s=15.0):
     t0 = time.perf_counter()
     c = oracle.score_sample(ds, lam, variables, cands, k, frac, threads)
     dt = time.perf_counter() - t0
-    return {"value": c / dt, "unit": "parent-set scores/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
-            "cpu_quota": cpu_quota(),
+    return {"value": c / dt, "unit": "parent-set scores/s", "cores": cores, "threads": threads, "kind": "port",
+            "cpu": cpu_model(), "cpu_quota": q, "affinity_cpus": len(os.sched_getaffinity(0)),
             "sample": f"CPU oracle (C restatement, per-set OLS over all N rows) on {nvars} of {n} variables, "
                       f"first {frac:.4f} of every layer 1..{k} in Gosper order: {c} parent sets in {dt:.2f} s "
                       f"on {threads} threads"}
@@ -98,11 +104,6 @@ PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", 
 # the scorer's passes were re-taken in round 4 (the kernels timed now); the
 # sweep's kernel is unchanged since round 2
 PMC_TRAFFIC = os.path.join(os.path.dirname(PROFILES), "r4", "pmc_traffic.json")
-
-
-def step_sets_by_layer(cfg):
-    """{L: parent sets of L parents} over the variables of this step (cfg['msz'])."""
-    return {L: sum(math.comb(m, L) for m in cfg["msz"]) for L in range(0, cfg["k"] + 1)}
 
 
 def pmc_traffic(cfg, sets, label):
@@ -119,31 +120,15 @@ def pmc_traffic(cfg, sets, label):
     return t["traffic_bytes_per_launch"], "profiles/r4/pmc_traffic.json"
 
 
-ROOF_KERNELS = ["score_pipe", "score_layer_{k}_rest", "walk_{k}_rest"]
+ROOF_KERNELS = ["score_layer_{k}_rest", "walk_{k}_rest"]
 
 
-def roofline(ctx, cfg, per_layer_sets, steps, step_sets=None, step_bytes=None):
-    """Dominant unit.  With the persistent pipeline (score_pipe) it is the one
-    launch that decides every set of the call: its algorithmic bytes are the
-    step's (4 (L + 1) per set of layer L) over its average launch
-    duration.  With the layer launches it is the layer-k 'rest' launch (sets
-    without variable 0): the scoring kernel plus, with the two-pass scorer
-    (score_variant bit 4), the walk kernel over the sets it queued -- both
-    are one layer's decision, so their average durations are summed (rocprof
-    lists them separately)."""
+def roofline(ctx, cfg, per_layer_sets, steps):
+    """Dominant unit: the layer-k 'rest' launch (sets without variable 0):
+    the scoring kernel plus, with the two-pass scorer (score_variant bit 4),
+    the walk kernel over the sets it queued -- both are one layer's decision,
+    so their average durations are summed (rocprof lists them separately)."""
     k = cfg["k"]
-    pp = ctx.profile_get("score_pipe")
-    if pp is not None and step_bytes is not None:
-        traffic, traffic_src = pmc_traffic(cfg, step_sets, "score_pipe")
-        fl = sum(c * (2 * L ** 3 / 3 + 2 * L * L + 2 * L) for L, c in step_sets_by_layer(cfg).items())
-        return ({"bound": "hbm", "achieved": step_bytes / (pp["avg_ms"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                 "unit": "GB/s", "frac": step_bytes / (pp["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                 "traffic": traffic, "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
-                 "kernel": "score_pipe", "avg_launch_ms": pp["avg_ms"], "launches": pp["count"],
-                 "launches_per_step": 1, "sets_per_launch": step_sets,
-                 "algorithmic_bytes_per_launch": step_bytes,
-                 "bytes_per_set": "4 (L + 1) for a set of L parents (L direct-subset reads + 1 score write)",
-                 "fp64_tflops": fl / (pp["avg_ms"] * 1e-3) / 1e12}, pp)
     names = [f"score_layer_{k}_rest", f"walk_{k}_rest"]
     ps = [ctx.profile_get(nm) for nm in names]
     if ps[0] is None:
@@ -682,9 +667,7 @@ def main():
         ctx.score(variables, cands, k)
         ts_solo.append(time.perf_counter() - a)
     step_bytes = sum(math.comb(msz[v], L) * 4 * (L + 1) for v in variables for L in range(0, k + 1))
-    step_sets = sum(math.comb(msz[v], L) for v in variables for L in range(0, k + 1))
-    roof, _ = roofline(ctx, dict(cfg, k=kk, msz=[msz[v] for v in variables]), per_launch, solo_calls, step_sets,
-                       step_bytes)
+    roof, _ = roofline(ctx, dict(cfg, k=kk, msz=[msz[v] for v in variables]), per_launch, solo_calls)
     ctx.profile(False)
     if roof is not None:
         roof["note"] = ("one call at a time on one stream (context 0 after the timed region, %d calls): the "

@@ -112,9 +112,20 @@ int ulg_cbic_score_finish(ulg_ctx *ctx, int64_t *total_stored, int64_t *total_sc
  * [offsets[i], offsets[i+1]); within a variable, sets are ordered by
  * (|set|, set value) -- the reference's Gosper insertion order.
  * device_ptrs = 1: sets/scores/offsets are device pointers (e.g. torch
- * tensors on this context's device); 0: host pointers. */
+ * tensors on this context's device); 0: host pointers.
+ * Stream contract: the copies run on the context's own stream, and the call
+ * is synchronous -- it returns after they are complete, with host or device
+ * pointers alike, so the destination may be read on any stream afterwards.
+ * The copies are NOT ordered after work another stream queued on the
+ * destination (e.g. a torch zero fill on torch's current stream): the caller
+ * must finish that work first, or record an event after it and pass it to
+ * ulg_stream_wait_event before this call. */
 int ulg_cbic_fetch(ulg_ctx *ctx, uint64_t *sets, float *scores,
                    int64_t *offsets, int device_ptrs);
+/* The context's stream waits (on the device, no host sync) for a hipEvent_t
+ * the caller recorded on another stream of the same device; every later
+ * launch and copy of the context is ordered after it. */
+int ulg_stream_wait_event(ulg_ctx *ctx, void *event);
 /* Convenience: ulg_cbic_score + ulg_cbic_fetch to host buffers of
  * capacity cap entries; returns ULG_ERR_ARG if cap is too small. */
 int ulg_cbic_score_vars(ulg_ctx *ctx, const int *vars, int nv,
@@ -293,15 +304,6 @@ int ulg_sweep_shard_end(ulg_ctx *ctx, uint64_t *vpar, int *order, float *goal_co
  * "walk_small_sets" (>= 0, default 200000): a layer-6 launch of fewer sets
  * walks one set per lane instead of four (the small launches of 4- and
  * 8-rank shares end with their longest walk wave).
- * "score_pipe" (0/1, default 0): every layer unrolled (k <= 6) and variant
- * 113: the whole call is one persistent launch (cbic_pipe.hip) whose waves
- * claim score tiles and walk chunks from per-(variable, stage) device
- * counters, a variable's next stage released as soon as its previous one is
- * decided; "pipe_rounds" (1..64, default 2; at most 2 take effect): 64-set
- * rounds per two-pass tile; "pipe_rounds_small" (1..64, default 1): per
- * one-pass tile; "pipe_occ" (2/3, default 2): waves per SIMD the kernel is
- * compiled for (3 spills a few registers).  A call with a time limit uses the
- * layer launches.
  * "table_budget_kb" (KiB; default 0 = half the free HBM): memory for the dense
  * best-score tables (16 B per entry incl. the host cost copy).  Lists whose
  * tables over all variables exceed it (e.g. n = 32 with a full skeleton) are

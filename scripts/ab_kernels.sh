@@ -10,7 +10,7 @@ mkdir -p ${OUT}
 for lib in ${LIBS:-urlearning-cpp_amd/libulg.so ab/*.so}; do
   tag=$(basename ${lib} .so)
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d ${OUT}/${tag} -o run -- \
-    python3 scripts/pipe_probe.py --cases ${CASES:-c3 c5} --modes 0 --reps 10 --options score_streams=1 --lib ${lib} \
+    python3 scripts/score_probe.py --cases ${CASES:-c3 c5} --reps 10 --options score_streams=1 --lib ${lib} \
     > ${OUT}/${tag}.log 2>&1
   echo "${tag}: $(grep -ho '"case": "c[35]".*"layers_ms": \[[0-9.]*' ${OUT}/${tag}.log | sed 's/"n".*"layers_ms"/ms/' | tr '\n' ' ')"
 done

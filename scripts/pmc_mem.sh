@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-pmc_mem}
 mkdir -p ${OUT}
-CMD="python3 scripts/pipe_probe.py --modes 0 --reps 2 ${CMD_ARGS:---cases c5 --options score_streams=1}"
+CMD="python3 scripts/score_probe.py --reps 2 ${CMD_ARGS:---cases c5 --options score_streams=1}"
 i=0
 for ctrs in "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum TA_BUSY_avr TA_TA_BUSY_sum GRBM_GUI_ACTIVE" \
             "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_SERIALIZATION_STALL_sum TCP_UTCL1_THRASHING_STALL_sum" \

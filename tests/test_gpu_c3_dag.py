@@ -22,7 +22,7 @@ FIXTURE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c3
 
 
 @pytest.mark.timeout(600)
-def test_c3_pipeline_equals_oracle(ulg_ctx):
+def test_c3_scoring_equals_oracle(ulg_ctx):
     ref = json.load(open(FIXTURE))
     n, N, k = 25, 10000, 6
     X, _ = synth.gaussian_sem(n, N, 9200)

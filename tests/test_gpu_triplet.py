@@ -271,8 +271,10 @@ def test_triplet_budget_interrupts_a_running_search(ulg_ctx):
     assert ulg_ctx.info("out_of_time") == 0 and ref["distinct"] == 1
     try:
         # the host's speed sets the uncut time (0.55-1.5 s across boxes): the
-        # budget is a tenth of it, so the search outlasts the budget by far
-        assert uncut > 0.2, uncut
+        # budget is a tenth of it, so the search outlasts the budget by far;
+        # a host too fast to leave a measurable cut proves nothing either way
+        if uncut < 0.2:
+            pytest.skip(f"uncut search took {uncut:.3f} s: too short to measure a cut")
         budget_ms = max(20, int(100 * uncut))
         ulg_ctx.search_from_scores()  # an empty memo: the cluster is searched again
         ulg_ctx.set_option("time_limit_ms", budget_ms)

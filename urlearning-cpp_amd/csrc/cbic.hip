@@ -32,7 +32,6 @@
 #include "search_internal.h"
 #include "host_walk.h"
 #include "cbic_dev.h"
-#include "cbic_pipe.h"
 
 using namespace ulg;
 
@@ -2205,13 +2204,6 @@ int ulg_cbic_score_finish(ulg_ctx *c, int64_t *total_stored, int64_t *total_scor
         ULG_HIP(c, hipStreamSynchronize(c->stream));
         prof_collect(c);
         c->total_stored = (int64_t)*c->async_pinned;
-        if (c->pipe_pending) {
-            c->pipe_pending = false;
-            if (int rcp = pipe_check(c)) {
-                c->scored = false;
-                return rcp;
-            }
-        }
     }
     if (!c->scored) return set_err(c, ULG_ERR_STATE, "ulg_cbic_score_finish: nothing scored");
     if (total_stored) *total_stored = c->total_stored;
@@ -2335,24 +2327,10 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
         sa.hsub = c->d_hsub.p;
     }
     const char *wck = std::getenv("ULG_WALK_CLOCK");  // walk diagnostics (synchronising)
-    // Every layer unrolled (k <= 6) with the default variant: the whole call is
-    // one persistent launch (cbic_pipe.hip) instead of two launches per layer
-    // and phase.  The -r budget (checked between layers) and the diagnostic
-    // variants keep the layer launches.
-    const bool use_pipe = c->score_pipe && kmax <= kPipeMaxL && variant == 113 && c->time_limit_ms == 0 && !wck &&
-                          total_slots < (1ull << 32) && pipe_lds(n, nv, S).total <= 64 * 1024;
-    PipeArgs pargs{};
-    if (use_pipe) {
-        if ((rc = pipe_prepare(c, nv, S, kmax, max_parents, mv, meta, pargs))) return rc;
-        if (!c->pipe_stall_pinned) {
-            ULG_HIP(c, hipHostMalloc((void **)&c->pipe_stall_pinned, sizeof(unsigned int), hipHostMallocDefault));
-            *c->pipe_stall_pinned = 0;
-        }
-    }
     // Variables never read each other's slabs, so they are striped over G
     // groups on concurrent streams: a group's latency-bound walk kernels
     // overlap the other groups' scoring kernels.  Diagnostics run on one.
-    const int G = ((variant & 16) && !wck && !use_pipe) ? std::max(1, std::min(c->score_streams, nv)) : 1;
+    const int G = ((variant & 16) && !wck) ? std::max(1, std::min(c->score_streams, nv)) : 1;
     while ((int)c->aux_streams.size() < G - 1) {
         hipStream_t st;
         ULG_HIP(c, hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -2397,7 +2375,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
             }
     // queue counters per (group, layer, phase), then the wide walks' error flag
     const size_t nqc = (size_t)G * 2 * (kmax + 1) + 1;
-    if (((variant & 16) && !use_pipe) || kmax > kMaxL) {
+    if ((variant & 16) || kmax > kMaxL) {
         if ((rc = ensure(c, c->d_queue, (size_t)G * qwords)) || (rc = ensure(c, c->d_qcount, nqc)) ||
             (rc = ensure(c, c->d_wqueue, (size_t)G * wqwords)))
             return rc;
@@ -2476,7 +2454,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     // events, the profiling events) and replayed, which removes the host
     // launch path of ~40 kernels per call (score_graph, default on).
     const bool use_graph =
-        c->score_graph && !c->prof && kmax <= kMaxL && c->time_limit_ms == 0 && !wck && !std::getenv("ULG_PIPE_STATS");
+        c->score_graph && !c->prof && kmax <= kMaxL && c->time_limit_ms == 0 && !wck;
     std::vector<uint64_t> gkey;
     // An early return between BeginCapture and EndCapture (a failed launch,
     // "layer too large") must not leave the context stream capturing: the
@@ -2505,10 +2483,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                      (uint64_t)(uintptr_t)c->out_offsets.p, (uint64_t)(uintptr_t)c->d_blk.p,
                      (uint64_t)(uintptr_t)c->gram.p, (uint64_t)(uintptr_t)c->d_binom.p,
                      (uint64_t)(uintptr_t)c->d_binom64.p, (uint64_t)(uintptr_t)c->d_hsub.p, (uint64_t)total_slots,
-                     (uint64_t)use_pipe, (uint64_t)c->pipe_rounds, (uint64_t)c->pipe_rounds_small,
-                     (uint64_t)c->score_small_layers, (uint64_t)c->pipe_occ, (uint64_t)c->pipe_chain, (uint64_t)c->pipe_grid_max, (uint64_t)(uintptr_t)c->d_pwork.p, (uint64_t)(uintptr_t)c->d_pstate.p,
-                     (uint64_t)(uintptr_t)c->d_pqueue.p, (uint64_t)(uintptr_t)c->d_pstages.p,
-                     (uint64_t)(uintptr_t)c->d_pinit.p});
+                     (uint64_t)c->score_small_layers});
         for (int i = 0; i < nv; ++i) gkey.push_back((uint64_t)vars[i]);
         for (int i = 0; i < nv; ++i) gkey.push_back(candidates[i]);
         for (const std::string &nm : c->prof_only) gkey.push_back(std::hash<std::string>{}(nm));
@@ -2524,8 +2499,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     }
     {
     const size_t pend0 = c->pending.size();
-    if (use_pipe && (rc = pipe_launch(c, pargs, c->stream))) return rc;
-    for (int L = 1; L <= kmax && !use_pipe; ++L) {
+    for (int L = 1; L <= kmax; ++L) {
         for (int ph = 0; ph < 2; ++ph) {
             if (L <= Ls) {
                 const size_t wo = ((size_t)L * 2 + ph) * (nv + 1);
@@ -2703,8 +2677,6 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     }
     }
 launched:
-    if (use_pipe) ULG_HIP(c, hipMemcpyAsync(c->pipe_stall_pinned, pargs.done + 1, 4, hipMemcpyDeviceToHost, c->stream));
-    c->pipe_pending = use_pipe;
     if (async && kmax <= kMaxL && c->time_limit_ms == 0) {
         // no host sync on this path: the stored count is copied into pinned
         // memory behind the launches and collected by ulg_cbic_score_finish
@@ -2729,11 +2701,6 @@ launched:
     if (kmax > kMaxL) ULG_HIP(c, hipMemcpyAsync(&wide_err, c->d_qcount.p + nqc - 1, 8, hipMemcpyDeviceToHost, c->stream));
     ULG_HIP(c, hipStreamSynchronize(c->stream));
     prof_collect(c);
-    if (c->pipe_pending) {
-        c->pipe_pending = false;
-        if ((rc = pipe_check(c))) return rc;
-        pipe_report(c);
-    }
     if (wide_err)
         return set_err(c, ULG_ERR_UNSUPPORTED,
                        "ulg_cbic_score: a find_best_subset_score walk in a wide layer exceeded its cap (2^30 steps "

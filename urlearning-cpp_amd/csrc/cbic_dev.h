@@ -1,5 +1,5 @@
-// cbic_dev.h -- device building blocks of the cBIC scorer (cbic.hip's layer
-// kernels and cbic_pipe.hip's persistent pipeline share them).
+// cbic_dev.h -- device building blocks of the cBIC scorer's layer kernels
+// (cbic.hip).
 //
 // Reference semantics (ninalu/urlearning-cpp, urlearning/):
 //   colex rank == Gosper enumeration index    base/typedefs.h:692-697
@@ -18,19 +18,11 @@ using namespace ulg;
 
 constexpr int kBlock = 256;
 
-// How a kernel loads slab values written by other workgroups: plain loads
-// across kernel boundaries (the layer kernels), agent-scope sc1 loads inside
-// one persistent launch (cbic_pipe.hip: they bypass the CU's L1, which other
-// CUs' stores never refresh; MI355X_MICROARCH.md, inter-workgroup visibility).
+// How a kernel loads slab values written by other workgroups: every writer
+// of a slab is an earlier launch on the same stream (a layer is complete
+// before the next one starts), so plain loads see its values.
 struct LdPlain {
     __device__ static __forceinline__ float ld(const float *p) { return *p; }
-};
-typedef __attribute__((address_space(1))) uint32_t gu32;
-typedef __attribute__((address_space(1))) uint64_t gu64;
-struct LdSc1 {
-    __device__ static __forceinline__ float ld(const float *p) {
-        return __uint_as_float(__hip_atomic_load((const gu32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    }
 };
 
 __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
@@ -607,7 +599,7 @@ __device__ __forceinline__ void walk_sliced(uint32_t T, uint32_t pv, uint32_t ac
 // Gram matrix g = Z'Z (n x n, row-major, in LDS): Cholesky of G[P,P],
 // y = L^-1 G[P,v], RSS = G[v,v] - |y|^2, score = N ln(RSS / N) + lambda ln(N) L
 // (BIC_OLS.cpp:366), returned as float like the reference.  Every layer kernel
-// and the persistent pipeline use this one operation order.
+// uses this one operation order.
 template <int L>
 __device__ __forceinline__ float cbic_set_score(const double *g, int n, int v, const int (&gv)[L], double N,
                                                 double lambda) {

@@ -587,7 +587,8 @@ struct HostPmu {
             }
         }
     }
-    void stop(int64_t (&acc)[3]) {
+    // first: acc holds nothing yet (it reads -1 until a counter is read)
+    void stop(int64_t (&acc)[3], bool first) {
         for (int i = 0; i < 3; ++i) {
             if (fd[i] < 0) {
                 acc[i] = -1;
@@ -595,7 +596,8 @@ struct HostPmu {
             }
             ioctl(fd[i], PERF_EVENT_IOC_DISABLE, 0);
             uint64_t v = 0;
-            if (read(fd[i], &v, sizeof v) == (ssize_t)sizeof v && acc[i] >= 0) acc[i] += (int64_t)v;
+            if (read(fd[i], &v, sizeof v) == (ssize_t)sizeof v && (first || acc[i] >= 0))
+                acc[i] = (first ? 0 : acc[i]) + (int64_t)v;
             else acc[i] = -1;
             close(fd[i]);
             fd[i] = -1;
@@ -642,7 +644,9 @@ int ulg_astar_scc(ulg_ctx *c, const uint64_t *edges, int pd_count, int mode, uin
     if (net_text && net_cap > 0) net_text[0] = 0;
     if (mode == ULG_ASTAR_GPU) return astar_gpu(c, edges, vpar, order, goal_cost, expanded);
     if (mode != ULG_ASTAR_EXACT) return set_err(c, ULG_ERR_ARG, "ulg_astar: unknown mode");
-    c->exact_pmu[0] = c->exact_pmu[1] = c->exact_pmu[2] = 0;
+    // -1 (not measured) unless a component's search opens the counters
+    c->exact_pmu[0] = c->exact_pmu[1] = c->exact_pmu[2] = -1;
+    bool pmu_first = true;
     std::vector<uint64_t> comps;
     const bool good = edges != nullptr;
     if (good) components(edges, n, comps);
@@ -672,7 +676,8 @@ int ulg_astar_scc(ulg_ctx *c, const uint64_t *edges, int pd_count, int mode, uin
         HostPmu pmu;
         rc = dense ? astar_dense(c, T, edges, good, ancestors, comp, expanded, &hang, r, dl)
                    : astar_one(c, T, edges, good, ancestors, comp, expanded, &hang, r, dl);
-        pmu.stop(c->exact_pmu);
+        pmu.stop(c->exact_pmu, pmu_first);
+        pmu_first = false;
         if (rc) return rc;
         if (!r.found) { fail = true; continue; }
         // each component rewrites netFile and netFile.csv (astar_main.cpp:470,519)

@@ -312,11 +312,20 @@ int cluster_astar(Triplet &t, uint64_t cluster, std::vector<uint64_t> &op) {
 // :176-219 reverse DP) on the host, with search_build_pdb's exact float
 // operations and order (pdb_bs_kernel + pdb_layer_kernel), for the parallel
 // cluster searches: each needs its own database while the device holds one.
+// cancel (the -r watchdog of a look-ahead pool): checked per DP layer, so a
+// 24-variable group stops within one layer's work; P.cancelled tells.
 struct HostPdb {
     std::vector<uint64_t> groups, pd_off;
     std::vector<float> pd;
+    bool cancelled = false;
 };
-bool pdb_host(const HostTables &T, uint64_t scc, int pd_count, HostPdb &P) {
+bool pdb_host(const HostTables &T, uint64_t scc, int pd_count, HostPdb &P,
+              const std::atomic<bool> *cancel = nullptr) {
+    P.cancelled = false;
+    auto stopped = [&]() {
+        if (cancel && cancel->load(std::memory_order_relaxed)) P.cancelled = true;
+        return P.cancelled;
+    };
     const int remaining = __builtin_popcountll(scc);
     const int pds = (int)std::ceil((float)remaining / pd_count);
     int var = scc ? __builtin_ctzll(scc) : -1;
@@ -350,6 +359,7 @@ bool pdb_host(const HostTables &T, uint64_t scc, int pd_count, HostPdb &P) {
             if ((grp >> b) & 1ull) bitpos[q++] = b;
         bsv.assign((size_t)s << s, 0.0f);
         for (uint64_t R = 1; R < (1ull << s); ++R) {
+            if ((R & 0xFFFF) == 0 && stopped()) return true;
             uint64_t Rg = 0;
             for (int b = 0; b < s; ++b)
                 if ((R >> b) & 1ull) Rg |= 1ull << bitpos[b];
@@ -360,7 +370,8 @@ bool pdb_host(const HostTables &T, uint64_t scc, int pd_count, HostPdb &P) {
             }
         }
         float *pd = P.pd.data() + P.pd_off[g];
-        for (int layer = 1; layer <= s; ++layer)
+        for (int layer = 1; layer <= s; ++layer) {
+            if (stopped()) return true;
             for (uint64_t R = 1; R < (1ull << s); ++R) {
                 if (__builtin_popcountll(R) != layer) continue;
                 float cur = 0.0f;
@@ -371,6 +382,7 @@ bool pdb_host(const HostTables &T, uint64_t scc, int pd_count, HostPdb &P) {
                 }
                 pd[R] = cur;
             }
+        }
     }
     return true;
 }
@@ -449,8 +461,12 @@ struct SearchPool {
             state[cl] = 2;
             lk.unlock();
             ClusterRun R;
-            const bool ok = pdb_host(base, cl, pd_count, P);
-            if (ok) {
+            // a cluster dequeued after the watchdog fired is not started, and
+            // a PDB build it interrupts ends the search as cancelled
+            const bool ok = cancel.load(std::memory_order_relaxed) || pdb_host(base, cl, pd_count, P, &cancel);
+            if (cancel.load(std::memory_order_relaxed) || P.cancelled) {
+                R.cancelled = true;
+            } else if (ok) {
                 HostTables T = base;
                 T.pd = P.pd.data();
                 T.groups = P.groups;

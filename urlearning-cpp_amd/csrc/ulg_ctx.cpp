@@ -156,8 +156,6 @@ void ulg_destroy(ulg_ctx *c) {
     c->wide_pinned = nullptr;
     if (c->async_pinned) (void)hipHostFree(c->async_pinned);
     c->async_pinned = nullptr;
-    if (c->pipe_stall_pinned) (void)hipHostFree(c->pipe_stall_pinned);
-    c->pipe_stall_pinned = nullptr;
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
     c->event_pool.clear();
     for (hipStream_t s : c->aux_streams) (void)hipStreamDestroy(s);
@@ -167,7 +165,6 @@ void ulg_destroy(ulg_ctx *c) {
     release(c->raw); release(c->z); release(c->gram); release(c->partials); release(c->colstat);
     release(c->table); release(c->d_tbl_off); release(c->d_work); release(c->d_blk);
     release(c->d_cand); release(c->d_meta); release(c->d_binom); release(c->d_binom64); release(c->d_wqueue); release(c->d_wbits); release(c->d_stats); release(c->d_dump); release(c->d_queue); release(c->d_qcount); release(c->d_workg); release(c->d_vwork); release(c->d_hq); release(c->d_hqc); release(c->d_hmax); release(c->d_hoff); release(c->d_hmeta); release(c->d_scount); release(c->d_hsub);
-    release(c->d_pstate); release(c->d_pqueue); release(c->d_pstages); release(c->d_pinit); release(c->d_pstats); release(c->d_pwork);
     release(c->out_sets); release(c->out_scores); release(c->out_offsets);
     release(c->qbuf_in); release(c->qbuf_out);
     pss_release(c);
@@ -216,39 +213,9 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         c->sweep_xcd = (int)value;
         return ULG_OK;
     }
-    if (std::strcmp(name, "score_pipe") == 0) {
-        if (value < 0 || value > 1) return set_err(c, ULG_ERR_ARG, "score_pipe must be 0 or 1");
-        c->score_pipe = (int)value;
-        return ULG_OK;
-    }
-    if (std::strcmp(name, "pipe_occ") == 0) {
-        if (value != 2 && value != 3) return set_err(c, ULG_ERR_ARG, "pipe_occ must be 2 or 3");
-        c->pipe_occ = (int)value;
-        return ULG_OK;
-    }
-    if (std::strcmp(name, "pipe_chain") == 0) {
-        if (value < 0 || value > 1) return set_err(c, ULG_ERR_ARG, "pipe_chain must be 0 or 1");
-        c->pipe_chain = (int)value;
-        return ULG_OK;
-    }
     if (std::strcmp(name, "walk_small_sets") == 0) {
         if (value < 0) return set_err(c, ULG_ERR_ARG, "walk_small_sets must be >= 0");
         c->walk_small_sets = value;
-        return ULG_OK;
-    }
-    if (std::strcmp(name, "pipe_grid_max") == 0) {
-        if (value < 0 || value > (1 << 20)) return set_err(c, ULG_ERR_ARG, "pipe_grid_max must be 0..2^20");
-        c->pipe_grid_max = (int)value;
-        return ULG_OK;
-    }
-    if (std::strcmp(name, "pipe_rounds") == 0) {
-        if (value < 1 || value > 64) return set_err(c, ULG_ERR_ARG, "pipe_rounds must be 1..64");
-        c->pipe_rounds = (int)value;
-        return ULG_OK;
-    }
-    if (std::strcmp(name, "pipe_rounds_small") == 0) {
-        if (value < 1 || value > 64) return set_err(c, ULG_ERR_ARG, "pipe_rounds_small must be 1..64");
-        c->pipe_rounds_small = (int)value;
         return ULG_OK;
     }
     if (std::strcmp(name, "score_graph") == 0) {
@@ -339,6 +306,13 @@ int ulg_get_info(ulg_ctx *c, const char *name, int64_t *value) {
         return ULG_OK;
     }
     return set_err(c, ULG_ERR_ARG, std::string("unknown info: ") + name);
+}
+
+int ulg_stream_wait_event(ulg_ctx *c, void *event) {
+    if (!c || !event) return ULG_ERR_ARG;
+    ULG_HIP(c, hipSetDevice(c->device));
+    ULG_HIP(c, hipStreamWaitEvent(c->stream, (hipEvent_t)event, 0));
+    return ULG_OK;
 }
 
 int ulg_profile_enable(ulg_ctx *c, int on) {

@@ -164,11 +164,15 @@ class ListExchange:
             self.sets_ptr = self.stage.data_ptr()
         else:
             self.sets_ptr = base + self.hdr
+        self._fills_done = None
         if self.device.type == "cuda":
             # the zero fills run on torch's stream and libulg writes these
-            # blocks on its own: without this wait a fill could land after the
-            # scorer's copy and zero the lists (seen once in ~10 two-rank runs)
-            torch.cuda.current_stream(self.device).synchronize()
+            # blocks on its own (ulg.h's stream contract: ulg_cbic_fetch is not
+            # ordered after other streams' work): the next fetch makes the
+            # context's stream wait for this event, so no fill can land after
+            # the scorer's copy and zero the lists
+            self._fills_done = torch.cuda.Event()
+            self._fills_done.record(torch.cuda.current_stream(self.device))
 
     def _sets_view(self, blocks):
         """[ws, cap] int64 sets of gathered blocks [ws, block] (uint8)."""
@@ -183,6 +187,9 @@ class ListExchange:
         kind, a, b = self._src
         if kind == "ctx":
             ctx, stored = a, b
+            if self._fills_done is not None:
+                ctx.stream_wait_event(self._fills_done)
+                self._fills_done = None
             if stored <= self.cap:
                 ctx.fetch_device(self.sets_ptr, self.scores_ptr, self.offs_ptr)
                 if self.narrow:

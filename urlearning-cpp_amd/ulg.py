@@ -167,8 +167,16 @@ class Context:
         self._check(lib().ulg_cbic_fetch(self._h, _ptr(sets), _ptr(scores), _ptr(offs), 0), "ulg_cbic_fetch")
         return offs, sets[:total_stored], scores[:total_stored]
 
+    def stream_wait_event(self, event):
+        """ulg_stream_wait_event: this context's stream waits for a
+        torch.cuda.Event (or a raw hipEvent_t handle) recorded on another
+        stream of the same device."""
+        h = event.cuda_event if hasattr(event, "cuda_event") else int(event)
+        self._check(lib().ulg_stream_wait_event(self._h, C.c_void_p(h)), "ulg_stream_wait_event")
+
     def fetch_device(self, sets_ptr: int, scores_ptr: int, offsets_ptr: int):
-        """Copy results into caller-owned device buffers (e.g. torch tensors)."""
+        """Copy results into caller-owned device buffers (e.g. torch tensors).
+        Synchronous on the context's stream; see ulg.h's stream contract."""
         self._check(lib().ulg_cbic_fetch(self._h, C.c_void_p(sets_ptr), C.c_void_p(scores_ptr),
                                          C.c_void_p(offsets_ptr), 1), "ulg_cbic_fetch")
 
