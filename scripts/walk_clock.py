@@ -17,6 +17,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--case", default="c3")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "wclock"))
+    ap.add_argument("--options", default="", help="name=value,... (ulg_set_option)")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     os.environ["ULG_WALK_CLOCK"] = a.out
@@ -27,6 +28,9 @@ def main():
     X, _ = synth.gaussian_sem(n, N, 9200)
     ctx = ulg.Context(0)
     ctx.set_option("score_streams", 1)
+    for kv in filter(None, a.options.split(",")):
+        k_, v_ = kv.split("=")
+        ctx.set_option(k_, int(v_))
     ctx.load(X, 2.0)
     full = (1 << n) - 1
     ctx.score(list(range(n)), [full] * n, 6)

@@ -230,6 +230,76 @@ __device__ __forceinline__ void queue_walk(const BS &present, const BS &hi, uint
 
 
 
+#ifdef ULG_GATHER_STATS
+// Diagnostic build only (scripts/gather_stats.py): per (layer, phase) counts of
+// what the presence gathers of the compacted sets find.
+__device__ unsigned long long g_gstats[2 * (kMaxL + 1) * 16];
+
+// Compile-time masks over the local subsets t of a layer-L set: the keys the
+// full gather reads, the keys without child i's removed member (child i =
+// P minus its i-th member in compact order), the keys holding variable 0.
+template <int L, int PHASE>
+struct KeyMasks {
+    static constexpr int Q = PHASE == 0 ? L : L + 1;
+    static constexpr int W = bits_words(L);
+    uint64_t key[W], miss[L][W], v0[W];
+    constexpr KeyMasks() : key{}, miss{}, v0{} {
+        constexpr PresList<L, PHASE, Q, 0> PL{};
+        for (int i = 0; i < PL.n; ++i) key[PL.t[i] >> 6] |= 1ull << (PL.t[i] & 63);
+        for (uint32_t t = 0; t < (1u << Q); ++t) {
+            if (t & 1u) v0[t >> 6] |= 1ull << (t & 63);
+            for (int i = 0; i < L; ++i) {
+                const int b = PHASE == 1 ? i + 1 : i;
+                if (!((t >> b) & 1u)) miss[i][t >> 6] |= 1ull << (t & 63);
+            }
+        }
+    }
+};
+
+template <int L, int PHASE, class BS>
+__device__ void gather_stats(const BS &present, const BS &hi, uint32_t hotA, uint32_t hotZ, bool z, bool queued) {
+    constexpr int W = BS::kWords;
+    constexpr KeyMasks<L, PHASE> KM{};
+    uint64_t cov[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) cov[j] = hi.word(j);
+    cover_words<W>(cov);
+    unsigned long long c[16] = {};
+    c[0] = 1;
+    c[1] = __builtin_popcount(hotA);
+    c[2] = __builtin_popcount(hotZ);
+    const uint32_t sel = (PHASE == 1 && z) ? hotZ : hotA;
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+        uint64_t need = 0, hrel = 0;
+#pragma unroll
+        for (int i = 0; i < L; ++i) {
+            if ((sel >> i) & 1u) need |= KM.miss[i][j];
+            if ((hotA >> i) & 1u) hrel |= KM.miss[i][j] & ~KM.v0[j];
+            if (PHASE == 1 && z && ((hotZ >> i) & 1u)) hrel |= KM.miss[i][j] & KM.v0[j];
+        }
+        need &= KM.key[j];
+        hrel &= KM.key[j];
+        const uint64_t pr = present.word(j) & KM.key[j], hw = hi.word(j) & KM.key[j], cv = cov[j] & KM.key[j];
+        c[3] += __builtin_popcountll(pr);
+        c[4] += __builtin_popcountll(hw);
+        c[5] += __builtin_popcountll(need);
+        c[6] += __builtin_popcountll(hrel);
+        c[7] += __builtin_popcountll(cv);
+        c[8] += __builtin_popcountll(pr & need);
+        c[9] += __builtin_popcountll(hw & ~hrel);
+        c[10] += __builtin_popcountll(cv & ~need);
+        c[11] += __builtin_popcountll(KM.key[j]);
+        c[13] += __builtin_popcountll((hrel | cv) & KM.key[j]);
+        c[14] += __builtin_popcountll(pr & ~need);
+    }
+    c[12] = queued;
+    unsigned long long *g = g_gstats + (L * 2 + PHASE) * 16;
+#pragma unroll
+    for (int i = 0; i < 15; ++i) atomicAdd(g + i, c[i]);
+}
+#endif
+
 // PHASE 0: sets containing variable 0; 1: the rest.  V = variant bits (see
 // ulg_set_option "score_variant"), compile-time so each form gets its own
 // register allocation.
@@ -308,6 +378,10 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         float hch = absent_f();  // max over the proper nonempty subsets of P
         float hz = absent_f();   // ... and over the toggles P\a + {0}
         bool dh = false;         // a direct child >= -ts
+#ifdef ULG_GATHER_STATS
+        uint32_t hotA = 0u;      // children P\a_i holding a key >= -ts (hsub)
+        uint32_t hotZ = 0u;      // toggled children P\a_i + {0} holding one
+#endif
         {
             float ch[L], cv[L], zv[L];
             const uint32_t o1 = (uint32_t)toff[vbase + L - 1], o0 = (uint32_t)toff[vbase + L];
@@ -325,10 +399,21 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
                 if constexpr (L > 1) {
                     hch = fmaxf(hch, ch[i]);
                     dh |= cv[i] >= thr;
+#ifdef ULG_GATHER_STATS
+                    hotA |= (ch[i] >= thr) ? 1u << i : 0u;
+#endif
                 }
-                if constexpr (PHASE == 1) hz = fmaxf(hz, zv[i]);
+                if constexpr (PHASE == 1) {
+                    hz = fmaxf(hz, zv[i]);
+#ifdef ULG_GATHER_STATS
+                    hotZ |= (zv[i] >= thr) ? 1u << i : 0u;
+#endif
+                }
             }
             if (!z) hz = absent_f();
+#ifdef ULG_GATHER_STATS
+            if (!z) hotZ = 0u;
+#endif
         }
         bool need = false;
         float out;
@@ -364,12 +449,19 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
             eslot[k] = (uint32_t)slot;
             ets[k] = ts;
             ehch[k] = hch;
+#ifdef ULG_GATHER_STATS
+            evi[k] = vi | (int)(hotA << 8) | (int)(hotZ << 16);
+#else
             evi[k] = vi;
+#endif
         }
         __syncthreads();
         if (threadIdx.x >= *cnt) return;
         const int k = threadIdx.x;
-        const int vk = evi[k];
+        const int vk = evi[k] & 0xff;
+#ifdef ULG_GATHER_STATS
+        const uint32_t hk = (uint32_t)evi[k] >> 8;  // hotA | hotZ << 8
+#endif
         const bool zk = smeta[vk * 4 + 2] != 0;
         const float tk = ets[k];
         const uint64_t sk = eslot[k];
@@ -387,6 +479,15 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         gather_keys<L, PHASE, V, BS, LdPlain, 1>(present, hib, ls, -tk, binom, zk, a.table, toff + (uint64_t)vk * a.S);
         bool q;
         const bool dom = settle_rules<L, PHASE, BS, true>(present, hib, ls, q);
+#ifdef ULG_GATHER_STATS
+        if constexpr (W < 4) {
+            BS p2 = make_bits<BS>(lds_bits), h2 = make_bits<BS>(lds_bits);
+            p2.clear();
+            h2.clear();
+            gather_keys<L, PHASE, V, BS, LdPlain, 0>(p2, h2, ls, -tk, binom, zk, a.table, toff + (uint64_t)vk * a.S);
+            gather_stats<L, PHASE>(p2, h2, hk & 0xffu, hk >> 8, zk, q);
+        }
+#endif
         if (q) {
             gather_keys<L, PHASE, V, BS, LdPlain, 2>(present, hib, ls, -tk, binom, zk, a.table,
                                                     toff + (uint64_t)vk * a.S);
@@ -480,18 +581,14 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
 
 // Second half of a queued layer (variant bit 4): one wave (64 threads) per
 // 64*K queued sets.  Entry: table slot (low 32 bits) | ts bits (high 32), W
-// `hi` words, W open words (queue_walk).
-template <int L, int PHASE, int K>
-__global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, const unsigned long long *qcount,
-                                                         float *table, float *hsub, uint64_t *wclock) {
+// `hi` words, W open words (queue_walk).  walk_load gathers this lane's K
+// entries into the bit-sliced hi / open vectors (register r, field f <-
+// subset r*E + f, bit k of a field <- set k) and returns the alive mask.
+template <int L, int K>
+__device__ __forceinline__ uint32_t walk_load(const uint64_t *queue, uint64_t qn, uint64_t mine,
+                                              typename Sliced<L, K>::Vec &hiV, typename Sliced<L, K>::Vec &openV) {
     using S = Sliced<L, K>;
-    const uint64_t t_start = wclock ? wall_clock64() : 0;
     constexpr int W = bits_words(L);
-    const uint64_t qn = *qcount;
-    const uint64_t first = (uint64_t)blockIdx.x * 64 * S::K;
-    if (first >= qn) return;
-    const uint64_t mine = first + (uint64_t)threadIdx.x * S::K;
-    typename S::Vec hiV, openV;
 #pragma unroll
     for (int r = 0; r < S::NV; ++r) {
         hiV[r] = 0u;
@@ -533,6 +630,37 @@ __global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, 
             openV[r] |= os << k;
         }
     }
+    return alive;
+}
+
+// The decisions of this lane's sets: pruned (absent) or stored (-ts), and the
+// subset maxima raised to -ts when stored (variant bit 6).
+template <int K>
+__device__ __forceinline__ void walk_store(const uint64_t *queue, uint64_t qn, uint64_t mine, int W, uint32_t dom,
+                                           float *table, float *hsub) {
+#pragma nounroll
+    for (int k = 0; k < K; ++k) {
+        if (mine + k >= qn) break;
+        const uint64_t e0 = queue[(mine + k) * (uint64_t)(1 + 2 * W)];
+        const float ts = __uint_as_float((uint32_t)(e0 >> 32));
+        const bool d = (dom >> k) & 1u;
+        table[(uint32_t)e0] = d ? absent_f() : -ts;
+        if (hsub && !d) hsub[(uint32_t)e0] = fmaxf(hsub[(uint32_t)e0], -ts);
+    }
+}
+
+template <int L, int PHASE, int K>
+__global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, const unsigned long long *qcount,
+                                                         float *table, float *hsub, uint64_t *wclock) {
+    using S = Sliced<L, K>;
+    const uint64_t t_start = wclock ? wall_clock64() : 0;
+    constexpr int W = bits_words(L);
+    const uint64_t qn = *qcount;
+    const uint64_t first = (uint64_t)blockIdx.x * 64 * S::K;
+    if (first >= qn) return;
+    const uint64_t mine = first + (uint64_t)threadIdx.x * S::K;
+    typename S::Vec hiV, openV;
+    uint32_t alive = walk_load<L, K>(queue, qn, mine, hiV, openV);
     constexpr bool v0inP = PHASE == 0;
     constexpr uint32_t Plocal = v0inP ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
     uint32_t pvtop = 0;
@@ -552,15 +680,7 @@ __global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, 
         wclock[3 * blockIdx.x + 1] = wall_clock64();
         wclock[3 * blockIdx.x + 2] = pts;
     }
-#pragma nounroll
-    for (int k = 0; k < S::K; ++k) {
-        if (mine + k >= qn) break;
-        const uint64_t e0 = queue[(mine + k) * (uint64_t)(1 + 2 * W)];
-        const float ts = __uint_as_float((uint32_t)(e0 >> 32));
-        const bool d = (dom >> k) & 1u;
-        table[(uint32_t)e0] = d ? absent_f() : -ts;
-        if (hsub && !d) hsub[(uint32_t)e0] = fmaxf(hsub[(uint32_t)e0], -ts);  // subset maxima (variant bit 6)
-    }
+    walk_store<S::K>(queue, qn, mine, W, dom, table, hsub);
 }
 
 // ---- wide layers (kMaxL < L <= kWideMax) ------------------------------------
@@ -2196,6 +2316,21 @@ int ulg_cbic_gram(ulg_ctx *c, double *out) {
 static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candidates, int max_parents,
                       int64_t *total_stored, int64_t *total_scored, bool async);
 
+// ULG_WALK_CLOCK diagnostics: every walk wave's start / end clock and its
+// union points (steps) into <dir>/sliced_L<L>_p<phase>.bin (synchronising)
+static int dump_walk_clock(ulg_ctx *c, hipStream_t st, uint64_t sb, const char *dir, int L, int ph) {
+    std::vector<uint64_t> hw((size_t)3 * sb);
+    ULG_HIP(c, hipMemcpyAsync(hw.data(), c->d_dump.p, hw.size() * 8, hipMemcpyDeviceToHost, st));
+    ULG_HIP(c, hipStreamSynchronize(st));
+    char fn[512];
+    std::snprintf(fn, sizeof fn, "%s/sliced_L%d_p%d.bin", dir, L, ph);
+    if (FILE *f = std::fopen(fn, "wb")) {
+        std::fwrite(hw.data(), 8, hw.size(), f);
+        std::fclose(f);
+    }
+    return ULG_OK;
+}
+
 int ulg_cbic_score_finish(ulg_ctx *c, int64_t *total_stored, int64_t *total_scored) {
     if (!c) return ULG_ERR_ARG;
     if (c->async_pending) {
@@ -2588,17 +2723,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                         hipLaunchKernelGGL(sliced_fn(L, ph, wk), dim3((unsigned)sb), dim3(64), 0, st, sa.queue, qc,
                                            c->table.p, sa.hsub_out ? sa.hsub : nullptr, wck ? c->d_dump.p : nullptr);
                         prof_end_s(c, st);
-                        if (wck) {
-                            std::vector<uint64_t> hw((size_t)3 * sb);
-                            ULG_HIP(c, hipMemcpyAsync(hw.data(), c->d_dump.p, hw.size() * 8, hipMemcpyDeviceToHost, st));
-                            ULG_HIP(c, hipStreamSynchronize(st));
-                            char fn[512];
-                            std::snprintf(fn, sizeof fn, "%s/sliced_L%d_p%d.bin", wck, L, ph);
-                            if (FILE *f = std::fopen(fn, "wb")) {
-                                std::fwrite(hw.data(), 8, hw.size(), f);
-                                std::fclose(f);
-                            }
-                        }
+                        if (wck && (rc = dump_walk_clock(c, st, sb, wck, L, ph))) return rc;
                     }
                 }
             }
@@ -2791,5 +2916,18 @@ int ulg_quantize_costs(ulg_ctx *c, const float *scores, float *costs, int64_t co
     prof_collect(c);
     return ULG_OK;
 }
+
+#ifdef ULG_GATHER_STATS
+// diagnostic build: the gather counters (2 * (kMaxL + 1) * 16 values), then zeroed
+int ulg_diag_gather_stats(ulg_ctx *c, unsigned long long *out) {
+    if (!c || !out) return ULG_ERR_ARG;
+    ULG_HIP(c, hipSetDevice(c->device));
+    ULG_HIP(c, hipStreamSynchronize(c->stream));
+    ULG_HIP(c, hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gstats), sizeof(g_gstats)));
+    static const unsigned long long zero[2 * (kMaxL + 1) * 16] = {};
+    ULG_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(g_gstats), zero, sizeof(zero)));
+    return ULG_OK;
+}
+#endif
 
 }  // extern "C"

@@ -581,10 +581,10 @@ __device__ __forceinline__ void walk_sliced(uint32_t T, uint32_t pv, uint32_t ac
                 if (pi == u) continue;
                 npv |= pi << (4 * j);
                 ++j;
-                if (j == 1)
-                    walk_sliced<L, K, M - 1, DIAG, OV>(T2, npv, x, hiV, openV, alive, dom, pts, 0, M - 1 < 2 ? M - 1 : 2);
-                else
-                    walk_sliced<L, K, M - 1, DIAG, OV>(T2, npv, x, hiV, openV, alive, dom, pts, j - 1, j);
+                // one call site per level: two would inline the level below
+                // twice, 2^(L-1) copies of the deepest one (a ~40 KB kernel)
+                walk_sliced<L, K, M - 1, DIAG, OV>(T2, npv, x, hiV, openV, alive, dom, pts, j == 1 ? 0 : j - 1,
+                                                   j == 1 ? (M - 1 < 2 ? M - 1 : 2) : j);
                 sl_clear<L, K>(openV, T2, x);  // checked.insert(T2) for the sets that ran the call
                 x &= alive;
                 if (!wave_any(x)) break;
