@@ -101,23 +101,25 @@ def cpu_baseline(cfg, X, target_s=15.0):
 
 
 PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r2")
-# the scorer's passes were re-taken in round 4 (the kernels timed now); the
-# sweep's kernel is unchanged since round 2
-PMC_TRAFFIC = os.path.join(os.path.dirname(PROFILES), "r4", "pmc_traffic.json")
+# the scorer's counter passes of this round's kernels (scripts/r5_probe.sh +
+# pmc_r5_summarize.py on the same bench command); the sweep's kernel is
+# unchanged since round 2
+PMC_SCORER = os.path.join(os.path.dirname(PROFILES), "r5", "pmc_scorer.json")
 
 
-def pmc_traffic(cfg, sets, label):
-    """HBM bytes per launch of the roofline kernel from the committed rocprofv3
-    PMC passes of the same config (scripts/pmc_round.sh + pmc_summarize.py);
-    None if there is no summary for this config and launch size."""
+def pmc_scorer(cfg, sets, label):
+    """Counters of the roofline pair from the committed rocprofv3 PMC passes
+    of the same config and launch size: HBM traffic per launch (2 x FETCH_SIZE
+    + WRITE_SIZE), vector-L1 line lookups per set and the TA busy fraction.
+    None when there is no summary for this config, launch and kernel pair."""
     try:
-        t = json.load(open(PMC_TRAFFIC))
+        t = json.load(open(PMC_SCORER))
     except (OSError, ValueError):
-        return None, None
+        return None
     if (t.get("config_id") != cfg["id"] or round(t.get("sets_per_launch", -1)) != round(sets)
             or t.get("label") != label):
-        return None, None
-    return t["traffic_bytes_per_launch"], "profiles/r4/pmc_traffic.json"
+        return None
+    return t
 
 
 ROOF_KERNELS = ["score_layer_{k}_rest", "walk_{k}_rest"]
@@ -145,10 +147,19 @@ def roofline(ctx, cfg, per_layer_sets, steps):
     bytes_per_set = 4 * (k + 1)
     achieved = sets * bytes_per_set / (p["avg_ms"] * 1e-3) / 1e9
     flops_per_set = 2 * k ** 3 / 3 + 2 * k * k + 2 * k
-    traffic, traffic_src = pmc_traffic(cfg, sets, name)
+    pmc = pmc_scorer(cfg, sets, name)
+    traffic = pmc["traffic_bytes_per_launch"] if pmc else None
     return ({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per launch",
-             "traffic_source": traffic_src, "kernel": name,
+             "traffic_source": os.path.relpath(PMC_SCORER, ROOT) if pmc else None,
+             "l1_lines_per_set": pmc.get("l1_lines_per_set") if pmc else None,
+             "ta_busy_frac": pmc.get("ta_busy_frac") if pmc else None,
+             "pmc_kernels": pmc.get("kernels") if pmc else None,
+             "pmc_note": ("what binds the pair is the vector memory pipeline, not HBM bytes: l1_lines_per_set = "
+                          "TCP_TOTAL_CACHE_ACCESSES / sets (one tag lookup per distinct 128-B line per gather "
+                          "instruction), ta_busy_frac = per-CU TA_TA_BUSY / kernel cycles of the scoring kernel "
+                          "(profiles/r5, scripts/pmc_r5_summarize.py)"),
+             "kernel": name,
              "avg_launch_ms": p["avg_ms"], "avg_launch_ms_each": [q["avg_ms"] for q in ps],
              "launches": p["count"], "launches_per_step": groups, "sets_per_launch": sets,
              "note": "launches of different stream groups overlap; each duration is its own kernel's",

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Per-dispatch counters of the scorer's roofline pair from a
+scripts/r5_probe.sh output directory: layer 6 without variable 0 at C3,
+score_layer_kernel<6, 1, 81> (grid = the layer's 2,557,324 sets rounded to
+256) plus walk_sliced_kernel<6, 1, 4> (grid = the same sets / 4 per lane).
+
+* traffic = 2 x FETCH_SIZE + WRITE_SIZE (KiB per dispatch, gfx950
+  correction of MI355X_MICROARCH.md, calibrated for gathers in
+  DESIGN.md §3) -- per launch pair;
+* l1_lines_per_set = TCP_TOTAL_CACHE_ACCESSES / sets (vector L1 tag lookups:
+  a divergent 4-byte gather costs one per distinct 128-byte line per lane);
+* ta_busy_frac = (TA_TA_BUSY_sum / 256 CUs) / (GRBM_GUI_ACTIVE / 8 XCDs):
+  the fraction of the kernel's cycles the average CU's texture-address unit
+  is busy.
+
+    python scripts/pmc_r5_summarize.py gpurun_out/r5probe > profiles/r5/pmc_scorer.json
+"""
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+
+KERNELS = {"score": ("score_layer_kernel<6, 1, 81>", 256 * ((2557324 + 255) // 256)),
+           "walk": ("walk_sliced_kernel<6, 1, 4>", 64 * ((2557324 + 255) // 256))}
+N_CU, N_XCD = 256, 8
+
+
+def per_dispatch(outdir):
+    vals = {k: {} for k in KERNELS}
+    for p in sorted(glob.glob(os.path.join(outdir, "p*", "run_counter_collection.csv"))):
+        for r in csv.DictReader(open(p)):
+            for k, (name, grid) in KERNELS.items():
+                if name in r["Kernel_Name"] and int(r["Grid_Size"]) == grid:
+                    vals[k].setdefault(r["Counter_Name"], {}).setdefault(r["Dispatch_Id"] + p, 0.0)
+                    vals[k][r["Counter_Name"]][r["Dispatch_Id"] + p] += float(r["Counter_Value"])
+    return {k: {c: sum(d.values()) / len(d) for c, d in v.items()} | {"dispatches": {c: len(d) for c, d in v.items()}}
+            for k, v in vals.items()}
+
+
+def main():
+    outdir = sys.argv[1]
+    sets = 2557324
+    pd = per_dispatch(outdir)
+    out = {"config_id": "c3", "label": "score_layer_6_rest + walk_6_rest", "sets_per_launch": sets,
+           "kernels": {k: v[0] for k, v in KERNELS.items()}, "source": outdir}
+    try:
+        out["commit"] = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True,
+                                       cwd=os.path.dirname(os.path.abspath(__file__))).stdout.strip() or None
+    except OSError:
+        out["commit"] = None
+    tr, l1 = 0.0, 0.0
+    for k in KERNELS:
+        c = pd[k]
+        e = {}
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            e["traffic_bytes"] = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+            tr += e["traffic_bytes"]
+        if "TCP_TOTAL_CACHE_ACCESSES_sum" in c:
+            e["l1_lines_per_set"] = c["TCP_TOTAL_CACHE_ACCESSES_sum"] / sets
+            l1 += e["l1_lines_per_set"]
+        if "TA_TA_BUSY_sum" in c and c.get("GRBM_GUI_ACTIVE"):
+            e["ta_busy_frac"] = (c["TA_TA_BUSY_sum"] / N_CU) / (c["GRBM_GUI_ACTIVE"] / N_XCD)
+            e["kernel_cycles_per_xcd"] = c["GRBM_GUI_ACTIVE"] / N_XCD
+        if "TCP_TCC_READ_REQ_sum" in c and c["TCP_TCC_READ_REQ_sum"]:
+            e["l1_to_l2_latency_cycles"] = c["TCP_TCC_READ_REQ_LATENCY_sum"] / c["TCP_TCC_READ_REQ_sum"]
+        e["counters_per_dispatch"] = {kk: round(vv, 1) for kk, vv in c.items() if kk != "dispatches"}
+        e["dispatches_averaged"] = c.get("dispatches", {})
+        out[k] = e
+    out["traffic_bytes_per_launch"] = tr or None
+    out["l1_lines_per_set"] = l1 or None
+    out["ta_busy_frac"] = out["score"].get("ta_busy_frac")
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
