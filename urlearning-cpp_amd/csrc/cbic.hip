@@ -197,9 +197,26 @@ __host__ __device__ inline LdsLayout lds_layout(int n, int nv, int S, int L, int
 
 
 
-// Append a set to the walk queue (wave-aggregated: one atomic per wave):
-// table slot | ts bits << 32, the hi words, then the open words
-// (open = absent & cover(T without var 0) & not checked; checked = {empty}).
+// The walk queue of a two-pass launch is cut into nseg = ceil(blocks /
+// kSegBlocks) segments, each with its own counter on its own 128-byte line:
+// one counter for the whole launch took ~23 K wave atomics in a row at C3's
+// layer 6 and cost a third of the scoring kernel (318 -> 204 us without it).
+// Block b queues into segment b mod nseg, so the blocks resident at any time
+// spread over all counters and every segment is a cross-section of the
+// launch (segments of neighbouring blocks cluster the long walks into the
+// same walk waves: the layer-6 walk launch took 2x longer).  Segment s holds
+// its queued sets at entries [s * kSegEntries, s * kSegEntries + count_s);
+// the walk kernel takes one (segment, chunk) per wave.
+constexpr int kSegBlocks = 32;
+constexpr uint64_t kSegEntries = (uint64_t)kSegBlocks * kBlock;
+constexpr int kSegStride = 16;  // counters 128 B apart
+__host__ __device__ inline uint64_t seg_count(uint64_t blocks) { return (blocks + kSegBlocks - 1) / kSegBlocks; }
+__device__ __forceinline__ uint64_t walk_segment() { return blockIdx.x % seg_count(gridDim.x); }
+
+// Append a set to the walk queue (wave-aggregated: one atomic per wave on the
+// segment's counter): table slot | ts bits << 32, the hi words, then the open
+// words (open = absent & cover(T without var 0) & not checked; checked =
+// {empty}).  queue / qcount: the segment's entries and counter.
 template <class BS>
 __device__ __forceinline__ void queue_walk(const BS &present, const BS &hi, uint64_t *queue,
                                            unsigned long long *qcount, uint64_t slot, float ts) {
@@ -363,7 +380,11 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         }
     }
 
+#ifndef ULG_PROBE_NOSCORE  // ULG_PROBE_*: timing-only builds, see the two-pass section below
     const float ts = cbic_set_score<L>(g, a.n, v, gv, a.N, a.lambda);
+#else
+    const float ts = (float)(-a.N * g[gv[0] * a.n + gv[L - 1]] - (double)(r & 1023));
+#endif
 
     if constexpr (CMP) {
         // 1. settle by the subset maxima: ts >= 0, no key >= -ts in U(P), or a
@@ -433,6 +454,11 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
             a.table[slot] = out;
             if (a.hsub_out) a.hsub[slot] = fmaxf(out, hch);
         }
+// ULG_PROBE_*: timing-only builds (wrong lists, never shipped) that drop one
+// part of the two-pass kernel (scripts/r5_kernel_ab.sh)
+#ifdef ULG_PROBE_NOCMP  // the undecided sets are left undecided
+        return;
+#endif
         // 2. the rest of the block's sets, compacted in LDS, so the presence
         //    gathers (2^(L+1) reads each) run on dense waves
         unsigned int *cnt = reinterpret_cast<unsigned int *>(smem + lay.cmp);
@@ -458,6 +484,7 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         __syncthreads();
         if (threadIdx.x >= *cnt) return;
         const int k = threadIdx.x;
+        const uint64_t seg = walk_segment();
         const int vk = evi[k] & 0xff;
 #ifdef ULG_GATHER_STATS
         const uint32_t hk = (uint32_t)evi[k] >> 8;  // hotA | hotZ << 8
@@ -476,9 +503,16 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         // the keys the two-level rules read first; the rest only for the sets
         // the rules leave to the walk (the subset maxima already showed a
         // key >= -ts is present, so the rules need no "any key" test)
+#ifndef ULG_PROBE_NOPART1
         gather_keys<L, PHASE, V, BS, LdPlain, 1>(present, hib, ls, -tk, binom, zk, a.table, toff + (uint64_t)vk * a.S);
+#endif
         bool q;
+#ifndef ULG_PROBE_NORULES
         const bool dom = settle_rules<L, PHASE, BS, true>(present, hib, ls, q);
+#else
+        const bool dom = false;
+        q = false;
+#endif
 #ifdef ULG_GATHER_STATS
         if constexpr (W < 4) {
             BS p2 = make_bits<BS>(lds_bits), h2 = make_bits<BS>(lds_bits);
@@ -489,9 +523,14 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         }
 #endif
         if (q) {
+#ifndef ULG_PROBE_NOPART2
             gather_keys<L, PHASE, V, BS, LdPlain, 2>(present, hib, ls, -tk, binom, zk, a.table,
                                                     toff + (uint64_t)vk * a.S);
-            queue_walk(present, hib, a.queue, a.qcount, sk, tk);
+#endif
+#ifndef ULG_PROBE_NOQUEUE
+            queue_walk(present, hib, a.queue + seg * kSegEntries * (uint64_t)(1 + 2 * W), a.qcount + seg * kSegStride,
+                       sk, tk);
+#endif
             if (a.hsub_out) a.hsub[sk] = ehch[k];  // the walk raises it to -ts if it stores P
         } else {
             const float o = dom ? absent_f() : -tk;
@@ -530,7 +569,11 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         if constexpr ((V & 16) != 0) {
             // decide what needs no walk; queue the rest for the walk kernel
             const bool dom = settle_rules<L, PHASE>(present, hi, ls, queued);
-            if (queued) queue_walk(present, hi, a.queue, a.qcount, toff[vbase + L] + rankP, ts);
+            if (queued) {
+                const uint64_t seg = walk_segment();
+                queue_walk(present, hi, a.queue + seg * kSegEntries * (uint64_t)(1 + 2 * W), a.qcount + seg * kSegStride,
+                           toff[vbase + L] + rankP, ts);
+            }
             out = dom ? absent_f() : -ts;
         } else {
         BS checked = make_bits<BS>(lds_bits + (size_t)W * kBlock);
@@ -649,15 +692,24 @@ __device__ __forceinline__ void walk_store(const uint64_t *queue, uint64_t qn, u
     }
 }
 
+// One wave per (queue segment, chunk of 64 * K entries), chunk-major:
+// blockIdx.x = chunk * nseg + segment, so the few chunks that hold sets come
+// first in dispatch order and the empty ones (a segment can hold up to
+// kSegEntries sets) form the tail -- interleaved, the empty workgroups' own
+// dispatch delayed the last busy waves (the layer-6 walk's span 220 -> 427 us).
 template <int L, int PHASE, int K>
 __global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, const unsigned long long *qcount,
                                                          float *table, float *hsub, uint64_t *wclock) {
     using S = Sliced<L, K>;
     const uint64_t t_start = wclock ? wall_clock64() : 0;
     constexpr int W = bits_words(L);
-    const uint64_t qn = *qcount;
-    const uint64_t first = (uint64_t)blockIdx.x * 64 * S::K;
+    constexpr uint32_t kChunks = (uint32_t)((kSegEntries + 64 * K - 1) / (64 * K));
+    const uint32_t nseg = gridDim.x / kChunks;
+    const uint32_t seg = blockIdx.x % nseg;
+    const uint64_t qn = qcount[(uint64_t)seg * kSegStride];
+    const uint64_t first = (uint64_t)(blockIdx.x / nseg) * 64 * S::K;
     if (first >= qn) return;
+    queue += (uint64_t)seg * kSegEntries * (uint64_t)(1 + 2 * W);
     const uint64_t mine = first + (uint64_t)threadIdx.x * S::K;
     typename S::Vec hiV, openV;
     uint32_t alive = walk_load<L, K>(queue, qn, mine, hiV, openV);
@@ -2506,8 +2558,20 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
             for (int ph = 0; ph < 2; ++ph) {
                 const uint64_t cnt = h_wk[(size_t)g * (G > 1 ? wstride : 0) + ((size_t)L * 2 + ph) * (nv + 1) + nv];
                 if (L > kMaxL) wqwords = std::max<uint64_t>(wqwords, 6 * cnt);  // entries + straggler copies
-                else if (variant & 16) qwords = std::max<uint64_t>(qwords, cnt * (uint64_t)(1 + 2 * bits_words(L)));
+                else if (variant & 16)
+                    qwords = std::max<uint64_t>(qwords, seg_count((cnt + kBlock - 1) / kBlock) * kSegEntries *
+                                                            (uint64_t)(1 + 2 * bits_words(L)));
             }
+    // walk-queue segment counters per (group, layer, phase) of the unrolled
+    // two-pass launches (queue_walk), kSegStride words each
+    const size_t nseg_slots = (size_t)G * 2 * (kmax + 1);
+    std::vector<uint64_t> segoff(nseg_slots + 1, 0);
+    for (size_t i = 0; i < nseg_slots; ++i) {
+        const int g = (int)(i / (2 * (size_t)(kmax + 1))), L = (int)((i / 2) % (size_t)(kmax + 1)), ph = (int)(i % 2);
+        const uint64_t cnt = h_wk[(size_t)g * (G > 1 ? wstride : 0) + ((size_t)L * 2 + ph) * (nv + 1) + nv];
+        const bool queued = L >= 1 && L <= kMaxL && (variant & 16);
+        segoff[i + 1] = segoff[i] + (queued ? seg_count((cnt + kBlock - 1) / kBlock) * kSegStride : 0);
+    }
     // queue counters per (group, layer, phase), then the wide walks' error flag
     const size_t nqc = (size_t)G * 2 * (kmax + 1) + 1;
     if ((variant & 16) || kmax > kMaxL) {
@@ -2515,6 +2579,9 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
             (rc = ensure(c, c->d_wqueue, (size_t)G * wqwords)))
             return rc;
         ULG_HIP(c, hipMemsetAsync(c->d_qcount.p, 0, sizeof(unsigned long long) * nqc, c->stream));
+        if ((rc = ensure(c, c->d_qseg, (size_t)segoff.back()))) return rc;
+        ULG_HIP(c, hipMemsetAsync(c->d_qseg.p, 0, sizeof(unsigned long long) * std::max<uint64_t>(segoff.back(), 1),
+                                  c->stream));
     }
     // wide-layer walks: one checked-bitset slice per stream group, allocated
     // before any launch (2^q bits per walking set, q <= kmax + 1)
@@ -2612,7 +2679,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                      (uint64_t)c->walk_small_sets,
                      (uint64_t)(uintptr_t)c->table.p, (uint64_t)(uintptr_t)c->d_work.p,
                      (uint64_t)(uintptr_t)c->d_workg.p, (uint64_t)(uintptr_t)c->d_queue.p,
-                     (uint64_t)(uintptr_t)c->d_qcount.p, (uint64_t)(uintptr_t)c->d_cand.p,
+                     (uint64_t)(uintptr_t)c->d_qcount.p, (uint64_t)(uintptr_t)c->d_qseg.p, (uint64_t)(uintptr_t)c->d_cand.p,
                      (uint64_t)(uintptr_t)c->d_meta.p, (uint64_t)(uintptr_t)c->d_tbl_off.p,
                      (uint64_t)(uintptr_t)c->out_sets.p, (uint64_t)(uintptr_t)c->out_scores.p,
                      (uint64_t)(uintptr_t)c->out_offsets.p, (uint64_t)(uintptr_t)c->d_blk.p,
@@ -2681,7 +2748,8 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                 if (cnt == 0) continue;
                 hipStream_t st = gst[g];
                 sa.work = d_wk + wo;
-                unsigned long long *qc = (variant & 16) ? c->d_qcount.p + (size_t)g * 2 * (kmax + 1) + (L * 2 + ph) : nullptr;
+                unsigned long long *qc =
+                    (variant & 16) ? c->d_qseg.p + segoff[(size_t)g * 2 * (kmax + 1) + (size_t)L * 2 + ph] : nullptr;
                 sa.queue = (variant & 16) ? c->d_queue.p + (size_t)g * qwords : nullptr;
                 sa.qcount = qc;
                 // nothing reads the subset maxima of the top layer's second phase
@@ -2715,8 +2783,10 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                     // the undecided lanes of this launch, densely packed
                     const int wk = sliced_k(L, cnt, (uint64_t)c->walk_small_sets);
                     if ((variant & 32) && sliced_fn(L, ph, wk)) {
-                        const uint64_t per = 64ull * (uint64_t)wk;
-                        const uint64_t sb = (cnt + per - 1) / per;
+                        // one wave per (queue segment, chunk of 64 * K entries)
+                        const int kk = L == 7 ? 2 : (L == 8 ? 1 : wk);
+                        const uint64_t per = 64ull * (uint64_t)kk;
+                        const uint64_t sb = seg_count(blocks) * ((kSegEntries + per - 1) / per);
                         if (wck && (rc = ensure(c, c->d_dump, (size_t)3 * sb))) return rc;
                         if (wck) ULG_HIP(c, hipMemsetAsync(c->d_dump.p, 0, 24 * sb, st));
                         prof_begin_s(c, kWalkNames[ph][L], st);

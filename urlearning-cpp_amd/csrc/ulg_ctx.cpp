@@ -164,7 +164,7 @@ void ulg_destroy(ulg_ctx *c) {
     c->sync_events.clear();
     release(c->raw); release(c->z); release(c->gram); release(c->partials); release(c->colstat);
     release(c->table); release(c->d_tbl_off); release(c->d_work); release(c->d_blk);
-    release(c->d_cand); release(c->d_meta); release(c->d_binom); release(c->d_binom64); release(c->d_wqueue); release(c->d_wbits); release(c->d_stats); release(c->d_dump); release(c->d_queue); release(c->d_qcount); release(c->d_workg); release(c->d_vwork); release(c->d_hq); release(c->d_hqc); release(c->d_hmax); release(c->d_hoff); release(c->d_hmeta); release(c->d_scount); release(c->d_hsub);
+    release(c->d_cand); release(c->d_meta); release(c->d_binom); release(c->d_binom64); release(c->d_wqueue); release(c->d_wbits); release(c->d_stats); release(c->d_dump); release(c->d_queue); release(c->d_qcount); release(c->d_workg); release(c->d_vwork); release(c->d_hq); release(c->d_hqc); release(c->d_hmax); release(c->d_hoff); release(c->d_hmeta); release(c->d_scount); release(c->d_hsub); release(c->d_qseg);
     release(c->out_sets); release(c->out_scores); release(c->out_offsets);
     release(c->qbuf_in); release(c->qbuf_out);
     pss_release(c);

@@ -108,6 +108,7 @@ struct ulg_ctx {
     ulg::DevBuf<unsigned long long> d_stats;  // score_variant 13 statistics
     ulg::DevBuf<uint64_t> d_dump;
     ulg::DevBuf<uint64_t> d_queue;                // score_variant bit 4: undecided lanes
+    ulg::DevBuf<unsigned long long> d_qseg;       // ... their per-segment counters (cbic.hip kSegBlocks)
     ulg::DevBuf<unsigned long long> d_qcount;
     ulg::DevBuf<uint64_t> d_workg;                // per stream-group work prefixes
     ulg::DevBuf<uint64_t> d_vwork;                // per-variable work prefixes of the wide-layer pool
