@@ -501,6 +501,11 @@ def main():
         # step with 1 slot x 3 groups, 0.67 ms with 3 slots x 1 stream;
         # profiles/r3/slots/)
         args.option.append("score_streams=1")
+    if args.slots > 1 and not any(o.startswith("walk_k6=") for o in args.option):
+        # throughput with steps in flight: 8 sets per lane share one walk of
+        # the layer-6 union tree (10.17e9 against 9.80e9 sets/s with 4; the
+        # single-call context below keeps the library default, 4)
+        args.option.append("walk_k6=8")
 
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
         sys.exit(spawn_ranks(args.gpus))

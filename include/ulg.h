@@ -304,6 +304,11 @@ int ulg_sweep_shard_end(ulg_ctx *ctx, uint64_t *vpar, int *order, float *goal_co
  * "walk_small_sets" (>= 0, default 200000): a layer-6 launch of fewer sets
  * walks one set per lane instead of four (the small launches of 4- and
  * 8-rank shares end with their longest walk wave).
+ * "walk_k6" (1, 2, 4 or 8; default 4): sets per lane of the other layer-6
+ * walk launches: more sets share one walk of their union tree (less work per
+ * set, longer waves).  4 gives the shortest single call; with several calls
+ * in flight on one GPU (bench.py's slots) 8 gives the most sets per second
+ * (C3: 10.17e9 against 9.80e9, single call 0.91 against 0.89 ms).
  * "table_budget_kb" (KiB; default 0 = half the free HBM): memory for the dense
  * best-score tables (16 B per entry incl. the host cost copy).  Lists whose
  * tables over all variables exceed it (e.g. n = 32 with a full skeleton) are

@@ -22,21 +22,35 @@ import os
 import subprocess
 import sys
 
-KERNELS = {"score": ("score_layer_kernel<6, 1, 81>", 256 * ((2557324 + 255) // 256)),
-           "walk": ("walk_sliced_kernel<6, 1, 4>", 64 * ((2557324 + 255) // 256))}
+# (kernel name prefix; the dispatches averaged are those with the largest
+# grid, i.e. the full-layer launches of one stream per context)
+KERNELS = {"score": "score_layer_kernel<6, 1, 81>", "walk": "walk_sliced_kernel<6, 1, "}
 N_CU, N_XCD = 256, 8
 
 
 def per_dispatch(outdir):
     vals = {k: {} for k in KERNELS}
-    for p in sorted(glob.glob(os.path.join(outdir, "p*", "run_counter_collection.csv"))):
+    files = sorted(glob.glob(os.path.join(outdir, "p*", "run_counter_collection.csv")))
+    grid = {k: 0 for k in KERNELS}
+    names = {k: None for k in KERNELS}
+    for p in files:
         for r in csv.DictReader(open(p)):
-            for k, (name, grid) in KERNELS.items():
-                if name in r["Kernel_Name"] and int(r["Grid_Size"]) == grid:
+            for k, name in KERNELS.items():
+                if name in r["Kernel_Name"] and int(r["Grid_Size"]) > grid[k]:
+                    grid[k] = int(r["Grid_Size"])
+                    names[k] = r["Kernel_Name"].split("(")[1].rstrip(")") if False else r["Kernel_Name"][
+                        r["Kernel_Name"].find("::") + 2:r["Kernel_Name"].find(">(") + 1]
+    for p in files:
+        for r in csv.DictReader(open(p)):
+            for k, name in KERNELS.items():
+                if name in r["Kernel_Name"] and int(r["Grid_Size"]) == grid[k]:
                     vals[k].setdefault(r["Counter_Name"], {}).setdefault(r["Dispatch_Id"] + p, 0.0)
                     vals[k][r["Counter_Name"]][r["Dispatch_Id"] + p] += float(r["Counter_Value"])
-    return {k: {c: sum(d.values()) / len(d) for c, d in v.items()} | {"dispatches": {c: len(d) for c, d in v.items()}}
-            for k, v in vals.items()}
+    out = {k: {c: sum(d.values()) / len(d) for c, d in v.items()} | {"dispatches": {c: len(d) for c, d in v.items()}}
+           for k, v in vals.items()}
+    for k in KERNELS:
+        out[k]["kernel"], out[k]["grid"] = names[k], grid[k]
+    return out
 
 
 def main():
@@ -44,7 +58,8 @@ def main():
     sets = 2557324
     pd = per_dispatch(outdir)
     out = {"config_id": "c3", "label": "score_layer_6_rest + walk_6_rest", "sets_per_launch": sets,
-           "kernels": {k: v[0] for k, v in KERNELS.items()}, "source": outdir}
+           "kernels": {k: pd[k]["kernel"] for k in KERNELS}, "grids": {k: pd[k]["grid"] for k in KERNELS},
+           "source": outdir}
     try:
         out["commit"] = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True,
                                        cwd=os.path.dirname(os.path.abspath(__file__))).stdout.strip() or None
@@ -65,7 +80,8 @@ def main():
             e["kernel_cycles_per_xcd"] = c["GRBM_GUI_ACTIVE"] / N_XCD
         if "TCP_TCC_READ_REQ_sum" in c and c["TCP_TCC_READ_REQ_sum"]:
             e["l1_to_l2_latency_cycles"] = c["TCP_TCC_READ_REQ_LATENCY_sum"] / c["TCP_TCC_READ_REQ_sum"]
-        e["counters_per_dispatch"] = {kk: round(vv, 1) for kk, vv in c.items() if kk != "dispatches"}
+        e["counters_per_dispatch"] = {kk: round(vv, 1) for kk, vv in c.items()
+                                      if kk not in ("dispatches", "kernel", "grid")}
         e["dispatches_averaged"] = c.get("dispatches", {})
         out[k] = e
     out["traffic_bytes_per_launch"] = tr or None

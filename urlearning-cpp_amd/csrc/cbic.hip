@@ -1814,11 +1814,11 @@ constexpr int kSlicedK6 = 4;      // ... at layer 6
 // its few waves then each walk a quarter of the union tree, and the launch
 // ends with its longest wave (C3 8-rank share 0.80 -> 0.73 ms; the one-GPU
 // launches keep the wide union, best there, `profiles/r4/`).
-int sliced_k(int L, uint64_t cnt = ~0ull, uint64_t small = 0) {
+int sliced_k(int L, uint64_t cnt = ~0ull, uint64_t small = 0, int k6 = kSlicedK6) {
     if (L >= 7) return L == 7 ? 2 : 1;
     // ULG_SLICED_K=a (every layer) or a,b (layers <= 5, layer 6): A/B only
     const char *e = std::getenv("ULG_SLICED_K");
-    int k = L <= 5 ? kSlicedKSmall : (cnt < small ? 1 : kSlicedK6);
+    int k = L <= 5 ? kSlicedKSmall : (cnt < small ? 1 : k6);
     if (e) {
         const char *comma = std::strchr(e, ',');
         k = (L <= 5 || !comma) ? std::atoi(e) : std::atoi(comma + 1);
@@ -2676,7 +2676,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     if (use_graph) {
         gkey.assign({(uint64_t)nv, (uint64_t)max_parents, (uint64_t)variant, (uint64_t)G, (uint64_t)Ls,
                      (uint64_t)c->score_xcd, (uint64_t)n, (uint64_t)c->N, dbits(c->lambda), (uint64_t)c->prof,
-                     (uint64_t)c->walk_small_sets,
+                     (uint64_t)c->walk_small_sets, (uint64_t)c->walk_k6,
                      (uint64_t)(uintptr_t)c->table.p, (uint64_t)(uintptr_t)c->d_work.p,
                      (uint64_t)(uintptr_t)c->d_workg.p, (uint64_t)(uintptr_t)c->d_queue.p,
                      (uint64_t)(uintptr_t)c->d_qcount.p, (uint64_t)(uintptr_t)c->d_qseg.p, (uint64_t)(uintptr_t)c->d_cand.p,
@@ -2781,7 +2781,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                 prof_end_s(c, st);
                 if (variant & 16) {
                     // the undecided lanes of this launch, densely packed
-                    const int wk = sliced_k(L, cnt, (uint64_t)c->walk_small_sets);
+                    const int wk = sliced_k(L, cnt, (uint64_t)c->walk_small_sets, c->walk_k6);
                     if ((variant & 32) && sliced_fn(L, ph, wk)) {
                         // one wave per (queue segment, chunk of 64 * K entries)
                         const int kk = L == 7 ? 2 : (L == 8 ? 1 : wk);

@@ -213,6 +213,12 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         c->sweep_xcd = (int)value;
         return ULG_OK;
     }
+    if (std::strcmp(name, "walk_k6") == 0) {
+        if (value != 1 && value != 2 && value != 4 && value != 8)
+            return set_err(c, ULG_ERR_ARG, "walk_k6 must be 1, 2, 4 or 8");
+        c->walk_k6 = (int)value;
+        return ULG_OK;
+    }
     if (std::strcmp(name, "walk_small_sets") == 0) {
         if (value < 0) return set_err(c, ULG_ERR_ARG, "walk_small_sets must be >= 0");
         c->walk_small_sets = value;

@@ -148,6 +148,7 @@ struct ulg_ctx {
     std::map<std::string, std::vector<double>> prof_ms;
 
     int64_t walk_small_sets = 200000;  // layer-6 launches below this many sets walk one set per lane
+    int walk_k6 = 4;                   // sets per lane of the layer-6 walk launches (1, 2, 4 or 8)
 };
 
 namespace ulg {
