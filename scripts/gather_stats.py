@@ -41,7 +41,7 @@ def main():
             X, _ = synth.gaussian_sem(n, N, 9200)
             ctx.load(X, 2.0)
             variables, cands = cands_for(n, kind, n)
-            buf = np.zeros(2 * 9 * 16, dtype=np.uint64)
+            buf = np.zeros(2 * 2 * 9 * 16, dtype=np.uint64)
             L_.ulg_diag_gather_stats(ctx._h, buf.ctypes.data)  # zero
             st, scored = ctx.score(variables, cands, k)
             L_.ulg_diag_gather_stats(ctx._h, buf.ctypes.data)
@@ -55,6 +55,14 @@ def main():
                     out["layers"][f"L{L}p{ph}"] = dict({"sets": int(c[0])},
                                                         **{nm: round(float(v) / s, 3) for nm, v in
                                                            zip(NAMES[1:], c[1:])})
+            wb = buf[2 * 9 * 16:]
+            for L in range(1, 9):
+                for ph in range(2):
+                    w = wb[(L * 2 + ph) * 16:(L * 2 + ph) * 16 + 16]
+                    if w.sum() == 0:
+                        continue
+                    out["layers"].setdefault(f"L{L}p{ph}", {})["walk_hits_by_depth"] = [int(x) for x in w[:L]]
+                    out["layers"][f"L{L}p{ph}"]["walk_stored"] = int(w[15])
             print(json.dumps(out), flush=True)
     ctx.close()
 

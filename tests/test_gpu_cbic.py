@@ -266,6 +266,30 @@ def test_walk_forms_identical_c3(ulg_ctx, monkeypatch):
             assert a.tobytes() == b.tobytes(), k
 
 
+def test_walk_k6_option_identical_c3_and_segments(ulg_ctx):
+    """ulg_set_option("walk_k6"): 1, 2 and 8 sets per lane in the layer-6
+    walks store the default's (4) lists bit for bit at C3, with one stream
+    group (one walk-queue segment set per launch) and three (every group's
+    segment counters at their own offsets)."""
+    n = 25
+    X, _ = synth.gaussian_sem(n, 10000, 9200)
+    ulg_ctx.load(X, 2.0)
+    full = [(1 << n) - 1] * n
+    try:
+        for streams in (1, 3):
+            ulg_ctx.set_option("score_streams", streams)
+            ulg_ctx.set_option("walk_k6", 4)
+            ref = ulg_ctx.score_all(list(range(n)), full, 6)
+            for k6 in (1, 2, 8):
+                ulg_ctx.set_option("walk_k6", k6)
+                got = ulg_ctx.score_all(list(range(n)), full, 6)
+                for a, b in zip(ref, got):
+                    assert np.asarray(a).tobytes() == np.asarray(b).tobytes(), (streams, k6)
+    finally:
+        ulg_ctx.set_option("walk_k6", 4)
+        ulg_ctx.set_option("score_streams", 3)
+
+
 def test_score_graph_replay_identical_and_profiled(ulg_ctx):
     """ulg_set_option("score_graph"): the scoring launch sequence is captured
     into a hipGraph on the first call and replayed on the next ones with the

@@ -493,6 +493,70 @@ __device__ __forceinline__ void child_ranks(uint64_t cm, const uint32_t *binom, 
     }
 }
 
+// May find_best_subset_score's walk of P reach a key >= -ts?  A superset of
+// every node the walk tests: below the root any first removal (a child call
+// keeps the entries after the removed one), from the second removal on only
+// entries before the last removed one in the list order (one level down the
+// call keeps just the entries before it), and variable 0 toggled at any node
+// below the root (padding zeros; in phase 0 variable 0 is also the first list
+// entry).  Only absent nodes are expanded; `checked` and the hi-cover prune
+// only remove tests.  If no key >= -ts lies in that superset, the walk stores
+// P -- the two-pass scorer then stores it without queueing a walk
+// (scripts/walk_closure_check.py checks the superset against the recursion).
+// Bit t of word t >> 6 is local subset t; root = P (and, phase 1, P + {0})
+// are never keys.
+template <int L, int PHASE, int W>
+__device__ __forceinline__ bool walk_may_hit(const uint64_t (&pres)[W], const uint64_t (&hiw)[W]) {
+    constexpr int Q = PHASE == 0 ? L : L + 1;
+    constexpr uint32_t root = PHASE == 0 ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
+    constexpr uint64_t kM[6] = {0xAAAAAAAAAAAAAAAAull, 0xCCCCCCCCCCCCCCCCull, 0xF0F0F0F0F0F0F0F0ull,
+                                0xFF00FF00FF00FF00ull, 0xFFFF0000FFFF0000ull, 0xFFFFFFFF00000000ull};
+    auto bitw = [](uint32_t t, int j) constexpr -> uint64_t { return (int)(t >> 6) == j ? 1ull << (t & 63) : 0ull; };
+    uint64_t absent[W], tested[W], reach[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+        const uint64_t valid = Q >= 6 ? (j < (1 << (Q - 6)) ? ~0ull : 0ull) : (j == 0 ? (1ull << (1 << Q)) - 1ull : 0ull);
+        uint64_t first = 0;  // the root's children: every element removed once
+#pragma unroll
+        for (int b = (PHASE == 0 ? 0 : 1); b <= (PHASE == 0 ? L - 1 : L); ++b) first |= bitw(root ^ (1u << b), j);
+        const uint64_t notkey = bitw(root, j) | (PHASE == 1 ? bitw(root | 1u, j) : 0ull);
+        absent[j] = ~pres[j] & valid & ~notkey;
+        tested[j] = first;
+        reach[j] = first & absent[j];
+    }
+    auto closure = [&]() {  // variable 0 toggled at every reached node
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            const uint64_t c = ((reach[j] & 0x5555555555555555ull) << 1) | ((reach[j] & 0xAAAAAAAAAAAAAAAAull) >> 1);
+            tested[j] |= c;
+            reach[j] |= c & absent[j];
+        }
+    };
+    closure();
+#pragma unroll
+    for (int e = (PHASE == 0 ? L - 1 : L); e >= 1; --e) {
+        uint64_t n[W];
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            if (e < 6) n[j] = (reach[j] & kM[e < 6 ? e : 0]) >> (1 << (e < 6 ? e : 0));
+            else n[j] = (j + (1 << (e - 6)) < W && ((j >> (e - 6)) & 1) == 0) ? reach[j + (1 << (e - 6))] : 0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            tested[j] |= n[j];
+            reach[j] |= n[j] & absent[j];
+        }
+        closure();
+    }
+    bool hit = false;
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+        const uint64_t notkey = bitw(root, j) | (PHASE == 1 ? bitw(root | 1u, j) : 0ull);
+        hit |= (tested[j] & ~notkey & hiw[j]) != 0ull;
+    }
+    return hit;
+}
+
 // ---- bit-sliced walk (score_variant bit 5) ----------------------------------
 // The walk's tree (T, pv, idx, i) never depends on the data: only which
 // subtrees a set enters does.  So one wave walks the union tree ONCE for 64*K
@@ -554,7 +618,12 @@ __device__ __forceinline__ void sl_clear(OpenLds<L, K> &v, uint32_t t, uint32_t 
 // from j on, whose child T2 ^ {0} call 1 tested at its position 1 -- so call 1
 // walks positions 0..1 and call j >= 2 position j-1 only (the reference's
 // remaining re-tests are no-ops; the same tests in the same order).
-template <int L, int K, int M, bool DIAG = false, class OV = typename Sliced<L, K>::Vec>
+#ifdef ULG_GATHER_STATS
+// diagnostic build: per (layer, phase) the walk's hits by recursion depth
+// (slot L - M), then [15] the sets the walk stores (scripts/gather_stats.py)
+__device__ unsigned long long g_wstats[2 * (kMaxL + 1) * 16];
+#endif
+template <int L, int K, int M, bool DIAG = false, class OV = typename Sliced<L, K>::Vec, int PH = 0>
 __device__ __forceinline__ void walk_sliced(uint32_t T, uint32_t pv, uint32_t act, const typename Sliced<L, K>::Vec &hiV,
                                             OV &openV, uint32_t &alive, uint32_t &dom, uint32_t &pts, int idx_lo = 0,
                                             int idx_hi = M) {
@@ -568,6 +637,9 @@ __device__ __forceinline__ void walk_sliced(uint32_t T, uint32_t pv, uint32_t ac
         // a hit ends that set's walk (the reference returns up the recursion)
         const uint32_t h = sl_get<L, K>(hiV, T2) & act;
         dom |= h;
+#ifdef ULG_GATHER_STATS
+        if (h) atomicAdd(&g_wstats[(L * 2 + PH) * 16 + (L - M)], (unsigned long long)__builtin_popcount(h));
+#endif
         alive &= ~h;
         act &= ~h;
         if constexpr (M > 1) {
@@ -583,8 +655,8 @@ __device__ __forceinline__ void walk_sliced(uint32_t T, uint32_t pv, uint32_t ac
                 ++j;
                 // one call site per level: two would inline the level below
                 // twice, 2^(L-1) copies of the deepest one (a ~40 KB kernel)
-                walk_sliced<L, K, M - 1, DIAG, OV>(T2, npv, x, hiV, openV, alive, dom, pts, j == 1 ? 0 : j - 1,
-                                                   j == 1 ? (M - 1 < 2 ? M - 1 : 2) : j);
+                walk_sliced<L, K, M - 1, DIAG, OV, PH>(T2, npv, x, hiV, openV, alive, dom, pts, j == 1 ? 0 : j - 1,
+                                                       j == 1 ? (M - 1 < 2 ? M - 1 : 2) : j);
                 sl_clear<L, K>(openV, T2, x);  // checked.insert(T2) for the sets that ran the call
                 x &= alive;
                 if (!wave_any(x)) break;
