@@ -290,6 +290,33 @@ def test_walk_k6_option_identical_c3_and_segments(ulg_ctx):
         ulg_ctx.set_option("score_streams", 3)
 
 
+def test_score_fused_small_layers_identical(ulg_ctx):
+    """ulg_set_option("score_fused"): layers up to 1..4 in one launch (a
+    workgroup per variable, its layers and phases in order) store the
+    per-layer launches' lists bit for bit: C3 (k = 6, the layers above the
+    fused ones read its subset maxima), a call whose top layer is fused
+    (k = 3: no layer reads layer 3's phase-1 maxima), a sparse candidate
+    set, and variables without variable 0 among their candidates."""
+    rng = np.random.default_rng(31)
+    n = 25
+    X, _ = synth.gaussian_sem(n, 10000, 9200)
+    ulg_ctx.load(X, 2.0)
+    full = [(1 << n) - 1] * n
+    sparse = [int(rng.integers(1, 1 << n)) | (1 << int(rng.integers(0, n))) for _ in range(n)]
+    no0 = [((1 << n) - 1) & ~1] * n
+    try:
+        for cands, k in ((full, 6), (full, 3), (sparse, 6), (no0, 5)):
+            ulg_ctx.set_option("score_fused", 0)
+            ref = ulg_ctx.score_all(list(range(n)), cands, k)
+            for f in (1, 2, 3, 4):
+                ulg_ctx.set_option("score_fused", f)
+                got = ulg_ctx.score_all(list(range(n)), cands, k)
+                for a, b in zip(ref, got):
+                    assert np.asarray(a).tobytes() == np.asarray(b).tobytes(), (k, f)
+    finally:
+        ulg_ctx.set_option("score_fused", 3)
+
+
 def test_score_graph_replay_identical_and_profiled(ulg_ctx):
     """ulg_set_option("score_graph"): the scoring launch sequence is captured
     into a hipGraph on the first call and replayed on the next ones with the

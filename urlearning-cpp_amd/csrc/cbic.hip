@@ -317,6 +317,154 @@ __device__ void gather_stats(const BS &present, const BS &hi, uint32_t hotA, uin
 }
 #endif
 
+// Set r of variable vi's (layer L, phase) launch: its compact mask over the
+// candidate list, colex rank, and parent variables in ascending order (==
+// BIC_OLS parent_vec order).  smeta / scand / binom: the LDS copies.
+template <int L>
+struct SetHead {
+    int v;
+    bool z;
+    uint64_t cm, rankP;
+    int gv[L];
+};
+template <int L, int PHASE>
+__device__ __forceinline__ SetHead<L> set_head(const int *smeta, const uint8_t *scand, const uint32_t *binom, int vi,
+                                               uint64_t r) {
+    SetHead<L> h;
+    h.v = smeta[vi * 4 + 0];
+    const int m = smeta[vi * 4 + 1];
+    h.z = smeta[vi * 4 + 2] != 0;
+    if (PHASE == 0) h.cm = (unrank_colex(r, L - 1, m - 1, binom) << 1) | 1ull;
+    else if (h.z) h.cm = unrank_colex(r, L, m - 1, binom) << 1;
+    else h.cm = unrank_colex(r, L, m, binom);
+    h.rankP = rank_colex(h.cm, binom);
+    const uint8_t *cl = scand + vi * 64;
+    uint64_t rem = h.cm;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        const int b = __builtin_ctzll(rem);
+        rem &= rem - 1;
+        h.gv[i] = cl[b];
+    }
+    return h;
+}
+
+// The one-pass form of one set (variant bit 4 clear): presence gathers, the
+// walk in registers (or LDS bitsets from 4 words), the store rule, and under
+// bit 6 the subset maxima.  Shared by score_layer_kernel and the fused small
+// layers (score_small_kernel).
+template <int L, int PHASE, int V>
+__device__ __forceinline__ void one_pass_set(const ScoreArgs &a, unsigned char *smem, const LdsLayout &lay,
+                                             const uint32_t *binom, const uint64_t *toff, int vi, bool z, uint64_t cm,
+                                             uint64_t rankP, float ts) {
+    constexpr bool HM = (V & 64) != 0;
+    // the children's subset maxima (bit 6), loaded before the gathers so both
+    // share one memory round trip
+    float hch = absent_f();
+    if constexpr (HM && L > 1) {
+        const uint64_t vbase = (uint64_t)vi * a.S;
+        uint64_t rc[L], rz[L];
+        child_ranks<L, false>(cm, binom, rc, rz);
+        float ch[L];
+#pragma unroll
+        for (int i = 0; i < L; ++i) ch[i] = a.hsub[toff[vbase + L - 1] + rc[i]];
+#pragma unroll
+        for (int i = 0; i < L; ++i) hch = fmaxf(hch, ch[i]);
+    }
+    // small layers (one bitset word, unrolled gathers): the gathered values
+    // stay in registers, so the walk's best needs no second round trip
+    constexpr int QV = PHASE == 0 ? L : L + 1;
+    constexpr bool KEEPV = bits_words(L) == 1 && (V & 1) && !(V & 16) && QV <= 5;
+    float out;
+    bool queued = false;  // variant bit 4: left for the walk launch
+    if (ts >= 0.0f) {
+        // returned -ts; the caller stores it iff it is < 0 (score_calculator.cpp:111)
+        const float s = -ts;
+        out = (s < 0.0f) ? s : absent_f();
+    } else {
+        constexpr int W = bits_words(L);
+        using BS = std::conditional_t<(W >= 4), BitsLds<W>, Bits<W>>;
+        uint64_t *lds_bits = reinterpret_cast<uint64_t *>(smem + lay.bits) + threadIdx.x;
+        const LocalSet<L> ls = local_set<L>(cm, z);
+        const uint64_t cpack = ls.cpack;
+        const uint32_t Plocal = ls.Plocal;
+        const uint32_t pvtop = ls.pvtop;
+        const uint64_t vbase = (uint64_t)vi * a.S;
+
+        // presence of every candidate key in the cache as it stands now
+        // the first LDS bitset is `present`; `hi` and `checked` share the
+        // second (only the decision-only walk uses `hi`); `visited` the third
+        BS present = make_bits<BS>(lds_bits);
+        BS hi = make_bits<BS>(lds_bits + (size_t)W * kBlock);
+        present.clear();
+        if constexpr ((V & 16) != 0) hi.clear();
+        const float thr = -ts;
+        float vals[KEEPV ? (1 << QV) : 1];
+        if constexpr (KEEPV) {
+#pragma unroll
+            for (int t = 0; t < (1 << QV); ++t) vals[t] = 0.0f;
+            presence_unrolled<L, PHASE, QV, W, LdPlain, 8, (V != 1), 0>(present, hi, thr, binom, ls.cpack, z, a.table,
+                                                                        toff + vbase, vals);
+        } else {
+            gather_keys<L, PHASE, V>(present, hi, ls, thr, binom, z, a.table, toff + vbase);
+        }
+
+        if constexpr ((V & 16) != 0) {
+            // decide what needs no walk; queue the rest for the walk kernel
+            const bool dom = settle_rules<L, PHASE>(present, hi, ls, queued);
+            if (queued) {
+                const uint64_t seg = walk_segment();
+                constexpr int QW = bits_words(L);
+                queue_walk(present, hi, a.queue + seg * kSegEntries * (uint64_t)(1 + 2 * QW),
+                           a.qcount + seg * kSegStride, toff[vbase + L] + rankP, ts);
+            }
+            out = dom ? absent_f() : -ts;
+        } else {
+        BS checked = make_bits<BS>(lds_bits + (size_t)W * kBlock);
+        BS visited = make_bits<BS>(lds_bits + (size_t)2 * W * kBlock);
+        checked.clear();
+        visited.clear();
+        checked.set(0u);  // checked.insert(empty_set)
+        best_subset<L, BS>(Plocal, pvtop, present, checked, visited);
+
+        float best = 0.0f;
+        if constexpr (KEEPV) {
+            // every visited node is a present key, gathered above
+            const uint64_t x = visited.word(0);
+#pragma unroll
+            for (int t = 0; t < (1 << QV); ++t)
+                if (((x >> t) & 1ull) && vals[t] > best) best = vals[t];
+        } else {
+#pragma unroll
+        for (int wj = 0; wj < W; ++wj) {
+            uint64_t x = visited.word(wj);
+            while (x) {
+                const uint32_t t = (uint32_t)(wj * 64 + __builtin_ctzll(x));
+                x &= x - 1;
+                uint64_t rk = 0;
+                uint32_t rem = t;
+                int j = 0;
+                while (rem) {
+                    const int lb = __builtin_ctz(rem);
+                    rem &= rem - 1;
+                    ++j;
+                    rk += B(binom, (int)((cpack >> (6 * lb)) & 63ull), j);
+                }
+                const float val = a.table[toff[vbase + __builtin_popcount(t)] + rk];
+                if (val > best) best = val;
+            }
+        }
+        }
+        // BIC_OLS.cpp:234: best_subset_score + bic_threshold >= -the_score
+        out = ((double)best + 0.0 >= (double)(-ts)) ? absent_f() : -ts;
+        }
+    }
+    if (!queued) a.table[toff[(uint64_t)vi * a.S + L] + rankP] = out;
+    // the one-pass form keeps the subset maxima for the layers above it
+    if constexpr (HM)
+        if (a.hsub_out) a.hsub[toff[(uint64_t)vi * a.S + L] + rankP] = fmaxf(out, hch);
+}
+
 // PHASE 0: sets containing variable 0; 1: the rest.  V = variant bits (see
 // ulg_set_option "score_variant"), compile-time so each form gets its own
 // register allocation.
@@ -356,34 +504,15 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         if (work[mid] <= gid) lo = mid; else hi = mid;
     }
     const int vi = lo;
-    const int v = smeta[vi * 4 + 0];
-    const int m = smeta[vi * 4 + 1];
-    const bool z = smeta[vi * 4 + 2] != 0;
     const uint64_t r = gid - work[vi];
-
-    uint64_t cm;  // compact mask of P over the variable's candidate list
-    if (PHASE == 0) cm = (unrank_colex(r, L - 1, m - 1, binom) << 1) | 1ull;
-    else if (z) cm = unrank_colex(r, L, m - 1, binom) << 1;
-    else cm = unrank_colex(r, L, m, binom);
-    const uint64_t rankP = rank_colex(cm, binom);
-
-    // parent variables in ascending order (== BIC_OLS parent_vec order)
-    const uint8_t *cl = scand + vi * 64;
-    int gv[L];
-    {
-        uint64_t rem = cm;
-#pragma unroll
-        for (int i = 0; i < L; ++i) {
-            const int b = __builtin_ctzll(rem);
-            rem &= rem - 1;
-            gv[i] = cl[b];
-        }
-    }
+    const SetHead<L> hd = set_head<L, PHASE>(smeta, scand, binom, vi, r);
+    const bool z = hd.z;
+    const uint64_t cm = hd.cm, rankP = hd.rankP;
 
 #ifndef ULG_PROBE_NOSCORE  // ULG_PROBE_*: timing-only builds, see the two-pass section below
-    const float ts = cbic_set_score<L>(g, a.n, v, gv, a.N, a.lambda);
+    const float ts = cbic_set_score<L>(g, a.n, hd.v, hd.gv, a.N, a.lambda);
 #else
-    const float ts = (float)(-a.N * g[gv[0] * a.n + gv[L - 1]] - (double)(r & 1023));
+    const float ts = (float)(-a.N * g[hd.gv[0] * a.n + hd.gv[L - 1]] - (double)(r & 1023));
 #endif
 
     if constexpr (CMP) {
@@ -557,86 +686,55 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         return;
     }
 
-    float out;
-    bool queued = false;  // variant bit 4: left for the walk launch
-    if (ts >= 0.0f) {
-        // returned -ts; the caller stores it iff it is < 0 (score_calculator.cpp:111)
-        const float s = -ts;
-        out = (s < 0.0f) ? s : absent_f();
-    } else {
-        constexpr int W = bits_words(L);
-        using BS = std::conditional_t<(W >= 4), BitsLds<W>, Bits<W>>;
-        uint64_t *lds_bits = reinterpret_cast<uint64_t *>(smem + lay.bits) + threadIdx.x;
-        const LocalSet<L> ls = local_set<L>(cm, z);
-        const uint64_t cpack = ls.cpack;
-        const uint32_t Plocal = ls.Plocal;
-        const uint32_t pvtop = ls.pvtop;
-        const uint64_t vbase = (uint64_t)vi * a.S;
+    one_pass_set<L, PHASE, V>(a, smem, lay, binom, toff, vi, z, cm, rankP, ts);
+}
 
-        // presence of every candidate key in the cache as it stands now
-        // the first LDS bitset is `present`; `hi` and `checked` share the
-        // second (only the decision-only walk uses `hi`); `visited` the third
-        BS present = make_bits<BS>(lds_bits);
-        BS hi = make_bits<BS>(lds_bits + (size_t)W * kBlock);
-        present.clear();
-        if constexpr ((V & 16) != 0) hi.clear();
-        const float thr = -ts;
-        gather_keys<L, PHASE, V>(present, hi, ls, thr, binom, z, a.table, toff + vbase);
-
-        if constexpr ((V & 16) != 0) {
-            // decide what needs no walk; queue the rest for the walk kernel
-            const bool dom = settle_rules<L, PHASE>(present, hi, ls, queued);
-            if (queued) {
-                const uint64_t seg = walk_segment();
-                queue_walk(present, hi, a.queue + seg * kSegEntries * (uint64_t)(1 + 2 * W), a.qcount + seg * kSegStride,
-                           toff[vbase + L] + rankP, ts);
-            }
-            out = dom ? absent_f() : -ts;
-        } else {
-        BS checked = make_bits<BS>(lds_bits + (size_t)W * kBlock);
-        BS visited = make_bits<BS>(lds_bits + (size_t)2 * W * kBlock);
-        checked.clear();
-        visited.clear();
-        checked.set(0u);  // checked.insert(empty_set)
-        best_subset<L, BS>(Plocal, pvtop, present, checked, visited);
-
-        float best = 0.0f;
-#pragma unroll
-        for (int wj = 0; wj < W; ++wj) {
-            uint64_t x = visited.word(wj);
-            while (x) {
-                const uint32_t t = (uint32_t)(wj * 64 + __builtin_ctzll(x));
-                x &= x - 1;
-                uint64_t rk = 0;
-                uint32_t rem = t;
-                int j = 0;
-                while (rem) {
-                    const int lb = __builtin_ctz(rem);
-                    rem &= rem - 1;
-                    ++j;
-                    rk += B(binom, (int)((cpack >> (6 * lb)) & 63ull), j);
-                }
-                const float val = a.table[toff[vbase + __builtin_popcount(t)] + rk];
-                if (val > best) best = val;
-            }
-        }
-        // BIC_OLS.cpp:234: best_subset_score + bic_threshold >= -the_score
-        out = ((double)best + 0.0 >= (double)(-ts)) ? absent_f() : -ts;
-        }
+// Layers 1..LF of every variable in ONE launch (option score_fused; the
+// small layers' one-pass form, V = variant & 65).  Workgroup b takes variable
+// b and runs (L, phase) in order, its kFusedThreads lanes taking the phase's
+// sets kFusedThreads at a time, with a barrier between phases: a phase reads
+// only its own variable's lower layers and, in phase 1, the same layer's
+// var-0 sets, all written by this workgroup before the barrier
+// (its waves share one CU, so the workgroup-scope fences of __syncthreads
+// order the stores before the loads).  Replaces 2 LF dependent launches of
+// a few waves each (layers 1-4 at C3: ~117 us whatever the variable count).
+constexpr int kFusedThreads = 1024;
+template <int L, int PHASE, int LF, int V>
+__device__ __forceinline__ void fused_phase(const ScoreArgs &a, const uint64_t *work_all, unsigned char *smem,
+                                            const LdsLayout &lay, const double *g, const uint32_t *binom,
+                                            const uint64_t *toff, const int *smeta, const uint8_t *scand, int vi) {
+    const uint64_t *w = work_all + ((uint64_t)L * 2 + PHASE) * (uint64_t)(a.nv + 1);
+    const uint64_t cnt = w[vi + 1] - w[vi];
+    ScoreArgs as = a;
+    as.hsub_out = a.hsub_out || !(L == LF && PHASE == 1);
+    for (uint64_t r = threadIdx.x; r < cnt; r += kFusedThreads) {
+        const SetHead<L> hd = set_head<L, PHASE>(smeta, scand, binom, vi, r);
+        const float ts = cbic_set_score<L>(g, a.n, hd.v, hd.gv, a.N, a.lambda);
+        one_pass_set<L, PHASE, V>(as, smem, lay, binom, toff, vi, hd.z, hd.cm, hd.rankP, ts);
     }
-    if (!queued) a.table[toff[(uint64_t)vi * a.S + L] + rankP] = out;
-    if constexpr (HM && !CMP) {
-        // the one-pass form keeps the subset maxima for the layers above it
-        const uint64_t vbase = (uint64_t)vi * a.S;
-        uint64_t rc[L], rz[L];
-        child_ranks<L, false>(cm, binom, rc, rz);
-        float hch = absent_f();
-        if constexpr (L > 1) {
-#pragma unroll
-            for (int i = 0; i < L; ++i) hch = fmaxf(hch, a.hsub[toff[vbase + L - 1] + rc[i]]);
-        }
-        if (a.hsub_out) a.hsub[toff[vbase + L] + rankP] = fmaxf(out, hch);
-    }
+    __syncthreads();
+    if constexpr (PHASE == 0) fused_phase<L, 1, LF, V>(a, work_all, smem, lay, g, binom, toff, smeta, scand, vi);
+    else if constexpr (L < LF) fused_phase<L + 1, 0, LF, V>(a, work_all, smem, lay, g, binom, toff, smeta, scand, vi);
+}
+// a.hsub_out: whether layer LF's phase 1 writes the subset maxima (read by a
+// layer above LF); a.work unused (work_all: every (layer, phase) prefix)
+template <int LF, int V>
+__global__ void __launch_bounds__(kFusedThreads) score_small_kernel(ScoreArgs a, const uint64_t *work_all) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const LdsLayout lay = lds_layout(a.n, a.nv, a.S, LF, V);
+    double *g = reinterpret_cast<double *>(smem + lay.gram);
+    uint32_t *binom = reinterpret_cast<uint32_t *>(smem + lay.binom);
+    uint64_t *toff = reinterpret_cast<uint64_t *>(smem + lay.toff);
+    int *smeta = reinterpret_cast<int *>(smem + lay.meta);
+    uint8_t *scand = reinterpret_cast<uint8_t *>(smem + lay.cand);
+    for (int i = threadIdx.x; i < a.n * a.n; i += kFusedThreads) g[i] = a.gram[i];
+    for (int i = threadIdx.x; i < 64 * kBinomK; i += kFusedThreads) binom[i] = a.binom[i];
+    for (int i = threadIdx.x; i <= a.nv * a.S; i += kFusedThreads) toff[i] = a.tbl_off[i];
+    for (int i = threadIdx.x; i < a.nv * 4; i += kFusedThreads) smeta[i] = a.meta[i];
+    for (int i = threadIdx.x; i < a.nv * 16; i += kFusedThreads)
+        reinterpret_cast<uint32_t *>(scand)[i] = reinterpret_cast<const uint32_t *>(a.cand)[i];
+    __syncthreads();
+    fused_phase<1, 0, LF, V>(a, work_all, smem, lay, g, binom, toff, smeta, scand, (int)blockIdx.x);
 }
 
 // Second half of a queued layer (variant bit 4): one wave (64 threads) per
@@ -1862,6 +1960,16 @@ const char *kWalkNames[2][kMaxL + 1] = {
     {"", "walk_1_rest", "walk_2_rest", "walk_3_rest", "walk_4_rest", "walk_5_rest", "walk_6_rest", "walk_7_rest",
      "walk_8_rest"}};
 
+using SmallFn = void (*)(ScoreArgs, const uint64_t *);
+SmallFn small_kernel(int Lf) {
+    switch (Lf) {
+        case 1: return score_small_kernel<1, 65>;
+        case 2: return score_small_kernel<2, 65>;
+        case 3: return score_small_kernel<3, 65>;
+        default: return score_small_kernel<4, 65>;
+    }
+}
+
 KernelFn layer_kernel(int L, int phase, int variant) {
     switch (L) {
         case 1: return pick<1>(phase, variant);
@@ -2645,6 +2753,8 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     // launch, no stream groups.  The rest: per group, score + queued walk.
     const int Ls = (variant & 16) && !wck ? std::min(kmax, std::min(kMaxL, c->score_small_layers)) : 0;
     const int vsmall = variant & 65;  // the one-pass form (keeping the subset maxima under bit 6)
+    // ... of which layers <= Lf in one launch, a workgroup per variable
+    const int Lf = vsmall == 65 ? std::min(Ls, c->score_fused) : 0;
     bool forked = false;
     // The wide layers variable by variable (wide_pool 1) pay when the
     // variables that reach them differ in size: the long replays of one then
@@ -2705,7 +2815,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                      (uint64_t)(uintptr_t)c->out_offsets.p, (uint64_t)(uintptr_t)c->d_blk.p,
                      (uint64_t)(uintptr_t)c->gram.p, (uint64_t)(uintptr_t)c->d_binom.p,
                      (uint64_t)(uintptr_t)c->d_binom64.p, (uint64_t)(uintptr_t)c->d_hsub.p, (uint64_t)total_slots,
-                     (uint64_t)c->score_small_layers});
+                     (uint64_t)c->score_small_layers, (uint64_t)c->score_fused});
         for (int i = 0; i < nv; ++i) gkey.push_back((uint64_t)vars[i]);
         for (int i = 0; i < nv; ++i) gkey.push_back(candidates[i]);
         for (const std::string &nm : c->prof_only) gkey.push_back(std::hash<std::string>{}(nm));
@@ -2723,6 +2833,25 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     const size_t pend0 = c->pending.size();
     for (int L = 1; L <= kmax; ++L) {
         for (int ph = 0; ph < 2; ++ph) {
+            if (L <= Lf) {
+                if (L == 1 && ph == 0) {
+                    ScoreArgs ss = sa;
+                    ss.work = nullptr;
+                    ss.queue = nullptr;
+                    ss.qcount = nullptr;
+                    ss.hsub_out = Lf < kmax;  // layer Lf's phase 1 maxima: read only by a layer above
+                    const LdsLayout lay = lds_layout(n, nv, S, Lf, 65);
+                    const SmallFn kfn = small_kernel(Lf);
+                    if (lay.total > 64 * 1024)
+                        ULG_HIP(c, hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       lay.total));
+                    prof_begin_s(c, "score_small_fused", c->stream);
+                    hipLaunchKernelGGL(kfn, dim3((unsigned)nv), dim3(kFusedThreads), (size_t)lay.total, c->stream, ss,
+                                       (const uint64_t *)c->d_work.p);
+                    prof_end_s(c, c->stream);
+                }
+                continue;
+            }
             if (L <= Ls) {
                 const size_t wo = ((size_t)L * 2 + ph) * (nv + 1);
                 const uint64_t cnt = work[wo + nv];

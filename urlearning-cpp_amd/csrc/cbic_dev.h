@@ -213,9 +213,13 @@ struct PresList {
 // table base in SGPRs and a 32-bit VGPR offset (one address register per
 // pending load instead of a 64-bit pair).  !B32 (tables of 2^30 slots or
 // more, the one-pass variant 1 only): 64-bit slot arithmetic.
+//
+// vals (non-null): each gathered key's value at vals[t] (a local array of
+// 2^Q floats the caller indexes with constants only, so it stays in registers)
 template <int L, int PHASE, int Q, int W, class LD = LdPlain, int NB = 16, bool B32 = true, int PART = 0>
 __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi, float thr, const uint32_t *binom,
-                                                  uint64_t cpack, bool z, const float *table, const uint64_t *toffv) {
+                                                  uint64_t cpack, bool z, const float *table, const uint64_t *toffv,
+                                                  float *vals = nullptr) {
     constexpr PresList<L, PHASE, Q, PART> PL{};
     using Slot = std::conditional_t<B32, uint32_t, uint64_t>;
     uint32_t RB[Q][L + 1];
@@ -269,6 +273,7 @@ __device__ __forceinline__ void presence_unrolled(Bits<W> &present, Bits<W> &hi,
             const uint32_t t = PL.t[b0 + i];
             float x = v[i];
             if (t & 1u) x = z ? x : absent_f();
+            if (vals) vals[t] = x;
             const uint32_t bit = 1u << (t & 31u);
             pw[t >> 5] |= (fbits(x) != kAbsentBits) ? bit : 0u;
             hw[t >> 5] |= (x >= thr) ? bit : 0u;  // the absent sentinel is a NaN: never >= thr

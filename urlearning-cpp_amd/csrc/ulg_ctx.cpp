@@ -192,6 +192,11 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         c->score_small_layers = (int)value;
         return ULG_OK;
     }
+    if (std::strcmp(name, "score_fused") == 0) {
+        if (value < 0 || value > 4) return set_err(c, ULG_ERR_ARG, "score_fused must be 0..4");
+        c->score_fused = (int)value;
+        return ULG_OK;
+    }
     if (std::strcmp(name, "score_variant") == 0) {
         if (value != 1 && value != 49 && value != 65 && value != 113)
             return set_err(c, ULG_ERR_ARG, "score_variant must be 1, 49, 65 or 113");

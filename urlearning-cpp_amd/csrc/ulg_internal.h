@@ -72,6 +72,7 @@ struct ulg_ctx {
     int score_variant = 113;
     int score_streams = 3;                  // scorer variable groups on concurrent streams
     int score_small_layers = 4;             // layers <= this run one-pass on one stream (two-pass variants)
+    int score_fused = 3;                    // ... and layers <= this (<= small layers) in one launch, a workgroup per variable
     std::vector<hipStream_t> aux_streams;   // created on first use
     std::vector<hipEvent_t> sync_events;
     int64_t time_limit_ms = 0;     // -r: wall-clock budget per scoring call / search (0 = none)
