@@ -35,14 +35,42 @@ __device__ __forceinline__ float absent_f() { return __uint_as_float(kAbsentBits
 // ------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t B(const uint32_t *binom, int a, int k) { return binom[a * kBinomK + k]; }
 
+// Element i (from the top) of the set of colex rank r is the largest c below
+// the previous one with C(c, i) <= r.  A scan down the table is a chain of up
+// to U dependent LDS reads per set; instead C(x, i) i! = x (x-1) .. (x-i+1)
+// <= (x - (i-1)/2)^i (AM-GM) and >= (x - (i-1)/2 - 0.75)^i for i <= 8, so the
+// answer lies in [e - 3, e] for e = floor((r i!)^(1/i) + (i-1)/2) + 1, and
+// one round of four independent reads (e + 1 as the guard) settles it; the
+// scan remains as the fallback should the float estimate ever land low.
 __device__ __forceinline__ uint64_t unrank_colex(uint64_t r, int l, int U, const uint32_t *binom) {
+    constexpr float kFact[9] = {1.f, 1.f, 2.f, 6.f, 24.f, 120.f, 720.f, 5040.f, 40320.f};
+    constexpr float kInv[9] = {1.f, 1.f, 0.5f, 1.f / 3.f, 0.25f, 0.2f, 1.f / 6.f, 1.f / 7.f, 0.125f};
     uint64_t mask = 0;
     int c = U - 1;
     for (int i = l; i >= 1; --i) {
-        while (c >= 0 && (uint64_t)B(binom, c, i) > r) --c;
-        mask |= 1ull << c;
-        r -= B(binom, c, i);
-        --c;
+        int e;
+        if (i == 1 || i > 8) {
+            e = i == 1 ? (int)(r < (uint64_t)c ? r : (uint64_t)c) : c;
+        } else {
+            const float g = exp2f(log2f((float)r * kFact[i]) * kInv[i]);  // r = 0: 0
+            e = (int)(g + 0.5f * (float)(i - 1)) + 1;
+            e = e < c ? e : c;
+            e = e > i - 1 ? e : i - 1;  // C(i - 1, i) = 0 <= r
+        }
+        const bool low = e < c && (uint64_t)B(binom, e + 1, i) <= r;  // the estimate fell short
+        const uint64_t b0 = B(binom, e, i);
+        const uint64_t b1 = e >= 1 ? B(binom, e - 1, i) : 0ull;
+        const uint64_t b2 = e >= 2 ? B(binom, e - 2, i) : 0ull;
+        int cc = b0 <= r ? e : (b1 <= r ? e - 1 : (b2 <= r ? e - 2 : -1));
+        uint64_t bc = b0 <= r ? b0 : (b1 <= r ? b1 : b2);
+        if (low || cc < 0) {
+            cc = low ? c : e - 3;
+            while (cc >= 0 && (uint64_t)B(binom, cc, i) > r) --cc;
+            bc = B(binom, cc, i);
+        }
+        mask |= 1ull << cc;
+        r -= bc;
+        c = cc - 1;
     }
     return mask;
 }

@@ -26,30 +26,24 @@ inline bool host_walk(int L, int phase, uint64_t *skip, const uint64_t *hib, boo
     // bit b of the word w ^ 2^(l-6): one word read per neighbour, and six
     // neighbours from one read
     const int ql = q < 6 ? q : 6;
-    auto nbr = [&](uint32_t Nn, uint32_t &sm_, uint32_t &hm_) {
+    // (the kernel's hi mask hm is only ever tested at the chosen entry, so
+    // the host reads that one bit of hib directly instead)
+    auto nbr = [&](uint32_t Nn, uint32_t &sm_) {
         ++ncalls;
         const uint32_t w = Nn >> 6, b = Nn & 63u;
-        const uint64_t ws = skip[w], wh = hib[w];
-        uint32_t s_ = above, h_ = 0;
-        for (int l = 0; l < ql; ++l) {
-            const uint32_t bt = b ^ (1u << l);
-            s_ |= (uint32_t)((ws >> bt) & 1ull) << l;
-            h_ |= (uint32_t)((wh >> bt) & 1ull) << l;
-        }
-        for (int l = 6; l < q; ++l) {
-            const uint32_t wt = w ^ (1u << (l - 6));
-            s_ |= (uint32_t)((skip[wt] >> b) & 1ull) << l;
-            h_ |= (uint32_t)((hib[wt] >> b) & 1ull) << l;
-        }
+        const uint64_t ws = skip[w];
+        uint32_t s_ = above;
+        for (int l = 0; l < ql; ++l) s_ |= (uint32_t)((ws >> (b ^ (1u << l))) & 1ull) << l;
+        for (int l = 6; l < q; ++l) s_ |= (uint32_t)((skip[w ^ (1u << (l - 6))] >> b) & 1ull) << l;
         sm_ = s_;
-        hm_ = h_;
     };
+    auto hi_at = [&](uint32_t t) -> bool { return (hib[t >> 6] >> (t & 63u)) & 1ull; };
     struct Frame {
-        uint32_t N, rem, B, w, hm, sm;
+        uint32_t N, rem, B, w, sm;
     } frames[kStragDepth];
     const uint32_t P = phase == 0 ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
-    uint32_t N = P, rem = P, B = 0, sm, hm;
-    nbr(N, sm, hm);
+    uint32_t N = P, rem = P, B = 0, sm;
+    nbr(N, sm);
     int x = 31, zr = 0, js = 0, d = 0, mS = L;
     bool pend = false, incall = false, dom = false;
     uint64_t it = 0;
@@ -130,7 +124,6 @@ inline bool host_walk(int L, int phase, uint64_t *skip, const uint64_t *hib, boo
                 N = f.N;
                 rem = f.rem;
                 B = f.B;
-                hm = f.hm;
                 sm = f.sm;
                 x = (int)(f.w & 31u);
                 zr = (int)((f.w >> 5) & 31u);
@@ -141,14 +134,13 @@ inline bool host_walk(int L, int phase, uint64_t *skip, const uint64_t *hib, boo
                 if (cx != 0) {
                     if (cmarked) sm |= 1u << cx;
                 } else {
-                    uint32_t h2;
-                    nbr(N, sm, h2);
+                    nbr(N, sm);
                 }
                 continue;
             }
         }
         if ((sm >> y) & 1u) continue;
-        if ((hm >> y) & 1u) {
+        if (y < q && hi_at(N ^ (1u << y))) {
             dom = true;
             break;
         }
@@ -161,7 +153,7 @@ inline bool host_walk(int L, int phase, uint64_t *skip, const uint64_t *hib, boo
         frames[d] = Frame{N, rem, B,
                           (uint32_t)x | ((uint32_t)zr << 5) | ((uint32_t)js << 10) | ((uint32_t)pend << 15) |
                               ((uint32_t)incall << 16),
-                          hm, sm};
+                          sm};
         ++d;
         N ^= 1u << y;
         x = y;
@@ -172,7 +164,7 @@ inline bool host_walk(int L, int phase, uint64_t *skip, const uint64_t *hib, boo
         pend = false;
         incall = false;
         mS = mc;
-        nbr(N, sm, hm);
+        nbr(N, sm);
     }
     if (iters) *iters = it;
     if (nbr_calls) *nbr_calls = ncalls;
