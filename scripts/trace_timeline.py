@@ -1,8 +1,8 @@
 import csv, sys, collections
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-# the last call: kernels after the last empty_set_kernel
-idx = max(i for i, r in enumerate(rows) if "empty_set" in r["Kernel_Name"])
+# the last call: kernels after the last call_prologue_kernel
+idx = max(i for i, r in enumerate(rows) if "call_prologue" in r["Kernel_Name"])
 last = rows[idx:]
 t0 = int(last[0]["Start_Timestamp"])
 for r in last:

@@ -1626,9 +1626,17 @@ __global__ void __launch_bounds__(256) hikey_strided_kernel(HiArgs a) {
     for (int k = 0; k < (1 << G); ++k) h[base + ((uint64_t)k << a.bit_lo)] = r[k];
 }
 
-__global__ void empty_set_kernel(const uint64_t *tbl_off, int nv, int S, float *table) {
-    const int vi = blockIdx.x * blockDim.x + threadIdx.x;
-    if (vi < nv) table[tbl_off[(uint64_t)vi * S]] = -0.0f;  // cache[empty] = -0.0f (BIC_OLS.cpp:249)
+// The call's first launch: cache[empty] = -0.0f per variable (BIC_OLS.cpp:249)
+// and the walk-queue counters zeroed.  It sits inside the call's hipGraph;
+// as three eager launches before the replay (a kernel and two memsets) they
+// left ~40 us of submission gaps ahead of the first layer.
+__global__ void call_prologue_kernel(const uint64_t *tbl_off, int nv, int S, float *table,
+                                     unsigned long long *qcount, uint64_t nqc, unsigned long long *qseg,
+                                     uint64_t nseg) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < (uint64_t)nv) table[tbl_off[i * (uint64_t)S]] = -0.0f;
+    if (qcount && i < nqc) qcount[i] = 0ull;
+    if (qseg && i < nseg) qseg[i] = 0ull;
 }
 
 // ---- compaction of the slabs into (set, score) lists ------------------------
@@ -2628,9 +2636,6 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
         (rc = ensure(c, c->out_scores, total_slots)) || (rc = ensure(c, c->out_offsets, (size_t)nv + 1)))
         return rc;
 
-    prof_begin(c, "empty_set");
-    empty_set_kernel<<<(nv + 63) / 64, 64, 0, c->stream>>>(c->d_tbl_off.p, nv, S, c->table.p);
-    prof_end(c);
     ScoreArgs sa;
     sa.hsub_out = 1;
     sa.gram = c->gram.p;
@@ -2720,11 +2725,11 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
         if ((rc = ensure(c, c->d_queue, (size_t)G * qwords)) || (rc = ensure(c, c->d_qcount, nqc)) ||
             (rc = ensure(c, c->d_wqueue, (size_t)G * wqwords)))
             return rc;
-        ULG_HIP(c, hipMemsetAsync(c->d_qcount.p, 0, sizeof(unsigned long long) * nqc, c->stream));
-        if ((rc = ensure(c, c->d_qseg, (size_t)segoff.back()))) return rc;
-        ULG_HIP(c, hipMemsetAsync(c->d_qseg.p, 0, sizeof(unsigned long long) * std::max<uint64_t>(segoff.back(), 1),
-                                  c->stream));
+        if ((rc = ensure(c, c->d_qseg, (size_t)std::max<uint64_t>(segoff.back(), 1)))) return rc;
     }
+    // zeroed by call_prologue_kernel (the first launch of the sequence below)
+    const bool zero_q = (variant & 16) || kmax > kMaxL;
+    const uint64_t nqseg = zero_q ? std::max<uint64_t>(segoff.back(), 1) : 0;
     // wide-layer walks: one checked-bitset slice per stream group, allocated
     // before any launch (2^q bits per walking set, q <= kmax + 1)
     uint64_t wslice = 0;
@@ -2845,6 +2850,14 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     }
     {
     const size_t pend0 = c->pending.size();
+    {
+        const uint64_t nz = std::max<uint64_t>((uint64_t)nv, std::max<uint64_t>(zero_q ? nqc : 0, nqseg));
+        prof_begin(c, "call_prologue");
+        call_prologue_kernel<<<(unsigned)((nz + 255) / 256), 256, 0, c->stream>>>(
+            c->d_tbl_off.p, nv, S, c->table.p, zero_q ? c->d_qcount.p : nullptr, zero_q ? nqc : 0,
+            zero_q ? c->d_qseg.p : nullptr, nqseg);
+        prof_end(c);
+    }
     for (int L = 1; L <= kmax; ++L) {
         for (int ph = 0; ph < 2; ++ph) {
             if (L <= Lf) {
@@ -3052,11 +3065,15 @@ launched:
         c->async_pending = true;
         return ULG_OK;
     }
-    uint64_t stored = 0;
     unsigned long long wide_err = 0;
-    ULG_HIP(c, hipMemcpyAsync(&stored, c->d_blk.p + nb, 8, hipMemcpyDeviceToHost, c->stream));
+    // the stored count through the context's pinned word (a pageable
+    // destination goes through a staging copy)
+    if (!c->async_pinned)
+        ULG_HIP(c, hipHostMalloc((void **)&c->async_pinned, sizeof(unsigned long long), hipHostMallocDefault));
+    ULG_HIP(c, hipMemcpyAsync(c->async_pinned, c->d_blk.p + nb, 8, hipMemcpyDeviceToHost, c->stream));
     if (kmax > kMaxL) ULG_HIP(c, hipMemcpyAsync(&wide_err, c->d_qcount.p + nqc - 1, 8, hipMemcpyDeviceToHost, c->stream));
     ULG_HIP(c, hipStreamSynchronize(c->stream));
+    const uint64_t stored = *c->async_pinned;
     prof_collect(c);
     if (wide_err)
         return set_err(c, ULG_ERR_UNSUPPORTED,
