@@ -8,6 +8,35 @@
 
 namespace ulg {
 
+// In-word neighbours of a node at bit b of its word: positions b ^ 2^l,
+// l < 6.  pext over mask[b] returns them in ascending position order -- the
+// l with bit l of b set in decreasing l, then the others in increasing l --
+// and perm[b] puts them back in l order.
+struct NbrTables {
+    uint64_t mask[64];
+    uint8_t perm[64][64];
+    NbrTables() {
+        for (int b = 0; b < 64; ++b) {
+            int order[6], k = 0;
+            for (int l = 5; l >= 0; --l)
+                if ((b >> l) & 1) order[k++] = l;
+            for (int l = 0; l < 6; ++l)
+                if (!((b >> l) & 1)) order[k++] = l;
+            mask[b] = 0;
+            for (int l = 0; l < 6; ++l) mask[b] |= 1ull << (b ^ (1 << l));
+            for (int v = 0; v < 64; ++v) {
+                uint8_t o = 0;
+                for (int j = 0; j < 6; ++j) o |= (uint8_t)(((v >> j) & 1) << order[j]);
+                perm[b][v] = o;
+            }
+        }
+    }
+};
+inline const NbrTables &nbr_tables() {
+    static const NbrTables t;
+    return t;
+}
+
 constexpr int kStragDepth = 24;                // frames of a replay (cbic.hip's LDS replay has the same)
 constexpr uint64_t kStragIterCap = 1ull << 32;  // iterations before a replay fails loudly
 
@@ -28,12 +57,17 @@ inline bool host_walk(int L, int phase, uint64_t *skip, const uint64_t *hib, boo
     const int ql = q < 6 ? q : 6;
     // (the kernel's hi mask hm is only ever tested at the chosen entry, so
     // the host reads that one bit of hib directly instead)
+    const NbrTables &nt = nbr_tables();
     auto nbr = [&](uint32_t Nn, uint32_t &sm_) {
         ++ncalls;
         const uint32_t w = Nn >> 6, b = Nn & 63u;
         const uint64_t ws = skip[w];
         uint32_t s_ = above;
-        for (int l = 0; l < ql; ++l) s_ |= (uint32_t)((ws >> (b ^ (1u << l))) & 1ull) << l;
+        if (ql == 6) {
+            s_ |= nt.perm[b][__builtin_ia32_pext_di(ws, nt.mask[b])];
+        } else {
+            for (int l = 0; l < ql; ++l) s_ |= (uint32_t)((ws >> (b ^ (1u << l))) & 1ull) << l;
+        }
         for (int l = 6; l < q; ++l) s_ |= (uint32_t)((skip[w ^ (1u << (l - 6))] >> b) & 1ull) << l;
         sm_ = s_;
     };
