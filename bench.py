@@ -186,12 +186,13 @@ def host_pmu(ctx, expanded):
     return out if any(out[k] is not None for k in ("cycles_per_expansion", "cache_misses_per_expansion")) else None
 
 
-PMC_SEARCH = os.path.join(PROFILES, "pmc_search_traffic.json")
+# round 6: FETCH/WRITE passes of the sweep kernel HEAD launches (scripts/pmc_search.sh)
+PMC_SEARCH = os.path.join(os.path.dirname(PROFILES), "r6", "pmc_search_traffic.json")
 
 
 def search_roofline(cfg, n, pull, reps):
-    """Roofline of the GPU order-graph sweep (layer_pull_kernel, one launch
-    per layer) on a full skeleton: a layer-L node reads L predecessors' g
+    """Roofline of the GPU order-graph sweep (layer_pull_w32_kernel at C3,
+    search_gpu.hip, one launch per layer) on a full skeleton: a layer-L node reads L predecessors' g
     (4 B) and best-score costs (4 B, the 32-bit lattice) and writes its g
     (4 B) and leaf (1 B), so one sweep's algorithmic bytes are
     sum_L C(n, L) (8 L + 5).  The achieved rate divides them by the sweep's
@@ -200,16 +201,17 @@ def search_roofline(cfg, n, pull, reps):
     cnt, sweep_ms = pull["count"], pull["total_ms"] / reps
     algo = sum(math.comb(n, L) * (8 * L + 5) for L in range(1, n + 1))
     achieved = algo / (sweep_ms * 1e-3) / 1e9
-    traffic, src = None, None
+    traffic, src, kern = None, None, pull.get("kernel", "layer_pull_w32_kernel")
     try:
         t = json.load(open(PMC_SEARCH))
         if t.get("config_id") == cfg["id"] and t.get("n") == n:
-            traffic, src = t["traffic_bytes_per_sweep"], "profiles/r2/pmc_search_traffic.json"
+            traffic, src = t["traffic_bytes_per_sweep"], os.path.relpath(PMC_SEARCH, ROOT)
+            kern = t.get("kernel", kern)
     except (OSError, ValueError):
         pass
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per sweep",
-            "traffic_source": src, "kernel": "layer_pull_kernel", "launches_per_sweep": cnt // reps,
+            "traffic_source": src, "kernel": kern, "launches_per_sweep": cnt // reps,
             "sweep_kernel_ms": sweep_ms, "algorithmic_bytes_per_sweep": algo,
             "bytes_per_node": "8 L + 5 (L predecessors x (4 B g + 4 B best-score cost) + 4 B g + 1 B leaf written)"}
 

@@ -322,7 +322,8 @@ int ulg_sweep_shard_end(ulg_ctx *ctx, uint64_t *vpar, int *order, float *goal_co
  * (0..4, default 3): layers up to this size (and up to score_small_layers)
  * run in ONE launch, a workgroup of 1024 threads per variable taking its
  * layers and phases in order with a barrier between them (score_variant 113
- * / 65 only; lists identical either way; C3 layers 1-3: 40 us against 54 us
+ * only, and not under time_limit_ms, whose budget is checked after every
+ * layer; lists identical either way; C3 layers 1-3: 40 us against 54 us
  * for six launches, layer 4 in it 340 us: too many sets for one workgroup).
  * "time_limit_ms" (default 0 = none): the reference's -r running-time budget
  * (score: per calculateScores call, score_calculator.cpp:33-52,78,91; astar:
@@ -368,7 +369,10 @@ int ulg_set_option(ulg_ctx *ctx, const char *name, int64_t value);
  * score_calculator.h:45), "exact_cycles" / "exact_instructions" /
  * "exact_cache_misses" (the last exact-order A*'s user-space host counters on
  * the calling thread, perf_event_open; -1 where the host does not grant
- * them). */
+ * them), "score_error_word" (the last scoring call's device error word: 0,
+ * or bit 0 a wide walk over its cap, bit 1 a walk-queue segment overflow,
+ * bit 2 a walk entry naming a slot past the call's table -- any nonzero
+ * word also made that call return a nonzero status). */
 int ulg_get_info(ulg_ctx *ctx, const char *name, int64_t *value);
 
 /* ---- profiling (per-kernel HIP-event timing on the context stream) ---- */
@@ -384,6 +388,13 @@ int ulg_profile_reset(ulg_ctx *ctx);
  * each timed kernel costs two event records on the host, which the small
  * launches of a scoring call notice. */
 int ulg_profile_select(ulg_ctx *ctx, const char *names);
+
+/* ---- diagnostics (tests only; no reference counterpart) ---- */
+/* One host pattern-database build in the form the triplet look-ahead pool
+ * uses (StaticPatternDatabase, static_pattern_database.cpp:82-247, over
+ * `cluster`), with the pool's cancel flag preset when cancel_preset != 0.
+ * out[4]: built, cancelled, entries built, entries equal to the device PDB's. */
+int ulg_diag_pdb_host(ulg_ctx *ctx, uint64_t cluster, int pd_count, int cancel_preset, int64_t *out);
 
 #ifdef __cplusplus
 }

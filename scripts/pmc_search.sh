@@ -1,7 +1,7 @@
 #!/bin/bash
 # FETCH_SIZE and WRITE_SIZE passes (each its own rocprofv3 --pmc run) over a
 # short C3 bench WITH the search side, then the HBM traffic of one GPU
-# order-graph sweep (all layer_pull_kernel dispatches / sweeps).
+# order-graph sweep (all layer_pull*_kernel dispatches / sweeps).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

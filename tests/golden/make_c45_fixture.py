@@ -17,8 +17,11 @@ stored-set count, a SHA-256 of the sorted uint64 masks, the float64 sum of
 the float32 scores, and every 512th stored (set, score) pair in sorted-set
 order so the test can hold each sampled score to 1e-6 relative.
 
-This runs in this container only (it needs oracle/build/ and about an hour
-of CPU on 5 cores):  python tests/golden/make_c45_fixture.py [procs]
+This runs in this container only (it needs oracle/build/; the full set is
+about five hours of CPU):  python tests/golden/make_c45_fixture.py [procs]
+Variables already in the committed fixture are kept (same data, same
+skeleton), only the missing ones are run, and the file is rewritten after
+every finished variable so a partial run keeps what it has.
 """
 import hashlib
 import json
@@ -35,8 +38,11 @@ import synth  # noqa: E402
 
 LAM, SEED, STRIDE = 2.0, 9200, 512
 CONFIGS = {
-    "c4": dict(n=30, N=100000, k=29, skeleton="mmpc", alpha=0.01, variables=[3, 7, 9]),
-    "c5": dict(n=32, N=50000, k=6, skeleton="full", variables=[0, 17]),
+    # C4: every variable (round 6; cost grows ~2.2x per candidate, the
+    # m = 18 variable 9 takes ~52 min, m = 17 variable 23 ~20 min).
+    "c4": dict(n=30, N=100000, k=29, skeleton="mmpc", alpha=0.01, variables=list(range(30))),
+    # C5: 8 variables spread over the order (~41 min each).
+    "c5": dict(n=32, N=50000, k=6, skeleton="full", variables=[0, 5, 9, 13, 17, 21, 25, 31]),
 }
 
 
@@ -76,7 +82,8 @@ def main():
     import oracle
     oracle.build()
     procs = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    jobs = [(nm, v) for nm, c in CONFIGS.items() for v in c["variables"]]
+    path = os.path.join(ROOT, "tests", "golden", "c45_oracle.json")
+    old = json.load(open(path)) if os.path.exists(path) else {}
     out = {"generator": "tests/golden/make_c45_fixture.py (oracle ora_score_variable, ora_mmpc)",
            "lambda": LAM, "seed": SEED, "sample_stride": STRIDE}
     for nm, c in CONFIGS.items():
@@ -84,13 +91,24 @@ def main():
         _, rows = candidates(c, oracle.Dataset(X))
         out[nm] = {k: v for k, v in c.items() if k != "variables"}
         out[nm]["skeleton_rows"] = rows
-        out[nm]["per_variable"] = {}
+        kept = old.get(nm, {})
+        same = kept.get("skeleton_rows") == rows and kept.get("k") == c["k"]
+        out[nm]["per_variable"] = dict(kept.get("per_variable", {})) if same else {}
+    jobs = [(nm, v) for nm, c in CONFIGS.items() for v in c["variables"]
+            if str(v) not in out[nm]["per_variable"]]
+    # Longest first (C5, then C4 by candidate count) so the pool ends together.
+    X4, _ = synth.gaussian_sem(30, 100000, SEED)
+    c4c, _ = candidates(CONFIGS["c4"], oracle.Dataset(X4))
+    jobs.sort(key=lambda j: -(1 << 40) if j[0] == "c5" else -(1 << bin(c4c[j[1]]).count("1")))
+    print(f"{len(jobs)} variables to run: {jobs}", flush=True)
     with Pool(procs) as p:
         for nm, v, res in p.imap_unordered(job, jobs):
             out[nm]["per_variable"][str(v)] = res
             print(f"{nm} v={v}: {res['stored']} stored in {res['oracle_seconds']:.0f} s", flush=True)
-    path = os.path.join(ROOT, "tests", "golden", "c45_oracle.json")
-    json.dump(out, open(path, "w"), indent=1)
+            json.dump(out, open(path + ".tmp", "w"), indent=1)
+            os.replace(path + ".tmp", path)
+    json.dump(out, open(path + ".tmp", "w"), indent=1)
+    os.replace(path + ".tmp", path)
     print("wrote", path)
 
 

@@ -191,7 +191,7 @@ def test_rescoring_is_deterministic(ulg_ctx):
         assert x.tobytes() == y.tobytes()
 
 
-@pytest.mark.parametrize("variant", [1, 49, 65, 113])
+@pytest.mark.parametrize("variant", [1, 49, 65, 113, 241])
 def test_scorer_variants_identical(ulg_ctx, oracle_built, variant):
     """Every scorer variant (presence gather x recursion form x decision-only
     walk x subset-maxima settling) stores exactly the oracle's sets (k=6
@@ -229,9 +229,10 @@ def test_walk_forms_identical(ulg_ctx, oracle_built, monkeypatch, sets_per_lane)
 
 
 def test_subset_maxima_identical_c3_and_without_var0(ulg_ctx):
-    """Variant 113 (subset maxima settle sets before the presence gathers,
-    the rule keys gathered before the rest) against 49 (every set gathered in
-    full): identical lists at C3 and on candidate
+    """Variants 113 (subset maxima settle sets before the presence gathers,
+    the rule keys gathered before the rest) and 241 (113 with the sets the
+    rules leave to the walk compacted a second time) against 49 (every set
+    gathered in full): identical lists at C3 and on candidate
     lists without variable 0 (phase 1 then has no P\\a+{0} keys)."""
     n = 25
     X, _ = synth.gaussian_sem(n, 10000, 9200)
@@ -241,10 +242,10 @@ def test_subset_maxima_identical_c3_and_without_var0(ulg_ctx):
     try:
         for variables, cands, k in cases:
             res = {}
-            for variant in (49, 113):
+            for variant in (49, 113, 241):
                 ulg_ctx.set_option("score_variant", variant)
                 res[variant] = ulg_ctx.score_all(variables, cands, k)
-            for other in (113,):
+            for other in (113, 241):
                 for a, b in zip(res[49], res[other]):
                     assert np.asarray(a).tobytes() == np.asarray(b).tobytes(), (len(variables), k, other)
     finally:
@@ -288,6 +289,54 @@ def test_walk_k6_option_identical_c3_and_segments(ulg_ctx):
     finally:
         ulg_ctx.set_option("walk_k6", 4)
         ulg_ctx.set_option("score_streams", 3)
+
+
+@pytest.mark.parametrize("variant", [113, 241])
+def test_walk_lane_matches_oracle(ulg_ctx, oracle_built, variant):
+    """ulg_set_option("walk_lane", 1): one queued set per lane, the recursion
+    as a per-lane state machine (walk_lane_kernel) -- the oracle's sets with
+    and without variable 0 among the candidates (both N4 phases), k = 6, and
+    on a sparse skeleton."""
+    n = 12
+    X, _ = synth.gaussian_sem(n, 3000, 9251)
+    ulg_ctx.load(X, 2.0)
+    rng = np.random.default_rng(5)
+    sparse = [int(((1 << n) - 1) & ~int(rng.integers(0, 1 << n))) | 1 for _ in range(n)]
+    try:
+        ulg_ctx.set_option("score_variant", variant)
+        ulg_ctx.set_option("walk_lane", 1)
+        for cands in ([(1 << n) - 1] * n, [((1 << n) - 1) & ~1] * n, sparse):
+            variables = list(range(1, n)) if cands[0] & 1 == 0 else list(range(n))
+            cands = cands[:len(variables)]
+            g = ulg_ctx.score_all(variables, cands, 6)
+            o = _oracle_lists(oracle_built, X, 2.0, variables, cands, 6)
+            _compare_lists(*o, *g, variables, ctx=f"walk_lane variant {variant}")
+    finally:
+        ulg_ctx.set_option("walk_lane", 0)
+        ulg_ctx.set_option("score_variant", DEFAULT_VARIANT)
+
+
+def test_walk_lane_identical_c3_c5(ulg_ctx):
+    """The per-lane walk stores the union walk's lists bit for bit at C3 (and
+    so the oracle command lines', tests/golden/c3_oracle.json) and at the
+    k = 6 C5 shape, with one and three stream groups."""
+    for n, N in ((25, 10000), (32, 50000)):
+        X, _ = synth.gaussian_sem(n, N, 9200)
+        ulg_ctx.load(X, 2.0)
+        full = [(1 << n) - 1] * n
+        try:
+            for streams in (1, 3):
+                ulg_ctx.set_option("score_streams", streams)
+                ulg_ctx.set_option("walk_lane", 0)
+                ref = ulg_ctx.score_all(list(range(n)), full, 6)
+                ulg_ctx.set_option("walk_lane", 1)
+                got = ulg_ctx.score_all(list(range(n)), full, 6)
+                assert ulg_ctx.info("score_error_word") == 0
+                for a, b in zip(ref, got):
+                    assert np.asarray(a).tobytes() == np.asarray(b).tobytes(), (n, streams)
+        finally:
+            ulg_ctx.set_option("walk_lane", 0)
+            ulg_ctx.set_option("score_streams", 3)
 
 
 def test_score_fused_small_layers_identical(ulg_ctx):

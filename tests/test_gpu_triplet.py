@@ -255,26 +255,27 @@ def test_triplet_budget_interrupts_a_running_search(ulg_ctx):
     """-r bounds the wall clock: the reference's A* loop stops inside the
     search once outOfTime is set (triplet_astar.cpp:355), so a budget shorter
     than one cluster's search ends the call early instead of after that
-    search.  Full skeleton, n=22: one 22-variable cluster (2^22 lattice
-    nodes); with a budget of a tenth of the uncut call's time the call
-    returns well before the uncut search would finish, with the empty MEC."""
+    search.  Full skeleton: one n-variable cluster (2^n lattice nodes),
+    n = 22, or 24 when the host searches n = 22 in under 0.2 s (so the cut is
+    always measured); with a budget of a tenth of the uncut call's time the
+    call returns well before the uncut search would finish, with the empty
+    MEC."""
     import time
-    n = 22
-    X, _ = synth.gaussian_sem(n, 2000, 9417)
-    full = [(1 << n) - 1] * n
-    ulg_ctx.load(X, 2.0)
-    ulg_ctx.score(list(range(n)), full, 3)
-    ulg_ctx.search_from_scores()
-    t0 = time.perf_counter()
-    ref = ulg_ctx.triplet(edges=full)
-    uncut = time.perf_counter() - t0
-    assert ulg_ctx.info("out_of_time") == 0 and ref["distinct"] == 1
+    for n in (22, 24):
+        X, _ = synth.gaussian_sem(n, 2000, 9417)
+        full = [(1 << n) - 1] * n
+        ulg_ctx.load(X, 2.0)
+        ulg_ctx.score(list(range(n)), full, 3)
+        ulg_ctx.search_from_scores()
+        t0 = time.perf_counter()
+        ref = ulg_ctx.triplet(edges=full)
+        uncut = time.perf_counter() - t0
+        assert ulg_ctx.info("out_of_time") == 0 and ref["distinct"] == 1
+        if uncut >= 0.2:
+            break
+    # the host's speed sets the uncut time (n = 22: 0.55-1.5 s across boxes)
+    assert uncut >= 0.2, f"uncut n={n} search took {uncut:.3f} s: too short to measure a cut"
     try:
-        # the host's speed sets the uncut time (0.55-1.5 s across boxes): the
-        # budget is a tenth of it, so the search outlasts the budget by far;
-        # a host too fast to leave a measurable cut proves nothing either way
-        if uncut < 0.2:
-            pytest.skip(f"uncut search took {uncut:.3f} s: too short to measure a cut")
         budget_ms = max(20, int(100 * uncut))
         ulg_ctx.search_from_scores()  # an empty memo: the cluster is searched again
         ulg_ctx.set_option("time_limit_ms", budget_ms)
@@ -286,3 +287,25 @@ def test_triplet_budget_interrupts_a_running_search(ulg_ctx):
         assert dt < 0.5 * uncut, (dt, uncut, budget_ms)
     finally:
         ulg_ctx.set_option("time_limit_ms", 0)
+
+
+def test_pdb_host_cancel_flag(ulg_ctx):
+    """The look-ahead pool's host pattern database (pdb_host) stops on the
+    pool's cancel flag and says so: built normally it equals the
+    device PDB entry for entry; with the flag set before the build it reports
+    cancelled and builds nothing (the pool then ends that search as
+    cancelled, triplet_host.cpp SearchPool::work)."""
+    n = 14
+    X, _ = synth.gaussian_sem(n, 3000, 9418)
+    full = [(1 << n) - 1] * n
+    ulg_ctx.load(X, 2.0)
+    ulg_ctx.score(list(range(n)), full, 4)
+    ulg_ctx.search_from_scores()
+    cluster = (1 << n) - 1
+    built, cancelled, entries, same = ulg_ctx.diag_pdb_host(cluster, 2, False)
+    assert built == 1 and cancelled == 0 and entries == 2 ** 7 + 2 ** 7 and same == entries
+    built, cancelled, entries, same = ulg_ctx.diag_pdb_host(cluster, 2, True)
+    assert cancelled == 1 and entries == 0
+    # a smaller cluster: the flag works whatever the group sizes
+    built, cancelled, entries, same = ulg_ctx.diag_pdb_host(0b1011011101, 2, False)
+    assert built == 1 and cancelled == 0 and same == entries > 0

@@ -150,6 +150,7 @@ struct ScoreArgs {
                                 // nonempty subsets (the set included; NaN = none), table layout
     uint64_t *queue;            // variant bit 4: lanes left for the walk launch
     unsigned long long *qcount;
+    unsigned long long *err;    // the call's error word (kErrQueue: a walk-queue segment overflowed)
     double N;
     double lambda;
     int n, nv, S;
@@ -175,7 +176,7 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, int on) {
 // then per entry compact mask, slot, ts, children maximum, variable) (16-B
 // aligned)
 struct LdsLayout {
-    int gram, binom, work, toff, meta, cand, stack, bits, cmp, total;
+    int gram, binom, work, toff, meta, cand, stack, bits, cmp, cmp2, total;
 };
 constexpr int kCmpEntryBytes = 8 + 4 + 4 + 4 + 4;
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
@@ -191,7 +192,10 @@ __host__ __device__ inline LdsLayout lds_layout(int n, int nv, int S, int L, int
     l.bits = l.stack;
     const int W = bits_words(L);
     l.cmp = align16(l.bits + (W >= 4 ? 3 * W * kBlock * 8 : 0));
-    l.total = l.cmp + ((V & 80) == 80 ? 16 + kBlock * kCmpEntryBytes : 0);
+    // variant bit 7: the second compaction carries each set's gathered
+    // present / hi words (register bitsets only, W < 4)
+    l.cmp2 = align16(l.cmp + ((V & 80) == 80 ? 16 + kBlock * kCmpEntryBytes : 0));
+    l.total = l.cmp2 + ((V & 208) == 208 && W < 4 ? 2 * W * kBlock * 8 : 0);
     return l;
 }
 
@@ -210,6 +214,11 @@ __host__ __device__ inline LdsLayout lds_layout(int n, int nv, int S, int L, int
 constexpr int kSegBlocks = 32;
 constexpr uint64_t kSegEntries = (uint64_t)kSegBlocks * kBlock;
 constexpr int kSegStride = 16;  // counters 128 B apart
+// Bits of the call's error word (d_qcount[nqc - 1], zeroed by the prologue,
+// copied beside the stored count by scan_kernel): a wide walk over its cap;
+// a queue position past its segment (nothing is written there); a walk entry
+// whose table slot lies past the call's slots (its decision is not written).
+constexpr unsigned long long kErrWide = 1ull, kErrQueue = 2ull, kErrSlot = 4ull;
 __host__ __device__ inline uint64_t seg_count(uint64_t blocks) { return (blocks + kSegBlocks - 1) / kSegBlocks; }
 __device__ __forceinline__ uint64_t walk_segment() { return blockIdx.x % seg_count(gridDim.x); }
 
@@ -219,7 +228,8 @@ __device__ __forceinline__ uint64_t walk_segment() { return blockIdx.x % seg_cou
 // {empty}).  queue / qcount: the segment's entries and counter.
 template <class BS>
 __device__ __forceinline__ void queue_walk(const BS &present, const BS &hi, uint64_t *queue,
-                                           unsigned long long *qcount, uint64_t slot, float ts) {
+                                           unsigned long long *qcount, unsigned long long *err, uint64_t slot,
+                                           float ts) {
     constexpr int W = BS::kWords;
     const unsigned long long act = __ballot(1);
     const int lane = threadIdx.x & 63;
@@ -228,6 +238,12 @@ __device__ __forceinline__ void queue_walk(const BS &present, const BS &hi, uint
     if (lane == leader) base = atomicAdd(qcount, (unsigned long long)__popcll(act));
     base = __shfl(base, leader);
     const uint64_t pos = base + (uint64_t)__popcll(act & ((1ull << lane) - 1ull));
+    // a segment holds at most kSegBlocks blocks' lanes by construction
+    // (seg_count); a sizing mistake becomes an error status, not a stray write
+    if (pos >= kSegEntries) {
+        if (err) atomicOr(err, kErrQueue);
+        return;
+    }
     uint64_t ow[W];
 #pragma unroll
     for (int wj = 0; wj < W; ++wj) ow[wj] = hi.word(wj);
@@ -416,7 +432,7 @@ __device__ __forceinline__ void one_pass_set(const ScoreArgs &a, unsigned char *
                 const uint64_t seg = walk_segment();
                 constexpr int QW = bits_words(L);
                 queue_walk(present, hi, a.queue + seg * kSegEntries * (uint64_t)(1 + 2 * QW),
-                           a.qcount + seg * kSegStride, toff[vbase + L] + rankP, ts);
+                           a.qcount + seg * kSegStride, a.err, toff[vbase + L] + rankP, ts);
             }
             out = dom ? absent_f() : -ts;
         } else {
@@ -463,6 +479,41 @@ __device__ __forceinline__ void one_pass_set(const ScoreArgs &a, unsigned char *
     // the one-pass form keeps the subset maxima for the layers above it
     if constexpr (HM)
         if (a.hsub_out) a.hsub[toff[(uint64_t)vi * a.S + L] + rankP] = fmaxf(out, hch);
+}
+
+// The rest of a queued set's gathers (the keys the rules did not read), then
+// either the walk queue or, when the walk closure shows the walk cannot reach
+// a key >= -ts, the store it would make.  toffv: this variable's slab offsets.
+template <int L, int PHASE, int V, class BS>
+__device__ __forceinline__ void walk_or_store(const ScoreArgs &a, BS &present, BS &hib, const LocalSet<L> &ls,
+                                              float tk, const uint32_t *binom, bool zk, const uint64_t *toffv,
+                                              uint64_t seg, uint64_t sk, float hch) {
+    constexpr int W = BS::kWords;
+#ifndef ULG_PROBE_NOPART2
+    gather_keys<L, PHASE, V, BS, LdPlain, 2>(present, hib, ls, -tk, binom, zk, a.table, toffv);
+#endif
+    // no key >= -ts among the nodes the walk can test: it would store P
+    // (80 % of the walked sets at C3's layer 6 end stored)
+    bool may_hit = true;
+    if constexpr (W < 4) {
+        uint64_t pw[W], hw[W];
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            pw[j] = present.word(j);
+            hw[j] = hib.word(j);
+        }
+        may_hit = walk_may_hit<L, PHASE, W>(pw, hw);
+    }
+    if (may_hit) {
+#ifndef ULG_PROBE_NOQUEUE
+        queue_walk(present, hib, a.queue + seg * kSegEntries * (uint64_t)(1 + 2 * W), a.qcount + seg * kSegStride,
+                   a.err, sk, tk);
+#endif
+        if (a.hsub_out) a.hsub[sk] = hch;  // the walk raises it to -ts if it stores P
+    } else {
+        a.table[sk] = -tk;
+        if (a.hsub_out) a.hsub[sk] = fmaxf(-tk, hch);
+    }
 }
 
 // PHASE 0: sets containing variable 0; 1: the rest.  V = variant bits (see
@@ -596,7 +647,10 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         float *ets = reinterpret_cast<float *>(eslot + kBlock);
         float *ehch = ets + kBlock;
         int *evi = reinterpret_cast<int *>(ehch + kBlock);
-        if (threadIdx.x == 0) *cnt = 0u;
+        if (threadIdx.x == 0) {
+            cnt[0] = 0u;
+            cnt[1] = 0u;  // the second compaction's count (variant bit 7)
+        }
         __syncthreads();
         if (valid && need) {
             const unsigned int k = atomicAdd(cnt, 1u);
@@ -611,77 +665,103 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
 #endif
         }
         __syncthreads();
-        if (threadIdx.x >= *cnt) return;
-        const int k = threadIdx.x;
-        const uint64_t seg = walk_segment();
-        const int vk = evi[k] & 0xff;
-#ifdef ULG_GATHER_STATS
-        const uint32_t hk = (uint32_t)evi[k] >> 8;  // hotA | hotZ << 8
-#endif
-        const bool zk = smeta[vk * 4 + 2] != 0;
-        const float tk = ets[k];
-        const uint64_t sk = eslot[k];
         constexpr int W = bits_words(L);
         using BS = std::conditional_t<(W >= 4), BitsLds<W>, Bits<W>>;
+        constexpr bool CMP2 = (V & 128) != 0 && W < 4;
+        if constexpr (!CMP2)
+            if (threadIdx.x >= *cnt) return;
+        const int k = threadIdx.x;
+        const bool a1 = threadIdx.x < cnt[0];
+        const uint64_t seg = walk_segment();
+        // this lane's compacted set (the lanes past the count, variant bit 7
+        // only, carry a dummy and gather nothing)
+        const int vk = a1 ? evi[k] & 0xff : 0;
+#ifdef ULG_GATHER_STATS
+        const uint32_t hk = a1 ? (uint32_t)evi[k] >> 8 : 0u;  // hotA | hotZ << 8
+#endif
+        const bool zk = smeta[vk * 4 + 2] != 0;
+        const float tk = a1 ? ets[k] : -1.0f;
+        const uint64_t sk = a1 ? eslot[k] : 0u;
+        const uint64_t cmk = a1 ? ecm[k] : 1ull;
+        const float hk1 = a1 ? ehch[k] : absent_f();
         uint64_t *lds_bits = reinterpret_cast<uint64_t *>(smem + lay.bits) + threadIdx.x;
-        const LocalSet<L> ls = local_set<L>(ecm[k], zk);
+        const LocalSet<L> ls = local_set<L>(cmk, zk);
         BS present = make_bits<BS>(lds_bits);
         BS hib = make_bits<BS>(lds_bits + (size_t)W * kBlock);
         present.clear();
         hib.clear();
-        // the keys the two-level rules read first; the rest only for the sets
-        // the rules leave to the walk (the subset maxima already showed a
-        // key >= -ts is present, so the rules need no "any key" test)
+        bool q = false;
+        if (a1) {
+            // the keys the two-level rules read first; the rest only for the
+            // sets the rules leave to the walk (the subset maxima already
+            // showed a key >= -ts is present, so the rules need no "any key"
+            // test)
 #ifndef ULG_PROBE_NOPART1
-        gather_keys<L, PHASE, V, BS, LdPlain, 1>(present, hib, ls, -tk, binom, zk, a.table, toff + (uint64_t)vk * a.S);
-#endif
-        bool q;
-#ifndef ULG_PROBE_NORULES
-        const bool dom = settle_rules<L, PHASE, BS, true>(present, hib, ls, q);
-#else
-        const bool dom = false;
-        q = false;
-#endif
-#ifdef ULG_GATHER_STATS
-        if constexpr (W < 4) {
-            BS p2 = make_bits<BS>(lds_bits), h2 = make_bits<BS>(lds_bits);
-            p2.clear();
-            h2.clear();
-            gather_keys<L, PHASE, V, BS, LdPlain, 0>(p2, h2, ls, -tk, binom, zk, a.table, toff + (uint64_t)vk * a.S);
-            gather_stats<L, PHASE>(p2, h2, hk & 0xffu, hk >> 8, zk, q);
-        }
-#endif
-        if (q) {
-#ifndef ULG_PROBE_NOPART2
-            gather_keys<L, PHASE, V, BS, LdPlain, 2>(present, hib, ls, -tk, binom, zk, a.table,
+            gather_keys<L, PHASE, V, BS, LdPlain, 1>(present, hib, ls, -tk, binom, zk, a.table,
                                                     toff + (uint64_t)vk * a.S);
 #endif
-            // no key >= -ts among the nodes the walk can test: it would store P
-            // (80 % of the walked sets at C3's layer 6 end stored)
-            bool may_hit = true;
+#ifndef ULG_PROBE_NORULES
+            const bool dom = settle_rules<L, PHASE, BS, true>(present, hib, ls, q);
+#else
+            const bool dom = false;
+            q = false;
+#endif
+#ifdef ULG_GATHER_STATS
             if constexpr (W < 4) {
-                uint64_t pw[W], hw[W];
+                BS p2 = make_bits<BS>(lds_bits), h2 = make_bits<BS>(lds_bits);
+                p2.clear();
+                h2.clear();
+                gather_keys<L, PHASE, V, BS, LdPlain, 0>(p2, h2, ls, -tk, binom, zk, a.table,
+                                                        toff + (uint64_t)vk * a.S);
+                gather_stats<L, PHASE>(p2, h2, hk & 0xffu, hk >> 8, zk, q);
+            }
+#endif
+            if (!q) {
+                const float o = dom ? absent_f() : -tk;
+                a.table[sk] = o;
+                if (a.hsub_out) a.hsub[sk] = fmaxf(o, hk1);
+            }
+        }
+        if constexpr (CMP2) {
+            // 3. the sets the rules leave to the walk (about a third of the
+            //    compacted ones) compacted once more, with their gathered
+            //    words, so the rest of the gathers, the walk closure and the
+            //    queue run on dense waves: at ~30 % of the lanes every wave
+            //    would still issue them
+            uint64_t *c2w = reinterpret_cast<uint64_t *>(smem + lay.cmp2);  // [2W][kBlock]
+            __syncthreads();  // every lane has read its first entry
+            if (q) {
+                const unsigned int k2 = atomicAdd(cnt + 1, 1u);
+                ecm[k2] = cmk;
+                eslot[k2] = (uint32_t)sk;
+                ets[k2] = tk;
+                ehch[k2] = hk1;
+                evi[k2] = vk;
 #pragma unroll
                 for (int j = 0; j < W; ++j) {
-                    pw[j] = present.word(j);
-                    hw[j] = hib.word(j);
+                    c2w[j * kBlock + k2] = present.word(j);
+                    c2w[(W + j) * kBlock + k2] = hib.word(j);
                 }
-                may_hit = walk_may_hit<L, PHASE, W>(pw, hw);
             }
-            if (may_hit) {
-#ifndef ULG_PROBE_NOQUEUE
-                queue_walk(present, hib, a.queue + seg * kSegEntries * (uint64_t)(1 + 2 * W),
-                           a.qcount + seg * kSegStride, sk, tk);
-#endif
-                if (a.hsub_out) a.hsub[sk] = ehch[k];  // the walk raises it to -ts if it stores P
-            } else {
-                a.table[sk] = -tk;
-                if (a.hsub_out) a.hsub[sk] = fmaxf(-tk, ehch[k]);
+            __syncthreads();
+            if (threadIdx.x >= cnt[1]) return;
+            const int vq = evi[k];
+            const bool zq = smeta[vq * 4 + 2] != 0;
+            const float tq = ets[k];
+            const uint64_t sq = eslot[k];
+            const float hq = ehch[k];
+            const LocalSet<L> lq = local_set<L>(ecm[k], zq);
+            BS pq = make_bits<BS>(lds_bits), hq_bits = make_bits<BS>(lds_bits);
+#pragma unroll
+            for (int j = 0; j < W; ++j) {
+                pq.w[j] = c2w[j * kBlock + k];
+                hq_bits.w[j] = c2w[(W + j) * kBlock + k];
             }
+            walk_or_store<L, PHASE, V, BS>(a, pq, hq_bits, lq, tq, binom, zq, toff + (uint64_t)vq * a.S, seg, sq, hq);
         } else {
-            const float o = dom ? absent_f() : -tk;
-            a.table[sk] = o;
-            if (a.hsub_out) a.hsub[sk] = fmaxf(o, ehch[k]);
+            if (q)
+                walk_or_store<L, PHASE, V, BS>(a, present, hib, ls, tk, binom, zk, toff + (uint64_t)vk * a.S, seg, sk,
+                                               hk1);
         }
         return;
     }
@@ -795,13 +875,17 @@ __device__ __forceinline__ uint32_t walk_load(const uint64_t *queue, uint64_t qn
 // subset maxima raised to -ts when stored (variant bit 6).
 template <int K>
 __device__ __forceinline__ void walk_store(const uint64_t *queue, uint64_t qn, uint64_t mine, int W, uint32_t dom,
-                                           float *table, float *hsub) {
+                                           float *table, float *hsub, uint64_t nslots, unsigned long long *err) {
 #pragma nounroll
     for (int k = 0; k < K; ++k) {
         if (mine + k >= qn) break;
         const uint64_t e0 = queue[(mine + k) * (uint64_t)(1 + 2 * W)];
         const float ts = __uint_as_float((uint32_t)(e0 >> 32));
         const bool d = (dom >> k) & 1u;
+        if ((uint32_t)e0 >= nslots) {  // an entry no scoring lane wrote
+            atomicOr(err, kErrSlot);
+            continue;
+        }
         table[(uint32_t)e0] = d ? absent_f() : -ts;
         if (hsub && !d) hsub[(uint32_t)e0] = fmaxf(hsub[(uint32_t)e0], -ts);
     }
@@ -814,14 +898,16 @@ __device__ __forceinline__ void walk_store(const uint64_t *queue, uint64_t qn, u
 // dispatch delayed the last busy waves (the layer-6 walk's span 220 -> 427 us).
 template <int L, int PHASE, int K>
 __global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, const unsigned long long *qcount,
-                                                         float *table, float *hsub, uint64_t *wclock) {
+                                                         float *table, float *hsub, uint64_t *wclock, uint64_t nslots,
+                                                         unsigned long long *err) {
     using S = Sliced<L, K>;
     const uint64_t t_start = wclock ? wall_clock64() : 0;
     constexpr int W = bits_words(L);
     constexpr uint32_t kChunks = (uint32_t)((kSegEntries + 64 * K - 1) / (64 * K));
     const uint32_t nseg = gridDim.x / kChunks;
     const uint32_t seg = blockIdx.x % nseg;
-    const uint64_t qn = qcount[(uint64_t)seg * kSegStride];
+    const uint64_t qc = qcount[(uint64_t)seg * kSegStride];
+    const uint64_t qn = qc < kSegEntries ? qc : kSegEntries;  // past it: kErrQueue is set
     const uint64_t first = (uint64_t)(blockIdx.x / nseg) * 64 * S::K;
     if (first >= qn) return;
     queue += (uint64_t)seg * kSegEntries * (uint64_t)(1 + 2 * W);
@@ -850,7 +936,153 @@ __global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, 
         wclock[3 * blockIdx.x + 1] = wall_clock64();
         wclock[3 * blockIdx.x + 2] = pts;
     }
-    walk_store<S::K>(queue, qn, mine, W, dom, table, hsub);
+    walk_store<S::K>(queue, qn, mine, W, dom, table, hsub, nslots, err);
+}
+
+// ---- per-lane walk (round 6, option walk_lane) -------------------------------
+// One queued set per lane, find_best_subset_score's recursion (walk_sliced's
+// order, no-op re-tests skipped) run as an explicit state machine: each
+// iteration a lane may return from a call (RET: pop its caller's frame, clear
+// `checked` for the node it expanded), start the next call of an expansion
+// (CALL: append the next list entry, push its frame) and test one node
+// (TEST).  Lanes walk independently, so a wave takes as many iterations as
+// its longest single walk instead of the union tree of its 256-512 sets'
+// walks: at C3's layer 6 without variable 0 the longest single walk tests 248
+// nodes where a wave's union tree tested up to 811 (walk_sched_study.cpp
+// replays the dumped queues both ways, with identical decisions).  The
+// frames of a lane's callers live in LDS ([depth][lane], 12 B); the current
+// frame, the hi and open bits are registers.
+constexpr int kLaneWaves = 4096;  // resident waves of a walk_lane launch (a grid-stride loop over the chunks)
+
+template <int W>
+__device__ __forceinline__ bool lane_bit(const uint64_t (&w)[W], uint32_t t) {
+    uint64_t x = w[0];
+#pragma unroll
+    for (int j = 1; j < W; ++j) x = (t >> 6) == (uint32_t)j ? w[j] : x;
+    return (x >> (t & 63u)) & 1ull;
+}
+template <int W>
+__device__ __forceinline__ void lane_clear(uint64_t (&w)[W], uint32_t t) {
+    const uint64_t m = ~(1ull << (t & 63u));
+#pragma unroll
+    for (int j = 0; j < W; ++j) w[j] &= (t >> 6) == (uint32_t)j ? m : ~0ull;
+}
+
+template <int L, int PHASE>
+__global__ void __launch_bounds__(64) walk_lane_kernel(const uint64_t *queue, const unsigned long long *qcount,
+                                                       float *table, float *hsub, uint64_t nslots,
+                                                       unsigned long long *err, uint32_t nseg) {
+    constexpr int W = bits_words(L);
+    constexpr uint32_t kChunks = (uint32_t)(kSegEntries / 64);
+    __shared__ uint32_t fr[L][3][64];  // the callers' frames: [depth][word][lane]
+    const int lane = threadIdx.x;
+    constexpr bool v0inP = PHASE == 0;
+    constexpr uint32_t Proot = v0inP ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
+    constexpr uint32_t pvroot = [] {
+        uint32_t p = 0;
+        for (int i = 0; i < L; ++i) p |= (uint32_t)(i + (v0inP ? 0 : 1)) << (4 * i);
+        return p;
+    }();
+    const uint64_t items = (uint64_t)nseg * kChunks;
+    for (uint64_t item = blockIdx.x; item < items; item += gridDim.x) {
+        const uint32_t seg = (uint32_t)(item % nseg);  // chunk-major: the busy chunks come first
+        const uint64_t first = (item / nseg) * 64;
+        const uint64_t qc = qcount[(uint64_t)seg * kSegStride];
+        const uint64_t qn = qc < kSegEntries ? qc : kSegEntries;  // past it: kErrQueue is set
+        if (first >= qn) continue;
+        const uint64_t mine = first + (uint64_t)lane;
+        const bool valid = mine < qn;
+        const uint64_t *e = queue + ((uint64_t)seg * kSegEntries + (valid ? mine : first)) * (uint64_t)(1 + 2 * W);
+        const uint64_t e0 = e[0];
+        uint64_t hiw[W], ow[W];
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            hiw[j] = e[1 + j];
+            ow[j] = e[1 + W + j];
+        }
+        // the current frame
+        uint32_t T = Proot, pv = pvroot, idx = 0, hend = L, u = 0, i = 0, j = 0, npv = 0;
+        int d = 0;
+        int state = 0;  // 0 TEST, 1 CALL, 2 RET
+        bool done = !valid, dom = false;
+        while (__ballot(!done) != 0ull) {
+            if (!done && state == 2) {
+                if (d == 0) {
+                    done = true;  // exhausted: no key >= -ts visited, P is stored
+                } else {
+                    lane_clear<W>(ow, T);  // checked.insert(T2) in the caller
+                    --d;
+                    const uint32_t w0 = fr[d][0][lane], w1 = fr[d][1][lane], w2 = fr[d][2][lane];
+                    pv = w0 & 0xFFFFFFu;
+                    idx = (w0 >> 24) & 7u;
+                    hend = w0 >> 27;
+                    npv = w1 & 0xFFFFFFu;
+                    i = (w1 >> 24) & 7u;
+                    j = w1 >> 27;
+                    T = w2 & 0xFFu;
+                    u = w2 >> 8;
+                    state = 1;
+                }
+            }
+            if (!done && state == 1) {
+                // the next list entry that is not u (an entry equal to u is
+                // skipped: the zero padding when u is variable 0)
+                const uint32_t M = (uint32_t)(L - d);
+                const uint32_t x = pv ^ (u * 0x111111u);
+                uint32_t nz = (x | (x >> 1) | (x >> 2) | (x >> 3)) & 0x111111u;
+                nz &= (0x111111u << (4 * i)) & ((1u << (4 * M)) - 1u);
+                if (nz == 0u) {
+                    ++idx;  // every call of the expansion made
+                    state = 0;
+                } else {
+                    const uint32_t ii = (uint32_t)__builtin_ctz(nz) >> 2;
+                    npv |= ((pv >> (4 * ii)) & 15u) << (4 * j);
+                    ++j;
+                    i = ii + 1;
+                    fr[d][0][lane] = pv | (idx << 24) | (hend << 27);
+                    fr[d][1][lane] = npv | (i << 24) | (j << 27);
+                    fr[d][2][lane] = T | (u << 8);
+                    ++d;
+                    T ^= 1u << u;
+                    pv = npv;
+                    const uint32_t Mc = M - 1;
+                    idx = j == 1 ? 0u : j - 1;
+                    hend = j == 1 ? (Mc < 2 ? Mc : 2u) : j;
+                    state = 0;
+                }
+            }
+            if (!done && state == 0) {
+                if (idx >= hend) {
+                    state = 2;
+                } else {
+                    const uint32_t u2 = (pv >> (4 * idx)) & 15u;
+                    const uint32_t T2 = T ^ (1u << u2);
+                    if (lane_bit<W>(hiw, T2)) {
+                        dom = true;  // a key >= -ts: find_best_subset_score returns >= -ts, P is pruned
+                        done = true;
+                    } else if (d < L - 1 && lane_bit<W>(ow, T2)) {
+                        u = u2;
+                        i = 0;
+                        j = 0;
+                        npv = 0;
+                        state = 1;
+                    } else {
+                        ++idx;
+                    }
+                }
+            }
+        }
+        if (valid) {
+            const float ts = __uint_as_float((uint32_t)(e0 >> 32));
+            const uint32_t slot = (uint32_t)e0;
+            if (slot >= nslots) {
+                atomicOr(err, kErrSlot);
+            } else {
+                table[slot] = dom ? absent_f() : -ts;
+                if (hsub && !dom) hsub[slot] = fmaxf(hsub[slot], -ts);
+            }
+        }
+    }
 }
 
 // ---- wide layers (kMaxL < L <= kWideMax) ------------------------------------
@@ -1684,7 +1916,10 @@ __global__ void __launch_bounds__(kBlock) count_kernel(const float *table, uint6
 // *total (the lists' end offset, offsets[nv]); one block: each thread sums
 // its run of counts, a shuffle scan per wave and one over the 16 wave
 // totals (two barriers; the Hillis-Steele form took 20, 10.6 us at C3)
-__global__ void __launch_bounds__(1024) scan_kernel(uint64_t *blk, int64_t nb, int64_t *total) {
+// blk[nb + 1]: a copy of the call's error word (0 without one), so one copy
+// brings the stored count and the error bits to the host
+__global__ void __launch_bounds__(1024) scan_kernel(uint64_t *blk, int64_t nb, int64_t *total,
+                                                    const unsigned long long *err) {
     __shared__ unsigned long long wsum[16];
     const int64_t per = (nb + 1023) / 1024;
     const int64_t b0 = threadIdx.x * per, b1 = b0 + per < nb ? b0 + per : nb;
@@ -1710,6 +1945,7 @@ __global__ void __launch_bounds__(1024) scan_kernel(uint64_t *blk, int64_t nb, i
         if (lane < 16) wsum[lane] = wi - w;
         if (lane == 15) {
             blk[nb] = wi;
+            blk[nb + 1] = err ? *err : 0ull;
             *total = (int64_t)wi;
         }
     }
@@ -1910,10 +2146,12 @@ KernelFn pick(int phase, int variant) {
         case 49: return pick_phase<L, 17>(phase);
         case 65: return pick_phase<L, 65>(phase);
         case 113: return pick_phase<L, 81>(phase);
+        case 241: return pick_phase<L, 209>(phase);
         default: return nullptr;
     }
 }
-using SlicedFn = void (*)(const uint64_t *, const unsigned long long *, float *, float *, uint64_t *);
+using SlicedFn = void (*)(const uint64_t *, const unsigned long long *, float *, float *, uint64_t *, uint64_t,
+                         unsigned long long *);
 template <int L, int K>
 SlicedFn sliced_pick(int phase) {
     return phase == 0 ? walk_sliced_kernel<L, 0, K> : walk_sliced_kernel<L, 1, K>;
@@ -1973,6 +2211,24 @@ SlicedFn sliced_fn(int L, int phase, int k) {
         case 2: return sliced_fn_k<2>(L, phase);
         case 4: return sliced_fn_k<4>(L, phase);
         default: return sliced_fn_k<8>(L, phase);
+    }
+}
+
+using LaneFn = void (*)(const uint64_t *, const unsigned long long *, float *, float *, uint64_t, unsigned long long *,
+                       uint32_t);
+template <int L>
+LaneFn lane_pick(int phase) {
+    return phase == 0 ? walk_lane_kernel<L, 0> : walk_lane_kernel<L, 1>;
+}
+LaneFn lane_fn(int L, int phase) {
+    switch (L) {
+        case 1: return lane_pick<1>(phase);
+        case 2: return lane_pick<2>(phase);
+        case 3: return lane_pick<3>(phase);
+        case 4: return lane_pick<4>(phase);
+        case 5: return lane_pick<5>(phase);
+        case 6: return lane_pick<6>(phase);
+        default: return nullptr;
     }
 }
 
@@ -2533,6 +2789,62 @@ static int dump_walk_clock(ulg_ctx *c, hipStream_t st, uint64_t sb, const char *
     return ULG_OK;
 }
 
+// Diagnostics (ULG_WALK_CLOCK with ULG_WALK_QUEUE_DUMP, after a layer's walk
+// launch): the walk queue of that launch, compacted, with each entry's
+// decision as the walk left it in the table -- scripts/walk_sched_study.cpp
+// replays the walks offline.  File: nseg, W, then per segment its count,
+// count x (1 + 2W) entry words and count decision words (the table's bits at
+// the entry's slot).
+static int dump_walk_queue(ulg_ctx *c, hipStream_t st, const uint64_t *queue, const unsigned long long *qc,
+                           uint64_t nseg, int W, uint64_t nslots, const char *dir, int L, int ph) {
+    std::vector<unsigned long long> cnt(nseg * kSegStride);
+    ULG_HIP(c, hipMemcpyAsync(cnt.data(), qc, cnt.size() * 8, hipMemcpyDeviceToHost, st));
+    ULG_HIP(c, hipStreamSynchronize(st));
+    char fn[512];
+    std::snprintf(fn, sizeof fn, "%s/queue_L%d_p%d.bin", dir, L, ph);
+    FILE *f = std::fopen(fn, "wb");
+    if (!f) return ULG_OK;
+    const uint64_t hdr[2] = {nseg, (uint64_t)W};
+    std::fwrite(hdr, 8, 2, f);
+    const uint64_t ew = 1 + 2 * (uint64_t)W;
+    std::vector<uint32_t> tab((size_t)nslots);
+    ULG_HIP(c, hipMemcpyAsync(tab.data(), reinterpret_cast<const uint32_t *>(c->table.p), tab.size() * 4,
+                              hipMemcpyDeviceToHost, st));
+    ULG_HIP(c, hipStreamSynchronize(st));
+    for (uint64_t s = 0; s < nseg; ++s) {
+        const uint64_t n = std::min<uint64_t>(cnt[s * kSegStride], kSegEntries);
+        std::vector<uint64_t> e(n * ew);
+        std::vector<uint32_t> d(n);
+        if (n) {
+            ULG_HIP(c, hipMemcpyAsync(e.data(), queue + s * kSegEntries * ew, e.size() * 8, hipMemcpyDeviceToHost, st));
+            ULG_HIP(c, hipStreamSynchronize(st));
+            for (uint64_t i = 0; i < n; ++i) {
+                const uint32_t slot = (uint32_t)e[i * ew];
+                d[i] = slot < tab.size() ? tab[slot] : 0u;
+            }
+        }
+        std::fwrite(&n, 8, 1, f);
+        std::fwrite(e.data(), 8, e.size(), f);
+        std::fwrite(d.data(), 4, d.size(), f);
+    }
+    std::fclose(f);
+    return ULG_OK;
+}
+
+// The call's error word (kErr* bits) as a status.
+static int call_error(ulg_ctx *c, unsigned long long w) {
+    c->last_err_word = w;
+    if (w & kErrWide)
+        return set_err(c, ULG_ERR_UNSUPPORTED,
+                       "ulg_cbic_score: a find_best_subset_score walk in a wide layer exceeded its cap (2^30 steps "
+                       "in walk_wide_kernel, 2^32 iterations or 24 frames in the LDS / host replay)");
+    if (w & (kErrQueue | kErrSlot))
+        return set_err(c, ULG_ERR_STATE,
+                       (w & kErrQueue) ? "ulg_cbic_score: a walk-queue segment overflowed (internal sizing error)"
+                                       : "ulg_cbic_score: a walk entry named a slot past the call's table");
+    return ULG_OK;
+}
+
 int ulg_cbic_score_finish(ulg_ctx *c, int64_t *total_stored, int64_t *total_scored) {
     if (!c) return ULG_ERR_ARG;
     if (c->async_pending) {
@@ -2540,7 +2852,12 @@ int ulg_cbic_score_finish(ulg_ctx *c, int64_t *total_stored, int64_t *total_scor
         ULG_HIP(c, hipSetDevice(c->device));
         ULG_HIP(c, hipStreamSynchronize(c->stream));
         prof_collect(c);
-        c->total_stored = (int64_t)*c->async_pinned;
+        c->total_stored = (int64_t)c->async_pinned[0];
+        c->last_err_word = c->async_pinned[1];
+        if (int rc = call_error(c, c->async_pinned[1])) {
+            c->scored = false;
+            return rc;
+        }
     }
     if (!c->scored) return set_err(c, ULG_ERR_STATE, "ulg_cbic_score_finish: nothing scored");
     if (total_stored) *total_stored = c->total_stored;
@@ -2647,6 +2964,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     sa.hsub = nullptr;
     sa.queue = nullptr;
     sa.qcount = nullptr;
+    sa.err = nullptr;
     sa.N = (double)c->N;
     sa.lambda = c->lambda;
     sa.n = n;
@@ -2730,6 +3048,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     // zeroed by call_prologue_kernel (the first launch of the sequence below)
     const bool zero_q = (variant & 16) || kmax > kMaxL;
     const uint64_t nqseg = zero_q ? std::max<uint64_t>(segoff.back(), 1) : 0;
+    sa.err = zero_q ? c->d_qcount.p + nqc - 1 : nullptr;
     // wide-layer walks: one checked-bitset slice per stream group, allocated
     // before any launch (2^q bits per walking set, q <= kmax + 1)
     uint64_t wslice = 0;
@@ -2773,7 +3092,9 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     const int Ls = (variant & 16) && !wck ? std::min(kmax, std::min(kMaxL, c->score_small_layers)) : 0;
     const int vsmall = variant & 65;  // the one-pass form (keeping the subset maxima under bit 6)
     // ... of which layers <= Lf in one launch, a workgroup per variable
-    const int Lf = vsmall == 65 ? std::min(Ls, c->score_fused) : 0;
+    // (not under -r: the budget is checked after every layer, and a fused
+    // launch would finish layers 2..Lf before the first check)
+    const int Lf = vsmall == 65 && c->time_limit_ms == 0 ? std::min(Ls, c->score_fused) : 0;
     bool forked = false;
     // The wide layers variable by variable (wide_pool 1) pay when the
     // variables that reach them differ in size: the long replays of one then
@@ -2797,7 +3118,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     c->out_of_time = 0;
     int done_L = kmax;
     const int64_t nb = (int64_t)((total_slots + kSlotsPerBlock - 1) / kSlotsPerBlock);
-    if ((rc = ensure(c, c->d_blk, (size_t)nb + 1))) return rc;
+    if ((rc = ensure(c, c->d_blk, (size_t)nb + 2))) return rc;
     // The launch sequence from here to write_kernel has no host sync when
     // every layer is unrolled and no budget / diagnostic is on, and it is the
     // same on every call with the same variables, limits and buffers: it is
@@ -2825,7 +3146,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     if (use_graph) {
         gkey.assign({(uint64_t)nv, (uint64_t)max_parents, (uint64_t)variant, (uint64_t)G, (uint64_t)Ls,
                      (uint64_t)c->score_xcd, (uint64_t)n, (uint64_t)c->N, dbits(c->lambda), (uint64_t)c->prof,
-                     (uint64_t)c->walk_small_sets, (uint64_t)c->walk_k6,
+                     (uint64_t)c->walk_small_sets, (uint64_t)c->walk_k6, (uint64_t)c->walk_lane,
                      (uint64_t)(uintptr_t)c->table.p, (uint64_t)(uintptr_t)c->d_work.p,
                      (uint64_t)(uintptr_t)c->d_workg.p, (uint64_t)(uintptr_t)c->d_queue.p,
                      (uint64_t)(uintptr_t)c->d_qcount.p, (uint64_t)(uintptr_t)c->d_qseg.p, (uint64_t)(uintptr_t)c->d_cand.p,
@@ -2958,7 +3279,18 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                 if (variant & 16) {
                     // the undecided lanes of this launch, densely packed
                     const int wk = sliced_k(L, cnt, (uint64_t)c->walk_small_sets, c->walk_k6);
-                    if ((variant & 32) && sliced_fn(L, ph, wk)) {
+                    if ((variant & 32) && c->walk_lane && !wck && lane_fn(L, ph)) {
+                        // one set per lane: 64-entry chunks, a grid-stride loop of
+                        // at most kLaneWaves waves
+                        const uint64_t nseg = seg_count(blocks);
+                        const uint64_t items = nseg * (kSegEntries / 64);
+                        const uint64_t lb = std::min<uint64_t>(items, (uint64_t)kLaneWaves);
+                        prof_begin_s(c, kWalkNames[ph][L], st);
+                        hipLaunchKernelGGL(lane_fn(L, ph), dim3((unsigned)lb), dim3(64), 0, st, sa.queue, qc,
+                                           c->table.p, sa.hsub_out ? sa.hsub : nullptr, total_slots, sa.err,
+                                           (uint32_t)nseg);
+                        prof_end_s(c, st);
+                    } else if ((variant & 32) && sliced_fn(L, ph, wk)) {
                         // one wave per (queue segment, chunk of 64 * K entries)
                         const int kk = L == 7 ? 2 : (L == 8 ? 1 : wk);
                         const uint64_t per = 64ull * (uint64_t)kk;
@@ -2967,9 +3299,14 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                         if (wck) ULG_HIP(c, hipMemsetAsync(c->d_dump.p, 0, 24 * sb, st));
                         prof_begin_s(c, kWalkNames[ph][L], st);
                         hipLaunchKernelGGL(sliced_fn(L, ph, wk), dim3((unsigned)sb), dim3(64), 0, st, sa.queue, qc,
-                                           c->table.p, sa.hsub_out ? sa.hsub : nullptr, wck ? c->d_dump.p : nullptr);
+                                           c->table.p, sa.hsub_out ? sa.hsub : nullptr, wck ? c->d_dump.p : nullptr,
+                                           total_slots, sa.err);
                         prof_end_s(c, st);
                         if (wck && (rc = dump_walk_clock(c, st, sb, wck, L, ph))) return rc;
+                        if (wck && std::getenv("ULG_WALK_QUEUE_DUMP") &&
+                            (rc = dump_walk_queue(c, st, sa.queue, qc, seg_count(blocks), bits_words(L), total_slots, wck, L,
+                                                  ph)))
+                            return rc;
                     }
                 }
             }
@@ -3011,7 +3348,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     count_kernel<<<(unsigned)nb, kBlock, 0, c->stream>>>(c->table.p, total_slots, c->d_blk.p);
     prof_end(c);
     prof_begin(c, "scan_stored");
-    scan_kernel<<<1, 1024, 0, c->stream>>>(c->d_blk.p, nb, c->out_offsets.p + nv);
+    scan_kernel<<<1, 1024, 0, c->stream>>>(c->d_blk.p, nb, c->out_offsets.p + nv, sa.err);
     prof_end(c);
     WriteArgs wa;
     wa.table = c->table.p;
@@ -3051,8 +3388,8 @@ launched:
         // no host sync on this path: the stored count is copied into pinned
         // memory behind the launches and collected by ulg_cbic_score_finish
         if (!c->async_pinned)
-            ULG_HIP(c, hipHostMalloc((void **)&c->async_pinned, sizeof(unsigned long long), hipHostMallocDefault));
-        ULG_HIP(c, hipMemcpyAsync(c->async_pinned, c->d_blk.p + nb, 8, hipMemcpyDeviceToHost, c->stream));
+            ULG_HIP(c, hipHostMalloc((void **)&c->async_pinned, 2 * sizeof(unsigned long long), hipHostMallocDefault));
+        ULG_HIP(c, hipMemcpyAsync(c->async_pinned, c->d_blk.p + nb, 16, hipMemcpyDeviceToHost, c->stream));
         c->nv = nv;
         c->kmax = kmax;
         c->vars.assign(vars, vars + nv);
@@ -3065,20 +3402,15 @@ launched:
         c->async_pending = true;
         return ULG_OK;
     }
-    unsigned long long wide_err = 0;
-    // the stored count through the context's pinned word (a pageable
-    // destination goes through a staging copy)
+    // the stored count and the error word through the context's pinned words
+    // (a pageable destination goes through a staging copy)
     if (!c->async_pinned)
-        ULG_HIP(c, hipHostMalloc((void **)&c->async_pinned, sizeof(unsigned long long), hipHostMallocDefault));
-    ULG_HIP(c, hipMemcpyAsync(c->async_pinned, c->d_blk.p + nb, 8, hipMemcpyDeviceToHost, c->stream));
-    if (kmax > kMaxL) ULG_HIP(c, hipMemcpyAsync(&wide_err, c->d_qcount.p + nqc - 1, 8, hipMemcpyDeviceToHost, c->stream));
+        ULG_HIP(c, hipHostMalloc((void **)&c->async_pinned, 2 * sizeof(unsigned long long), hipHostMallocDefault));
+    ULG_HIP(c, hipMemcpyAsync(c->async_pinned, c->d_blk.p + nb, 16, hipMemcpyDeviceToHost, c->stream));
     ULG_HIP(c, hipStreamSynchronize(c->stream));
-    const uint64_t stored = *c->async_pinned;
+    const uint64_t stored = c->async_pinned[0];
     prof_collect(c);
-    if (wide_err)
-        return set_err(c, ULG_ERR_UNSUPPORTED,
-                       "ulg_cbic_score: a find_best_subset_score walk in a wide layer exceeded its cap (2^30 steps "
-                       "in walk_wide_kernel, 2^32 iterations or 24 frames in the LDS / host replay)");
+    if ((rc = call_error(c, c->async_pinned[1]))) return rc;
 
     c->nv = nv;
     c->kmax = kmax;

@@ -538,8 +538,10 @@ __device__ __forceinline__ void child_ranks(uint64_t cm, const uint32_t *binom, 
 // (scripts/walk_closure_check.py checks the superset against the recursion).
 // Bit t of word t >> 6 is local subset t; root = P (and, phase 1, P + {0})
 // are never keys.
+// (__host__ too: host/walk_may_hit_check.cpp runs this very function against
+// scripts/walk_closure_check.py's restatement, tests/test_walk_closure.py)
 template <int L, int PHASE, int W>
-__device__ __forceinline__ bool walk_may_hit(const uint64_t (&pres)[W], const uint64_t (&hiw)[W]) {
+__host__ __device__ __forceinline__ bool walk_may_hit(const uint64_t (&pres)[W], const uint64_t (&hiw)[W]) {
     constexpr int Q = PHASE == 0 ? L : L + 1;
     constexpr uint32_t root = PHASE == 0 ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
     constexpr uint64_t kM[6] = {0xAAAAAAAAAAAAAAAAull, 0xCCCCCCCCCCCCCCCCull, 0xF0F0F0F0F0F0F0F0ull,

@@ -961,6 +961,36 @@ extern "C" int ulg_triplet_solve(ulg_ctx *c, const uint64_t *clusters, int64_t n
     return ULG_OK;
 }
 
+// Diagnostics (tests/test_gpu_triplet.py): one host PDB build of the look-ahead
+// pool's form (pdb_host) over `cluster`, with the pool's cancel flag preset
+// when cancel_preset != 0.  out[0] = built, out[1] = P.cancelled, out[2] =
+// entries built, out[3] = the entries equal to the device PDB's over the same
+// cluster (search_build_pdb, which the driver's own searches use).
+extern "C" int ulg_diag_pdb_host(ulg_ctx *c, uint64_t cluster, int pd_count, int cancel_preset, int64_t *out) {
+    if (!c || !out || pd_count < 1) return ULG_ERR_ARG;
+    if (!c->search || !c->search->lists_ready)
+        return set_err(c, ULG_ERR_STATE, "ulg_diag_pdb_host: no parent-set lists");
+    ULG_HIP(c, hipSetDevice(c->device));
+    SearchState &s = *c->search;
+    int rc;
+    if ((rc = search_ensure_scope(c, cluster)) || (rc = search_cost_table_host(c)) ||
+        (rc = search_build_pdb(c, pd_count, 0, cluster)))
+        return rc;
+    HostTables base;
+    host_tables(s, base);
+    HostPdb P;
+    std::atomic<bool> cancel{cancel_preset != 0};
+    const bool ok = pdb_host(base, cluster, pd_count, P, &cancel);
+    out[0] = ok;
+    out[1] = P.cancelled;
+    out[2] = ok && !P.cancelled ? (int64_t)P.pd.size() : 0;
+    int64_t same = 0;
+    if (ok && !P.cancelled && base.pd && P.pd_off == base.pd_off)
+        for (size_t i = 0; i < P.pd.size(); ++i) same += std::memcmp(&P.pd[i], base.pd + i, 4) == 0;
+    out[3] = same;
+    return ULG_OK;
+}
+
 // Seed the memo with other ranks' results (same lists, same pd_count).
 extern "C" int ulg_triplet_memo_put(ulg_ctx *c, const uint64_t *clusters, int64_t nc, int pd_count,
                                     const uint64_t *parents) {

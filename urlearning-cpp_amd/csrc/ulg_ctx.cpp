@@ -198,8 +198,8 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         return ULG_OK;
     }
     if (std::strcmp(name, "score_variant") == 0) {
-        if (value != 1 && value != 49 && value != 65 && value != 113)
-            return set_err(c, ULG_ERR_ARG, "score_variant must be 1, 49, 65 or 113");
+        if (value != 1 && value != 49 && value != 65 && value != 113 && value != 241)
+            return set_err(c, ULG_ERR_ARG, "score_variant must be 1, 49, 65, 113 or 241");
         c->score_variant = (int)value;
         return ULG_OK;
     }
@@ -222,6 +222,11 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         if (value != 1 && value != 2 && value != 4 && value != 8)
             return set_err(c, ULG_ERR_ARG, "walk_k6 must be 1, 2, 4 or 8");
         c->walk_k6 = (int)value;
+        return ULG_OK;
+    }
+    if (std::strcmp(name, "walk_lane") == 0) {
+        if (value != 0 && value != 1) return set_err(c, ULG_ERR_ARG, "walk_lane must be 0 or 1");
+        c->walk_lane = (int)value;
         return ULG_OK;
     }
     if (std::strcmp(name, "walk_small_sets") == 0) {
@@ -301,6 +306,12 @@ int ulg_get_info(ulg_ctx *c, const char *name, int64_t *value) {
     }
     if (std::strcmp(name, "highest_completed_layer") == 0) {
         *value = c->completed_layer;
+        return ULG_OK;
+    }
+    // the last scoring call's device error word: 0 unless a walk over its cap
+    // (1), a walk-queue segment overflow (2) or a walk entry past the table (4)
+    if (std::strcmp(name, "score_error_word") == 0) {
+        *value = (int64_t)c->last_err_word;
         return ULG_OK;
     }
     // the last exact A*'s host counters (user space, the calling thread; -1: not granted)

@@ -70,6 +70,7 @@ struct ulg_ctx {
     int64_t total_scored = 0;
     bool scored = false;
     int score_variant = 113;
+    int walk_lane = 0;  // layers <= 6: one queued set per lane (walk_lane_kernel) instead of the bit-sliced union walk
     int score_streams = 3;                  // scorer variable groups on concurrent streams
     int score_small_layers = 4;             // layers <= this run one-pass on one stream (two-pass variants)
     int score_fused = 3;                    // ... and layers <= this (<= small layers) in one launch, a workgroup per variable
@@ -143,7 +144,8 @@ struct ulg_ctx {
     unsigned long long *wide_pinned = nullptr;  // pinned queue / long-walk counts of the wide stages
     // ulg_cbic_score_async: the stored count lands here when the launches
     // finish; ulg_cbic_score_finish (or any later scorer call) collects it
-    unsigned long long *async_pinned = nullptr;
+    unsigned long long *async_pinned = nullptr;  // [stored count, error word] of the last call
+    unsigned long long last_err_word = 0;        // the last scoring call's error word (kErr* bits)
     bool async_pending = false;
     std::vector<unsigned long long> wide_host;
     std::map<std::string, std::vector<double>> prof_ms;

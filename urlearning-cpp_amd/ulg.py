@@ -72,6 +72,7 @@ def lib():
         L.ulg_profile_dump.argtypes = [P, C.c_char_p, I64]
         L.ulg_profile_reset.argtypes = [P]
         L.ulg_profile_select.argtypes = [P, C.c_char_p]
+        L.ulg_diag_pdb_host.argtypes = [P, C.c_uint64, I, I, P]
         _lib = L
     return _lib
 
@@ -371,9 +372,16 @@ class Context:
     def set_option(self, name: str, value: int):
         self._check(lib().ulg_set_option(self._h, name.encode(), int(value)), "ulg_set_option")
 
+    def diag_pdb_host(self, cluster: int, pd_count: int = 2, cancel_preset: bool = False):
+        """ulg_diag_pdb_host (tests): -> (built, cancelled, entries, entries equal to the device PDB's)."""
+        out = np.zeros(4, dtype=np.int64)
+        self._check(lib().ulg_diag_pdb_host(self._h, C.c_uint64(int(cluster)), int(pd_count), int(bool(cancel_preset)),
+                                            _ptr(out)), "ulg_diag_pdb_host")
+        return tuple(int(x) for x in out)
+
     def info(self, name: str) -> int:
-        """ulg_get_info: "out_of_time", "highest_completed_layer", "exact_cycles",
-        "exact_instructions", "exact_cache_misses"."""
+        """ulg_get_info: "out_of_time", "highest_completed_layer", "score_error_word",
+        "exact_cycles", "exact_instructions", "exact_cache_misses"."""
         v = C.c_int64()
         self._check(lib().ulg_get_info(self._h, name.encode(), C.byref(v)), "ulg_get_info")
         return v.value
