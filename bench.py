@@ -101,10 +101,9 @@ def cpu_baseline(cfg, X, target_s=15.0):
 
 
 PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r2")
-# the scorer's counter passes of this round's kernels (scripts/r5_probe.sh +
-# pmc_r5_summarize.py on the same bench command); the sweep's kernel is
-# unchanged since round 2
-PMC_SCORER = os.path.join(os.path.dirname(PROFILES), "r5", "pmc_scorer.json")
+# the scorer's counter passes of this round's kernels (scripts/gpu_probe.sh
+# step pmc_scorer + pmc_r5_summarize.py on the same bench command)
+PMC_SCORER = os.path.join(os.path.dirname(PROFILES), "r6", "pmc_scorer.json")
 
 
 def pmc_scorer(cfg, sets, label):
@@ -154,11 +153,13 @@ def roofline(ctx, cfg, per_layer_sets, steps):
              "traffic_source": os.path.relpath(PMC_SCORER, ROOT) if pmc else None,
              "l1_lines_per_set": pmc.get("l1_lines_per_set") if pmc else None,
              "ta_busy_frac": pmc.get("ta_busy_frac") if pmc else None,
+             "score_valu_per_wave": pmc.get("score", {}).get("valu_per_wave") if pmc else None,
+             "score_resident_waves_per_simd": pmc.get("score", {}).get("resident_waves_per_simd") if pmc else None,
              "pmc_kernels": pmc.get("kernels") if pmc else None,
              "pmc_note": ("what binds the pair is the vector memory pipeline, not HBM bytes: l1_lines_per_set = "
                           "TCP_TOTAL_CACHE_ACCESSES / sets (one tag lookup per distinct 128-B line per gather "
                           "instruction), ta_busy_frac = per-CU TA_TA_BUSY / kernel cycles of the scoring kernel "
-                          "(profiles/r5, scripts/pmc_r5_summarize.py)"),
+                          "(profiles/r6, scripts/pmc_r5_summarize.py)"),
              "kernel": name,
              "avg_launch_ms": p["avg_ms"], "avg_launch_ms_each": [q["avg_ms"] for q in ps],
              "launches": p["count"], "launches_per_step": groups, "sets_per_launch": sets,

@@ -292,18 +292,25 @@ int ulg_sweep_shard_end(ulg_ctx *ctx, uint64_t *vpar, int *order, float *goal_co
                         int64_t *expanded);
 
 /* ---- tuning knobs -------------------------------------------------------
- * "score_variant" (1, 49, 65, 113; default 113): bit 0 = fully
+ * "score_variant" (1, 49, 65, 113, 241; default 241): bit 0 = fully
  * unrolled presence gather (layers <= 6), bit 4 = two-pass layers (the
  * scoring kernel settles every set it can without a walk and queues the rest
  * for a dense walk kernel with the hi-cover prune), bit 5 = that walk
  * bit-sliced (64 x K sets per wave), bit 6 = subset maxima (a per-slot table
  * of the largest stored value below each set settles sets with 2L-3L reads
- * before the rest are compacted for the 2^(L+1) presence gathers).  1 and 65
- * are one-pass (every set decided in its lane).  All variants store
- * identical lists.
+ * before the rest are compacted for the 2^(L+1) presence gathers), bit 7 =
+ * the sets the two-level rules leave to the walk compacted once more before
+ * the rest of their gathers (round 6).  1 and 65 are one-pass (every set
+ * decided in its lane).  All variants store identical lists.
+ * "walk_bucket" (0 or 1; default 1, round 6): the layer-5 and layer-6 walk
+ * launches of the two-pass variants with subset maxima (113, 241) walk their
+ * queue sorted by walk key (which of the walk's first-level nodes a set may
+ * expand): sets with one key share more of their union walk (C3 layer 6
+ * without variable 0: its longest wave 811 -> ~465 union points, the
+ * launch's union points 3x fewer).  Identical lists either way.
  * "walk_small_sets" (>= 0, default 200000): a layer-6 launch of fewer sets
  * walks one set per lane instead of four (the small launches of 4- and
- * 8-rank shares end with their longest walk wave).
+ * 8-rank shares end with their longest walk wave; walk_bucket 0 only).
  * "walk_k6" (1, 2, 4 or 8; default 4): sets per lane of the other layer-6
  * walk launches: more sets share one walk of their union tree (less work per
  * set, longer waves).  4 gives the shortest single call; with several calls
@@ -322,7 +329,7 @@ int ulg_sweep_shard_end(ulg_ctx *ctx, uint64_t *vpar, int *order, float *goal_co
  * (0..4, default 3): layers up to this size (and up to score_small_layers)
  * run in ONE launch, a workgroup of 1024 threads per variable taking its
  * layers and phases in order with a barrier between them (score_variant 113
- * only, and not under time_limit_ms, whose budget is checked after every
+ * and 241 only, and not under time_limit_ms, whose budget is checked after every
  * layer; lists identical either way; C3 layers 1-3: 40 us against 54 us
  * for six launches, layer 4 in it 340 us: too many sets for one workgroup).
  * "time_limit_ms" (default 0 = none): the reference's -r running-time budget

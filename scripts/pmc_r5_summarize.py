@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Per-dispatch counters of the scorer's roofline pair from a
-scripts/r5_probe.sh output directory: layer 6 without variable 0 at C3,
-score_layer_kernel<6, 1, 81> (grid = the layer's 2,557,324 sets rounded to
-256) plus walk_sliced_kernel<6, 1, 4> (grid = the same sets / 4 per lane).
+scripts/gpu_probe.sh pmc_scorer output directory: layer 6 without variable 0
+at C3, score_layer_kernel<6, 1, 209> (grid = the layer's 2,557,324 sets
+rounded to 256) plus walk_bucket_kernel<6, 1, K> (round 5: <6, 1, 81> and
+walk_sliced_kernel<6, 1, K>).
 
 * traffic = 2 x FETCH_SIZE + WRITE_SIZE (KiB per dispatch, gfx950
   correction of MI355X_MICROARCH.md, calibrated for gathers in
@@ -13,7 +14,7 @@ score_layer_kernel<6, 1, 81> (grid = the layer's 2,557,324 sets rounded to
   the fraction of the kernel's cycles the average CU's texture-address unit
   is busy.
 
-    python scripts/pmc_r5_summarize.py gpurun_out/r5probe > profiles/r5/pmc_scorer.json
+    python scripts/pmc_r5_summarize.py gpurun_out/<tag> > profiles/r6/pmc_scorer.json
 """
 import csv
 import glob
@@ -24,7 +25,9 @@ import sys
 
 # (kernel name prefix; the dispatches averaged are those with the largest
 # grid, i.e. the full-layer launches of one stream per context)
-KERNELS = {"score": "score_layer_kernel<6, 1, 81>", "walk": "walk_sliced_kernel<6, 1, "}
+# round 6: variant 241 (V = 209) and the key-sorted walk (walk_bucket_kernel;
+# its count / scatter kernels are summed in as "sort" when present)
+KERNELS = {"score": "score_layer_kernel<6, 1, 209>", "walk": "walk_bucket_kernel<6, 1, "}
 N_CU, N_XCD = 256, 8
 
 
@@ -78,6 +81,13 @@ def main():
         if "TA_TA_BUSY_sum" in c and c.get("GRBM_GUI_ACTIVE"):
             e["ta_busy_frac"] = (c["TA_TA_BUSY_sum"] / N_CU) / (c["GRBM_GUI_ACTIVE"] / N_XCD)
             e["kernel_cycles_per_xcd"] = c["GRBM_GUI_ACTIVE"] / N_XCD
+        # VALU instructions per wave, and resident waves per SIMD over the
+        # kernel (SQ_WAVE_CYCLES counts quad-cycles: x4 cycles, / 4 SIMDs per CU)
+        if c.get("SQ_WAVES"):
+            e["valu_per_wave"] = c.get("SQ_INSTS_VALU", 0.0) / c["SQ_WAVES"]
+            e["salu_per_wave"] = c.get("SQ_INSTS_SALU", 0.0) / c["SQ_WAVES"]
+        if "SQ_WAVE_CYCLES" in c and e.get("kernel_cycles_per_xcd"):
+            e["resident_waves_per_simd"] = c["SQ_WAVE_CYCLES"] / (e["kernel_cycles_per_xcd"] * N_CU)
         if "TCP_TCC_READ_REQ_sum" in c and c["TCP_TCC_READ_REQ_sum"]:
             e["l1_to_l2_latency_cycles"] = c["TCP_TCC_READ_REQ_LATENCY_sum"] / c["TCP_TCC_READ_REQ_sum"]
         e["counters_per_dispatch"] = {kk: round(vv, 1) for kk, vv in c.items()

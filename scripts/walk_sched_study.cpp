@@ -365,6 +365,178 @@ int main(int argc, char **argv) {
                         per, mx2, tot2);
         }
     }
+    // 7. groupings by walk-tree similarity: sets sorted by a key of their
+    //    open bits (the nodes the walk may expand), 64*K per wave
+    {
+        auto popc_lvl = [&](const Set &x, int lvl) {  // open bits of the nodes with popcount == lvl
+            uint64_t k = 0;
+            const int Q = L_ + 1;
+            int nb = 0;
+            for (uint32_t t = 0; t < (1u << Q); ++t)
+                if (__builtin_popcount(t) == lvl) {
+                    if (tb(x.open, t)) k |= 1ull << nb;
+                    if (++nb == 64) break;
+                }
+            return k;
+        };
+        const int top = PH_ == 0 ? L_ - 1 : L_;
+        for (int depth = 1; depth <= 3; ++depth) {
+            std::vector<size_t> ix(all.size());
+            std::iota(ix.begin(), ix.end(), 0);
+            std::vector<std::vector<uint64_t>> key(all.size());
+            for (size_t i = 0; i < all.size(); ++i)
+                for (int d = 0; d < depth; ++d) key[i].push_back(popc_lvl(*all[i], top - d));
+            std::stable_sort(ix.begin(), ix.end(), [&](size_t a, size_t b) { return key[a] < key[b]; });
+            std::vector<Set *> o;
+            for (size_t i : ix) o.push_back(all[i]);
+            for (int per : {64, 64 * K}) {
+                long sum;
+                const long m = sched_max(o, per, &sum);
+                std::printf("sorted by open bits of the top %d levels, %d sets/wave: max union %ld, waves %zu, sum %ld\n",
+                            depth, per, m, (o.size() + per - 1) / per, sum);
+            }
+        }
+        // the full open words
+        std::vector<size_t> ix(all.size());
+        std::iota(ix.begin(), ix.end(), 0);
+        std::stable_sort(ix.begin(), ix.end(), [&](size_t a, size_t b) {
+            for (int w = W_ - 1; w >= 0; --w)
+                if (all[a]->open[w] != all[b]->open[w]) return all[a]->open[w] < all[b]->open[w];
+            return false;
+        });
+        std::vector<Set *> o;
+        for (size_t i : ix) o.push_back(all[i]);
+        for (int per : {64, 64 * K}) {
+            long sum;
+            const long m = sched_max(o, per, &sum);
+            std::printf("sorted by the open words, %d sets/wave: max union %ld, waves %zu, sum %ld\n", per, m,
+                        (o.size() + per - 1) / per, sum);
+        }
+    }
+    // 8. sorted by the open words within each segment only (a per-segment
+    //    sort in LDS by the walk launch), 64*K or 64 sets per wave
+    for (int per : {64, 128, 64 * K}) {
+        long mx = 0, tot = 0, nw = 0;
+        std::vector<long> wu;
+        for (auto &sg : segs) {
+            std::vector<Set *> o;
+            for (auto &x : sg) o.push_back(&x);
+            std::stable_sort(o.begin(), o.end(), [&](Set *a, Set *b) {
+                for (int w = W_ - 1; w >= 0; --w)
+                    if (a->open[w] != b->open[w]) return a->open[w] < b->open[w];
+                return false;
+            });
+            for (size_t i = 0; i < o.size(); i += per) {
+                Group g;
+                for (size_t j = i; j < std::min(o.size(), i + per); ++j) g.s.push_back(o[j]);
+                const long p = g.run();
+                wu.push_back(p);
+                mx = std::max(mx, p);
+                tot += p;
+                ++nw;
+            }
+        }
+        std::sort(wu.begin(), wu.end());
+        std::printf("per-segment sort by open words, %d sets/wave: waves %ld, max union %ld, p99 %ld, p90 %ld, sum %ld\n",
+                    per, nw, mx, wu[wu.size() * 99 / 100], wu[wu.size() * 9 / 10], tot);
+    }
+    // 9. a counting sort by B bits of the open words: the bits of the
+    //    first-level nodes (P minus one element, the walk's first tests) and
+    //    then the next levels, most significant first; queue order within a key
+    {
+        const int Q = L_ + 1;
+        const uint32_t root = PH_ == 0 ? ((1u << L_) - 1u) : (((1u << L_) - 1u) << 1);
+        // node order: by popcount descending (closest to the root first), then t
+        std::vector<uint32_t> nodes;
+        for (int pc = Q; pc >= 1; --pc)
+            for (uint32_t t = 0; t < (1u << Q); ++t)
+                if (__builtin_popcount(t) == pc && t != root && t != (root | 1u) && (t & ~(root | 1u)) == 0)
+                    nodes.push_back(t);
+        for (int B : {6, 8, 10, 12, 14, 16, 20}) {
+            std::vector<size_t> ix(all.size());
+            std::iota(ix.begin(), ix.end(), 0);
+            std::vector<uint32_t> key(all.size());
+            for (size_t i = 0; i < all.size(); ++i) {
+                uint32_t k = 0;
+                for (int b2 = 0; b2 < B && b2 < (int)nodes.size(); ++b2) k = (k << 1) | (uint32_t)tb(all[i]->open, nodes[b2]);
+                key[i] = k;
+            }
+            std::stable_sort(ix.begin(), ix.end(), [&](size_t a, size_t b) { return key[a] < key[b]; });
+            std::vector<Set *> o;
+            for (size_t i : ix) o.push_back(all[i]);
+            for (int per : {64 * K}) {
+                long sum;
+                const long m = sched_max(o, per, &sum);
+                std::printf("counting sort by %d open bits (levels from the root), %d sets/wave: max union %ld, sum %ld\n",
+                            B, per, m, sum);
+            }
+        }
+    }
+    // 10. buckets by the first-level open bits (6 at layer 6): the buckets
+    //     with at least H open children walked 64 (or 16) per wave, the rest
+    //     64*K2 per wave; queue order within a bucket
+    {
+        const int Q = L_ + 1;
+        const uint32_t root = PH_ == 0 ? ((1u << L_) - 1u) : (((1u << L_) - 1u) << 1);
+        std::vector<uint32_t> first;
+        for (int b2 = (PH_ == 0 ? 0 : 1); b2 <= (PH_ == 0 ? L_ - 1 : L_); ++b2) first.push_back(root ^ (1u << b2));
+        (void)Q;
+        for (int H : {3, 4, 5, 6}) {
+            for (int hp : {16, 64}) {
+                for (int K2 : {4, 8}) {
+                    std::vector<Set *> heavy, light;
+                    std::vector<std::pair<uint32_t, Set *>> lk;
+                    for (Set *x : all) {
+                        uint32_t k = 0;
+                        int nopen = 0;
+                        for (uint32_t t : first) {
+                            k = (k << 1) | (uint32_t)tb(x->open, t);
+                            nopen += tb(x->open, t);
+                        }
+                        if (nopen >= H) heavy.push_back(x);
+                        else lk.push_back({k, x});
+                    }
+                    std::stable_sort(lk.begin(), lk.end(), [](auto &a, auto &b) { return a.first < b.first; });
+                    for (auto &p2 : lk) light.push_back(p2.second);
+                    long s1, s2;
+                    const long m1 = sched_max(heavy, hp, &s1), m2 = sched_max(light, 64 * K2, &s2);
+                    std::printf("buckets: >=%d open children (%zu sets) %d/wave -> max %ld sum %ld (%zu waves); rest "
+                                "(%zu) %d/wave, by key -> max %ld sum %ld (%zu waves)\n",
+                                H, heavy.size(), hp, m1, s1, (heavy.size() + hp - 1) / hp, light.size(), 64 * K2, m2,
+                                s2, (light.size() + 64 * K2 - 1) / (64 * K2));
+                }
+            }
+        }
+    }
+    // 11. two queues: the heavy sets (>= H open first-level children) per
+    //     segment, 64 per wave; the rest per segment in queue order, 64*K2
+    {
+        const uint32_t root = PH_ == 0 ? ((1u << L_) - 1u) : (((1u << L_) - 1u) << 1);
+        std::vector<uint32_t> first;
+        for (int b2 = (PH_ == 0 ? 0 : 1); b2 <= (PH_ == 0 ? L_ - 1 : L_); ++b2) first.push_back(root ^ (1u << b2));
+        for (int H : {5, 6}) {
+            for (int K2 : {4, 8}) {
+                long mh = 0, sh = 0, ml = 0, sl = 0, wh = 0, wl = 0;
+                for (auto &sg : segs) {
+                    std::vector<Set *> heavy, light;
+                    for (auto &x : sg) {
+                        int nopen = 0;
+                        for (uint32_t t : first) nopen += tb(x.open, t);
+                        (nopen >= H ? heavy : light).push_back(&x);
+                    }
+                    long s1, s2;
+                    mh = std::max(mh, sched_max(heavy, 64, &s1));
+                    ml = std::max(ml, sched_max(light, 64 * K2, &s2));
+                    sh += s1;
+                    sl += s2;
+                    wh += (heavy.size() + 63) / 64;
+                    wl += (light.size() + 64 * K2 - 1) / (64 * K2);
+                }
+                std::printf("two queues per segment: heavy >= %d: max %ld sum %ld (%ld waves); light %d/wave: max %ld "
+                            "sum %ld (%ld waves)\n", H, mh, sh, wh, 64 * K2, ml, sl, wl);
+            }
+        }
+    }
     // 5. oracle schedule: by true length
     {
         std::vector<size_t> ix(all.size());

@@ -13,7 +13,7 @@ import synth
 pytestmark = pytest.mark.gpu
 
 REL_TOL = 1e-6
-DEFAULT_VARIANT = 113  # the library default (ulg_internal.h)
+DEFAULT_VARIANT = 241  # the library default (ulg_internal.h)
 
 
 def _compare_lists(o_offs, o_sets, o_scores, g_offs, g_sets, g_scores, variables, ctx=""):
@@ -291,12 +291,14 @@ def test_walk_k6_option_identical_c3_and_segments(ulg_ctx):
         ulg_ctx.set_option("score_streams", 3)
 
 
+@pytest.mark.parametrize("option", ["walk_bucket"])
 @pytest.mark.parametrize("variant", [113, 241])
-def test_walk_lane_matches_oracle(ulg_ctx, oracle_built, variant):
-    """ulg_set_option("walk_lane", 1): one queued set per lane, the recursion
-    as a per-lane state machine (walk_lane_kernel) -- the oracle's sets with
-    and without variable 0 among the candidates (both N4 phases), k = 6, and
-    on a sparse skeleton."""
+def test_walk_forms_match_oracle(ulg_ctx, oracle_built, variant, option):
+    """ulg_set_option("walk_bucket", 0 / 1): the layer-5/6 queues walked in
+    queue order (walk_sliced_kernel) or sorted by walk key
+    (walk_bucket_kernel) -- the oracle's sets with and without variable 0
+    among the candidates (both N4 phases), k = 6, and on a sparse
+    skeleton."""
     n = 12
     X, _ = synth.gaussian_sem(n, 3000, 9251)
     ulg_ctx.load(X, 2.0)
@@ -304,38 +306,42 @@ def test_walk_lane_matches_oracle(ulg_ctx, oracle_built, variant):
     sparse = [int(((1 << n) - 1) & ~int(rng.integers(0, 1 << n))) | 1 for _ in range(n)]
     try:
         ulg_ctx.set_option("score_variant", variant)
-        ulg_ctx.set_option("walk_lane", 1)
+        ulg_ctx.set_option(option, 1)
         for cands in ([(1 << n) - 1] * n, [((1 << n) - 1) & ~1] * n, sparse):
             variables = list(range(1, n)) if cands[0] & 1 == 0 else list(range(n))
             cands = cands[:len(variables)]
             g = ulg_ctx.score_all(variables, cands, 6)
+            assert ulg_ctx.info("score_error_word") == 0
             o = _oracle_lists(oracle_built, X, 2.0, variables, cands, 6)
-            _compare_lists(*o, *g, variables, ctx=f"walk_lane variant {variant}")
+            _compare_lists(*o, *g, variables, ctx=f"{option} variant {variant}")
     finally:
-        ulg_ctx.set_option("walk_lane", 0)
+        ulg_ctx.set_option(option, 0)
         ulg_ctx.set_option("score_variant", DEFAULT_VARIANT)
 
 
-def test_walk_lane_identical_c3_c5(ulg_ctx):
-    """The per-lane walk stores the union walk's lists bit for bit at C3 (and
-    so the oracle command lines', tests/golden/c3_oracle.json) and at the
-    k = 6 C5 shape, with one and three stream groups."""
+@pytest.mark.parametrize("option", ["walk_bucket"])
+def test_walk_forms_identical_c3_c5(ulg_ctx, option):
+    """The key-sorted walk stores the queue-order walk's lists bit for bit at C3 (and so the oracle command lines',
+    tests/golden/c3_oracle.json) and at the k = 6 C5 shape, with one and
+    three stream groups, 4 and 8 sets per lane at layer 6 (walk_k6)."""
     for n, N in ((25, 10000), (32, 50000)):
         X, _ = synth.gaussian_sem(n, N, 9200)
         ulg_ctx.load(X, 2.0)
         full = [(1 << n) - 1] * n
         try:
-            for streams in (1, 3):
+            for streams, k6 in ((1, 4), (3, 4), (1, 8)):
                 ulg_ctx.set_option("score_streams", streams)
-                ulg_ctx.set_option("walk_lane", 0)
+                ulg_ctx.set_option("walk_k6", k6)
+                ulg_ctx.set_option(option, 0)
                 ref = ulg_ctx.score_all(list(range(n)), full, 6)
-                ulg_ctx.set_option("walk_lane", 1)
+                ulg_ctx.set_option(option, 1)
                 got = ulg_ctx.score_all(list(range(n)), full, 6)
                 assert ulg_ctx.info("score_error_word") == 0
                 for a, b in zip(ref, got):
-                    assert np.asarray(a).tobytes() == np.asarray(b).tobytes(), (n, streams)
+                    assert np.asarray(a).tobytes() == np.asarray(b).tobytes(), (n, streams, k6)
         finally:
-            ulg_ctx.set_option("walk_lane", 0)
+            ulg_ctx.set_option(option, 0)
+            ulg_ctx.set_option("walk_k6", 4)
             ulg_ctx.set_option("score_streams", 3)
 
 

@@ -151,6 +151,7 @@ struct ScoreArgs {
     uint64_t *queue;            // variant bit 4: lanes left for the walk launch
     unsigned long long *qcount;
     unsigned long long *err;    // the call's error word (kErrQueue: a walk-queue segment overflowed)
+    uint8_t *qkey;              // bucketed walk launches: per queue entry, its walk key
     double N;
     double lambda;
     int n, nv, S;
@@ -214,6 +215,9 @@ __host__ __device__ inline LdsLayout lds_layout(int n, int nv, int S, int L, int
 constexpr int kSegBlocks = 32;
 constexpr uint64_t kSegEntries = (uint64_t)kSegBlocks * kBlock;
 constexpr int kSegStride = 16;  // counters 128 B apart
+// A bucketed launch's header after its segment counters (zeroed with them):
+// every key's set total (u32 64..127).
+constexpr int kBucketHdrWords = 64;
 // Bits of the call's error word (d_qcount[nqc - 1], zeroed by the prologue,
 // copied beside the stored count by scan_kernel): a wide walk over its cap;
 // a queue position past its segment (nothing is written there); a walk entry
@@ -226,10 +230,27 @@ __device__ __forceinline__ uint64_t walk_segment() { return blockIdx.x % seg_cou
 // segment's counter): table slot | ts bits << 32, the hi words, then the open
 // words (open = absent & cover(T without var 0) & not checked; checked =
 // {empty}).  queue / qcount: the segment's entries and counter.
-template <class BS>
+// The walk key of a queued set (walk_bucket): which of the walk's first-level
+// nodes (P minus one member, the top call's tests) it may expand, one bit per
+// member -- sets with the same key start the same union walk, so a launch
+// sorted by key walks ~3x fewer union points (scripts/walk_sched_study.cpp).
+template <int L, int PHASE, int W>
+__device__ __forceinline__ uint32_t walk_key(const uint64_t (&ow)[W]) {
+    constexpr uint32_t root = PHASE == 0 ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
+    uint32_t key = 0;
+#pragma unroll
+    for (int a = 0; a < L; ++a) {
+        constexpr int off = PHASE == 0 ? 0 : 1;
+        const uint32_t t = root ^ (1u << (a + off));
+        key |= (uint32_t)((ow[t >> 6] >> (t & 63u)) & 1ull) << a;
+    }
+    return key;
+}
+
+template <int L, int PHASE, class BS>
 __device__ __forceinline__ void queue_walk(const BS &present, const BS &hi, uint64_t *queue,
                                            unsigned long long *qcount, unsigned long long *err, uint64_t slot,
-                                           float ts) {
+                                           float ts, uint8_t *qkey = nullptr) {
     constexpr int W = BS::kWords;
     const unsigned long long act = __ballot(1);
     const int lane = threadIdx.x & 63;
@@ -253,6 +274,8 @@ __device__ __forceinline__ void queue_walk(const BS &present, const BS &hi, uint
         const uint64_t ce = ow[wj] & 0x5555555555555555ull;
         ow[wj] = (ce | (ce << 1)) & ~present.word(wj) & (wj == 0 ? ~1ull : ~0ull);
     }
+    if constexpr (W < 4)
+        if (qkey) qkey[pos] = (uint8_t)walk_key<L, PHASE, W>(ow);
     uint64_t *e = queue + pos * (uint64_t)(1 + 2 * W);
     e[0] = slot | ((uint64_t)fbits(ts) << 32);
 #pragma unroll
@@ -431,8 +454,8 @@ __device__ __forceinline__ void one_pass_set(const ScoreArgs &a, unsigned char *
             if (queued) {
                 const uint64_t seg = walk_segment();
                 constexpr int QW = bits_words(L);
-                queue_walk(present, hi, a.queue + seg * kSegEntries * (uint64_t)(1 + 2 * QW),
-                           a.qcount + seg * kSegStride, a.err, toff[vbase + L] + rankP, ts);
+                queue_walk<L, PHASE>(present, hi, a.queue + seg * kSegEntries * (uint64_t)(1 + 2 * QW),
+                                     a.qcount + seg * kSegStride, a.err, toff[vbase + L] + rankP, ts);
             }
             out = dom ? absent_f() : -ts;
         } else {
@@ -506,8 +529,9 @@ __device__ __forceinline__ void walk_or_store(const ScoreArgs &a, BS &present, B
     }
     if (may_hit) {
 #ifndef ULG_PROBE_NOQUEUE
-        queue_walk(present, hib, a.queue + seg * kSegEntries * (uint64_t)(1 + 2 * W), a.qcount + seg * kSegStride,
-                   a.err, sk, tk);
+        queue_walk<L, PHASE>(present, hib, a.queue + seg * kSegEntries * (uint64_t)(1 + 2 * W),
+                             a.qcount + seg * kSegStride, a.err, sk, tk,
+                             a.qkey ? a.qkey + seg * kSegEntries : nullptr);
 #endif
         if (a.hsub_out) a.hsub[sk] = hch;  // the walk raises it to -ts if it stores P
     } else {
@@ -527,15 +551,15 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
     uint32_t *binom = reinterpret_cast<uint32_t *>(smem + lay.binom);
     uint64_t *work = reinterpret_cast<uint64_t *>(smem + lay.work);
     uint64_t *toff = reinterpret_cast<uint64_t *>(smem + lay.toff);
-    for (int i = threadIdx.x; i < a.n * a.n; i += kBlock) g[i] = a.gram[i];
-    for (int i = threadIdx.x; i < 64 * kBinomK; i += kBlock) binom[i] = a.binom[i];
-    for (int i = threadIdx.x; i <= a.nv; i += kBlock) work[i] = a.work[i];
-    for (int i = threadIdx.x; i <= a.nv * a.S; i += kBlock) toff[i] = a.tbl_off[i];
     // the per-variable metadata and candidate lists too: every lane reads
     // them right after its variable is known, and from global memory those
     // would be two more dependent round trips per lane
     int *smeta = reinterpret_cast<int *>(smem + lay.meta);
     uint8_t *scand = reinterpret_cast<uint8_t *>(smem + lay.cand);
+    for (int i = threadIdx.x; i < a.n * a.n; i += kBlock) g[i] = a.gram[i];
+    for (int i = threadIdx.x; i < 64 * kBinomK; i += kBlock) binom[i] = a.binom[i];
+    for (int i = threadIdx.x; i <= a.nv; i += kBlock) work[i] = a.work[i];
+    for (int i = threadIdx.x; i <= a.nv * a.S; i += kBlock) toff[i] = a.tbl_off[i];
     for (int i = threadIdx.x; i < a.nv * 4; i += kBlock) smeta[i] = a.meta[i];
     for (int i = threadIdx.x; i < a.nv * 16; i += kBlock)
         reinterpret_cast<uint32_t *>(scand)[i] = reinterpret_cast<const uint32_t *>(a.cand)[i];
@@ -939,149 +963,255 @@ __global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, 
     walk_store<S::K>(queue, qn, mine, W, dom, table, hsub, nslots, err);
 }
 
-// ---- per-lane walk (round 6, option walk_lane) -------------------------------
-// One queued set per lane, find_best_subset_score's recursion (walk_sliced's
-// order, no-op re-tests skipped) run as an explicit state machine: each
-// iteration a lane may return from a call (RET: pop its caller's frame, clear
-// `checked` for the node it expanded), start the next call of an expansion
-// (CALL: append the next list entry, push its frame) and test one node
-// (TEST).  Lanes walk independently, so a wave takes as many iterations as
-// its longest single walk instead of the union tree of its 256-512 sets'
-// walks: at C3's layer 6 without variable 0 the longest single walk tests 248
-// nodes where a wave's union tree tested up to 811 (walk_sched_study.cpp
-// replays the dumped queues both ways, with identical decisions).  The
-// frames of a lane's callers live in LDS ([depth][lane], 12 B); the current
-// frame, the hi and open bits are registers.
-constexpr int kLaneWaves = 4096;  // resident waves of a walk_lane launch (a grid-stride loop over the chunks)
+// ---- bucketed walk launches (round 6, option walk_bucket) --------------------
+// A layer-5/6 launch's queued sets walked in the order of their walk key
+// (walk_key): a counting sort over (key, segment) -- the scoring kernel
+// writes each set's key, walk_bucket_count_kernel ranks the sets of each
+// segment by key and, in its last block, lays out the keys and a table of walk
+// waves, walk_bucket_scatter_kernel writes each set's queue index at its place -- and
+// walk_bucket_kernel walks the table.  The key whose every first-level node is
+// open holds the longest, least alike walks: it comes first in the table, 64
+// sets per wave (one per lane); every other key 64 x K per wave.  At C3's
+// layer 6 without variable 0 the longest wave's union walk drops from 811 to
+// ~465 points and the launch's union points from 311 K to ~100 K
+// (scripts/walk_sched_study.cpp on the dumped queues).  Same walks, same
+// decisions: only which sets share a wave changes.
+constexpr int kBucketMax = 64;  // walk keys (L <= 6 first-level nodes)
 
-template <int W>
-__device__ __forceinline__ bool lane_bit(const uint64_t (&w)[W], uint32_t t) {
-    uint64_t x = w[0];
+__device__ __forceinline__ uint32_t bucket_order(uint32_t key, uint32_t full) { return key == full ? 0u : key + 1u; }
+
+// One block per kBucketSegs segments: the segments' key histogram in LDS
+// (16 keys per 16-byte load), each entry's rank among the block's sets of its
+// key (qaux = key << 24 | rank), and one global atomic per key for the
+// block's base within the key (kbase; few blocks, so few atomics per address
+// -- one block per segment serialised ~300-2300 atomics on each key's total).
+// The key totals then give every key's sorted start and the list of walk
+// waves (bucket_lanes), recomputed by each later kernel instead of a table.
+#ifndef ULG_BUCKET_SEGS
+#define ULG_BUCKET_SEGS 8
+#endif
+constexpr int kBucketSegs = ULG_BUCKET_SEGS;
+__global__ void __launch_bounds__(256) walk_bucket_count_kernel(const unsigned long long *qseg, uint32_t nseg,
+                                                                int L, const uint8_t *qkey, uint32_t *qaux,
+                                                                uint32_t *kbase) {
+    __shared__ unsigned int lh[kBucketMax];
+    __shared__ unsigned int cst[kBucketSegs + 1];
+    __shared__ unsigned int qnl[kBucketSegs];
+    const uint32_t seg0 = blockIdx.x * kBucketSegs;
+    const uint32_t nsb = nseg - seg0 < (uint32_t)kBucketSegs ? nseg - seg0 : (uint32_t)kBucketSegs;
+    const uint32_t nk = 1u << L;
+    unsigned int *hdr = reinterpret_cast<unsigned int *>(const_cast<unsigned long long *>(qseg) + (uint64_t)nseg * kSegStride);
+    if (threadIdx.x < kBucketMax) lh[threadIdx.x] = 0u;
+    if (threadIdx.x < 64) {
+        // the block's segments: their set counts and 16-entry chunk offsets
+        const int lane = threadIdx.x;
+        unsigned int qn = 0;
+        if ((uint32_t)lane < nsb) {
+            const uint64_t qc = qseg[(uint64_t)(seg0 + lane) * kSegStride];
+            qn = (unsigned int)(qc < kSegEntries ? qc : kSegEntries);
+            qnl[lane] = qn;
+        }
+        const unsigned int ch = (qn + 15u) >> 4;
+        unsigned int incl = ch;
 #pragma unroll
-    for (int j = 1; j < W; ++j) x = (t >> 6) == (uint32_t)j ? w[j] : x;
-    return (x >> (t & 63u)) & 1ull;
-}
-template <int W>
-__device__ __forceinline__ void lane_clear(uint64_t (&w)[W], uint32_t t) {
-    const uint64_t m = ~(1ull << (t & 63u));
+        for (int o = 1; o < kBucketSegs; o <<= 1) {
+            const unsigned int t = __shfl_up(incl, o);
+            if (lane >= o) incl += t;
+        }
+        if (lane < kBucketSegs) cst[lane + 1] = incl;
+        if (lane == 0) cst[0] = 0u;
+    }
+    __syncthreads();
+    const unsigned int items = cst[nsb];
+    for (unsigned int it = threadIdx.x; it < items; it += 256) {
+        uint32_t s = 0;
+        while (s + 1 < nsb && cst[s + 1] <= it) ++s;
+        const uint32_t c = it - cst[s];
+        const uint64_t base = (uint64_t)(seg0 + s) * kSegEntries + (uint64_t)c * 16;
+        const unsigned int n = qnl[s] - c * 16 < 16u ? qnl[s] - c * 16 : 16u;
+        const uint4 k4 = *reinterpret_cast<const uint4 *>(qkey + base);
+        const uint32_t kw[4] = {k4.x, k4.y, k4.z, k4.w};
 #pragma unroll
-    for (int j = 0; j < W; ++j) w[j] &= (t >> 6) == (uint32_t)j ? m : ~0ull;
+        for (unsigned int j = 0; j < 16; ++j) {
+            if (j >= n) break;
+            const uint32_t key = (kw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            const uint32_t r = atomicAdd(&lh[key], 1u);
+            qaux[base + j] = (key << 24) | r;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < nk) {
+        const unsigned int c = lh[threadIdx.x];
+        kbase[(uint64_t)blockIdx.x * kBucketMax + threadIdx.x] = c ? atomicAdd(hdr + 64 + threadIdx.x, c) : 0u;
+    }
 }
 
-template <int L, int PHASE>
-__global__ void __launch_bounds__(64) walk_lane_kernel(const uint64_t *queue, const unsigned long long *qcount,
-                                                       float *table, float *hsub, uint64_t nslots,
-                                                       unsigned long long *err, uint32_t nseg) {
-    constexpr int W = bits_words(L);
-    constexpr uint32_t kChunks = (uint32_t)(kSegEntries / 64);
-    __shared__ uint32_t fr[L][3][64];  // the callers' frames: [depth][word][lane]
-    const int lane = threadIdx.x;
-    constexpr bool v0inP = PHASE == 0;
-    constexpr uint32_t Proot = v0inP ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
-    constexpr uint32_t pvroot = [] {
-        uint32_t p = 0;
-        for (int i = 0; i < L; ++i) p |= (uint32_t)(i + (v0inP ? 0 : 1)) << (4 * i);
-        return p;
-    }();
-    const uint64_t items = (uint64_t)nseg * kChunks;
+// The keys in walk order (the all-open key first) as one wave's lanes: lane kk
+// holds key order kk's set count, its first sorted position, and its wave
+// range [wbeg, wend) in the launch's wave list (64 sets per wave for the
+// all-open key, per_light for the others).  hdr: the launch's key totals.
+struct BucketLanes {
+    unsigned int tot, st, wbeg, wend, pk;
+};
+__device__ __forceinline__ BucketLanes bucket_lanes(const unsigned int *hdr, int L, uint32_t per_light) {
+    const uint32_t nk = 1u << L, full = nk - 1u;
+    const int lane = threadIdx.x & 63;
+    const uint32_t kk = (uint32_t)lane;
+    BucketLanes b;
+    b.tot = kk < nk ? hdr[64 + (kk == 0 ? full : kk - 1u)] : 0u;
+    b.pk = kk == 0 ? 64u : per_light;
+    const unsigned int nwk = (b.tot + b.pk - 1) / b.pk;
+    unsigned int st = b.tot, wi = nwk;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned int t = __shfl_up(st, o), u = __shfl_up(wi, o);
+        if (lane >= o) {
+            st += t;
+            wi += u;
+        }
+    }
+    b.st = st - b.tot;
+    b.wend = wi;
+    b.wbeg = wi - nwk;
+    return b;
+}
+
+// Every queued set's queue index at its sorted position: key start + the
+// segment's base in the key + the set's rank (256-entry chunks of each
+// segment, chunk-major, grid-stride).
+__global__ void __launch_bounds__(256) walk_bucket_scatter_kernel(const unsigned long long *qseg,
+                                                                  const uint32_t *qaux, const uint32_t *kbase,
+                                                                  uint32_t nseg, int L, uint32_t *sidx) {
+    const unsigned int *hdr =
+        reinterpret_cast<const unsigned int *>(qseg + (uint64_t)nseg * kSegStride);
+    __shared__ unsigned int kst[kBucketMax];
+    if (threadIdx.x < 64) {
+        const BucketLanes b = bucket_lanes(hdr, L, 64u);
+        const uint32_t nk = 1u << L, kk = threadIdx.x;
+        if (kk < nk) kst[kk == 0 ? nk - 1u : kk - 1u] = b.st;
+    }
+    __syncthreads();
+    const uint64_t items = (uint64_t)nseg * (kSegEntries / 256);
     for (uint64_t item = blockIdx.x; item < items; item += gridDim.x) {
-        const uint32_t seg = (uint32_t)(item % nseg);  // chunk-major: the busy chunks come first
-        const uint64_t first = (item / nseg) * 64;
-        const uint64_t qc = qcount[(uint64_t)seg * kSegStride];
-        const uint64_t qn = qc < kSegEntries ? qc : kSegEntries;  // past it: kErrQueue is set
-        if (first >= qn) continue;
-        const uint64_t mine = first + (uint64_t)lane;
-        const bool valid = mine < qn;
-        const uint64_t *e = queue + ((uint64_t)seg * kSegEntries + (valid ? mine : first)) * (uint64_t)(1 + 2 * W);
-        const uint64_t e0 = e[0];
-        uint64_t hiw[W], ow[W];
+        const uint32_t seg = (uint32_t)(item % nseg);
+        const uint64_t e = (item / nseg) * 256 + threadIdx.x;
+        const uint64_t qc = qseg[(uint64_t)seg * kSegStride];
+        const uint64_t qn = qc < kSegEntries ? qc : kSegEntries;
+        if ((item / nseg) * 256 >= qn) continue;
+        if (e >= qn) continue;
+        const uint32_t ax = qaux[(uint64_t)seg * kSegEntries + e];
+        const uint32_t key = ax >> 24, r = ax & 0xFFFFFFu;
+        const uint32_t pos = kst[key] + kbase[(uint64_t)(seg / kBucketSegs) * kBucketMax + key] + r;
+        sidx[pos] = (uint32_t)((uint64_t)seg * kSegEntries + e);
+    }
+}
+
+// walk_load / walk_sliced / walk_store over the sorted index: wave w of the
+// table walks its sets K per lane.
+template <int L, int PHASE, int K, int NVMAX>
+__device__ __forceinline__ void walk_group(const uint64_t *queue, const uint32_t *sidx, uint32_t st, uint32_t cnt,
+                                           uint32_t *open_lds, float *table, float *hsub, uint64_t nslots,
+                                           unsigned long long *err) {
+    using S = Sliced<L, K>;
+    static_assert(S::NV <= NVMAX, "open bits LDS");
+    constexpr int W = bits_words(L);
+    const uint32_t lane = threadIdx.x;
+    typename S::Vec hiV, openV;
 #pragma unroll
-        for (int j = 0; j < W; ++j) {
-            hiw[j] = e[1 + j];
-            ow[j] = e[1 + W + j];
+    for (int r = 0; r < S::NV; ++r) {
+        hiV[r] = 0u;
+        openV[r] = 0u;
+    }
+    uint32_t alive = 0u;
+    uint32_t ent[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t p = lane * K + k;
+        ent[k] = p < cnt ? sidx[st + p] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        if (ent[k] == 0xFFFFFFFFu) continue;
+        alive |= 1u << k;
+        const uint64_t *e = queue + (uint64_t)ent[k] * (1 + 2 * W);
+        uint64_t hw[W], ow[W];
+#pragma unroll
+        for (int wj = 0; wj < W; ++wj) {
+            hw[wj] = e[1 + wj];
+            ow[wj] = e[1 + W + wj];
         }
-        // the current frame
-        uint32_t T = Proot, pv = pvroot, idx = 0, hend = L, u = 0, i = 0, j = 0, npv = 0;
-        int d = 0;
-        int state = 0;  // 0 TEST, 1 CALL, 2 RET
-        bool done = !valid, dom = false;
-        while (__ballot(!done) != 0ull) {
-            if (!done && state == 2) {
-                if (d == 0) {
-                    done = true;  // exhausted: no key >= -ts visited, P is stored
-                } else {
-                    lane_clear<W>(ow, T);  // checked.insert(T2) in the caller
-                    --d;
-                    const uint32_t w0 = fr[d][0][lane], w1 = fr[d][1][lane], w2 = fr[d][2][lane];
-                    pv = w0 & 0xFFFFFFu;
-                    idx = (w0 >> 24) & 7u;
-                    hend = w0 >> 27;
-                    npv = w1 & 0xFFFFFFu;
-                    i = (w1 >> 24) & 7u;
-                    j = w1 >> 27;
-                    T = w2 & 0xFFu;
-                    u = w2 >> 8;
-                    state = 1;
-                }
-            }
-            if (!done && state == 1) {
-                // the next list entry that is not u (an entry equal to u is
-                // skipped: the zero padding when u is variable 0)
-                const uint32_t M = (uint32_t)(L - d);
-                const uint32_t x = pv ^ (u * 0x111111u);
-                uint32_t nz = (x | (x >> 1) | (x >> 2) | (x >> 3)) & 0x111111u;
-                nz &= (0x111111u << (4 * i)) & ((1u << (4 * M)) - 1u);
-                if (nz == 0u) {
-                    ++idx;  // every call of the expansion made
-                    state = 0;
-                } else {
-                    const uint32_t ii = (uint32_t)__builtin_ctz(nz) >> 2;
-                    npv |= ((pv >> (4 * ii)) & 15u) << (4 * j);
-                    ++j;
-                    i = ii + 1;
-                    fr[d][0][lane] = pv | (idx << 24) | (hend << 27);
-                    fr[d][1][lane] = npv | (i << 24) | (j << 27);
-                    fr[d][2][lane] = T | (u << 8);
-                    ++d;
-                    T ^= 1u << u;
-                    pv = npv;
-                    const uint32_t Mc = M - 1;
-                    idx = j == 1 ? 0u : j - 1;
-                    hend = j == 1 ? (Mc < 2 ? Mc : 2u) : j;
-                    state = 0;
-                }
-            }
-            if (!done && state == 0) {
-                if (idx >= hend) {
-                    state = 2;
-                } else {
-                    const uint32_t u2 = (pv >> (4 * idx)) & 15u;
-                    const uint32_t T2 = T ^ (1u << u2);
-                    if (lane_bit<W>(hiw, T2)) {
-                        dom = true;  // a key >= -ts: find_best_subset_score returns >= -ts, P is pruned
-                        done = true;
-                    } else if (d < L - 1 && lane_bit<W>(ow, T2)) {
-                        u = u2;
-                        i = 0;
-                        j = 0;
-                        npv = 0;
-                        state = 1;
-                    } else {
-                        ++idx;
-                    }
-                }
-            }
-        }
-        if (valid) {
-            const float ts = __uint_as_float((uint32_t)(e0 >> 32));
-            const uint32_t slot = (uint32_t)e0;
-            if (slot >= nslots) {
-                atomicOr(err, kErrSlot);
+#pragma unroll
+        for (int r = 0; r < S::NV0; ++r) {
+            const int t0 = r * S::E;
+            constexpr uint32_t EM = (uint32_t)((1ull << S::E) - 1ull);
+            const uint32_t hb = (uint32_t)(hw[t0 >> 6] >> (t0 & 63)) & EM;
+            const uint32_t ob = (uint32_t)(ow[t0 >> 6] >> (t0 & 63)) & EM;
+            uint32_t hs = 0u, os = 0u;
+            if constexpr (S::K == 8) {
+                hs = (hb * 0x00204081u) & 0x01010101u;
+                os = (ob * 0x00204081u) & 0x01010101u;
+            } else if constexpr (S::K == 1) {
+                hs = hb;
+                os = ob;
             } else {
-                table[slot] = dom ? absent_f() : -ts;
-                if (hsub && !dom) hsub[slot] = fmaxf(hsub[slot], -ts);
+#pragma unroll
+                for (int f = 0; f < S::E; ++f) {
+                    hs |= ((hb >> f) & 1u) << (S::K * f);
+                    os |= ((ob >> f) & 1u) << (S::K * f);
+                }
             }
+            hiV[r] |= hs << k;
+            openV[r] |= os << k;
         }
+    }
+    constexpr bool v0inP = PHASE == 0;
+    constexpr uint32_t Plocal = v0inP ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
+    uint32_t pvtop = 0;
+#pragma unroll
+    for (int i = 0; i < L; ++i) pvtop |= (uint32_t)(i + (v0inP ? 0 : 1)) << (4 * i);
+    uint32_t dom = 0u, pts = 0u;
+    OpenLds<L, K> ol{open_lds + lane};
+#pragma unroll
+    for (int r = 0; r < S::NV; ++r) ol.base[r * 64] = openV[r];
+    walk_sliced<L, K, L, false, OpenLds<L, K>, PHASE>(Plocal, pvtop, alive, hiV, ol, alive, dom, pts);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        if (ent[k] == 0xFFFFFFFFu) continue;
+        const uint64_t e0 = queue[(uint64_t)ent[k] * (1 + 2 * W)];
+        const float ts = __uint_as_float((uint32_t)(e0 >> 32));
+        const bool d = (dom >> k) & 1u;
+        const uint32_t slot = (uint32_t)e0;
+        if (slot >= nslots) {
+            atomicOr(err, kErrSlot);
+            continue;
+        }
+        table[slot] = d ? absent_f() : -ts;
+        if (hsub && !d) hsub[slot] = fmaxf(hsub[slot], -ts);
+    }
+}
+
+// hdr: the launch's bucket header (key totals); waves in key order, the
+// all-open key's first (bucket_lanes), a grid-stride loop over them.
+template <int L, int PHASE, int KL>
+__global__ void __launch_bounds__(64) walk_bucket_kernel(const uint64_t *queue, const uint32_t *sidx,
+                                                         const unsigned int *hdr, float *table, float *hsub,
+                                                         uint64_t nslots, unsigned long long *err) {
+    constexpr int NVMAX = Sliced<L, KL>::NV > Sliced<L, 1>::NV ? Sliced<L, KL>::NV : Sliced<L, 1>::NV;
+    __shared__ uint32_t open_lds[NVMAX * 64];
+    const BucketLanes b = bucket_lanes(hdr, L, 64u * KL);
+    const uint32_t nw = __shfl(b.wend, 63);
+    for (uint32_t w = blockIdx.x; w < nw; w += gridDim.x) {
+        // the key order kk holding wave w: the first lane whose range ends past w
+        const unsigned long long past = __ballot(b.wend > w);
+        const int kk = __ffsll((long long)past) - 1;
+        const uint32_t wbeg = __shfl(b.wbeg, kk), st = __shfl(b.st, kk), tot = __shfl(b.tot, kk),
+                       pk = __shfl(b.pk, kk);
+        const uint32_t off = (w - wbeg) * pk;
+        const uint32_t cw = tot - off < pk ? tot - off : pk;
+        if (kk == 0)
+            walk_group<L, PHASE, 1, NVMAX>(queue, sidx, st + off, cw, open_lds, table, hsub, nslots, err);
+        else
+            walk_group<L, PHASE, KL, NVMAX>(queue, sidx, st + off, cw, open_lds, table, hsub, nslots, err);
     }
 }
 
@@ -2214,22 +2344,17 @@ SlicedFn sliced_fn(int L, int phase, int k) {
     }
 }
 
-using LaneFn = void (*)(const uint64_t *, const unsigned long long *, float *, float *, uint64_t, unsigned long long *,
-                       uint32_t);
-template <int L>
-LaneFn lane_pick(int phase) {
-    return phase == 0 ? walk_lane_kernel<L, 0> : walk_lane_kernel<L, 1>;
+using BucketFn = void (*)(const uint64_t *, const uint32_t *, const unsigned int *, float *, float *, uint64_t,
+                         unsigned long long *);
+template <int L, int KL>
+BucketFn bucket_pick(int phase) {
+    return phase == 0 ? walk_bucket_kernel<L, 0, KL> : walk_bucket_kernel<L, 1, KL>;
 }
-LaneFn lane_fn(int L, int phase) {
-    switch (L) {
-        case 1: return lane_pick<1>(phase);
-        case 2: return lane_pick<2>(phase);
-        case 3: return lane_pick<3>(phase);
-        case 4: return lane_pick<4>(phase);
-        case 5: return lane_pick<5>(phase);
-        case 6: return lane_pick<6>(phase);
-        default: return nullptr;
-    }
+// layers 5 and 6; KL = sets per lane of the light keys (2 or 4 at layer 5, 4 or 8 at 6)
+BucketFn bucket_fn(int L, int phase, int kl) {
+    if (L == 5) return kl >= 4 ? bucket_pick<5, 4>(phase) : bucket_pick<5, 2>(phase);
+    if (L == 6) return kl >= 8 ? bucket_pick<6, 8>(phase) : bucket_pick<6, 4>(phase);
+    return nullptr;
 }
 
 const char *kWalkNames[2][kMaxL + 1] = {
@@ -2965,6 +3090,7 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     sa.queue = nullptr;
     sa.qcount = nullptr;
     sa.err = nullptr;
+    sa.qkey = nullptr;
     sa.N = (double)c->N;
     sa.lambda = c->lambda;
     sa.n = n;
@@ -3035,7 +3161,9 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
         const int g = (int)(i / (2 * (size_t)(kmax + 1))), L = (int)((i / 2) % (size_t)(kmax + 1)), ph = (int)(i % 2);
         const uint64_t cnt = h_wk[(size_t)g * (G > 1 ? wstride : 0) + ((size_t)L * 2 + ph) * (nv + 1) + nv];
         const bool queued = L >= 1 && L <= kMaxL && (variant & 16);
-        segoff[i + 1] = segoff[i] + (queued ? seg_count((cnt + kBlock - 1) / kBlock) * kSegStride : 0);
+        const bool bhdr = queued && (L == 5 || L == 6);  // room for a walk_bucket header
+        segoff[i + 1] = segoff[i] + (queued ? seg_count((cnt + kBlock - 1) / kBlock) * kSegStride : 0) +
+                        (bhdr && cnt ? kBucketHdrWords : 0);
     }
     // queue counters per (group, layer, phase), then the wide walks' error flag
     const size_t nqc = (size_t)G * 2 * (kmax + 1) + 1;
@@ -3044,6 +3172,25 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
             (rc = ensure(c, c->d_wqueue, (size_t)G * wqwords)))
             return rc;
         if ((rc = ensure(c, c->d_qseg, (size_t)std::max<uint64_t>(segoff.back(), 1)))) return rc;
+    }
+    // bucketed walk launches (walk_bucket, layers 5 and 6): per stream group a
+    // key/rank word and a sorted index per queue entry, the (key, segment)
+    // offsets and the wave table
+    const bool bucket = (variant & 112) == 112 && c->walk_bucket && !wck && kmax >= 5;  // the CMP path queues with keys
+    const uint64_t qcap = (qwords / 3 + 255) & ~255ull;  // queue entries per group (an entry is >= 3 words), 256-aligned
+    uint64_t nseg_max = 1;
+    for (int g = 0; g < G; ++g)
+        for (int L = 5; L <= std::min(kmax, 6); ++L)
+            for (int ph = 0; ph < 2; ++ph) {
+                const uint64_t cnt = h_wk[(size_t)g * (G > 1 ? wstride : 0) + ((size_t)L * 2 + ph) * (nv + 1) + nv];
+                nseg_max = std::max<uint64_t>(nseg_max, seg_count((cnt + kBlock - 1) / kBlock));
+            }
+    const uint64_t wave_cap = qcap / 64 + kBucketMax;  // walk waves of a bucketed launch, at most
+    if (bucket) {
+        if ((rc = ensure(c, c->d_qkey, (size_t)(G * qcap))) || (rc = ensure(c, c->d_qaux, (size_t)(G * qcap))) ||
+            (rc = ensure(c, c->d_qsidx, (size_t)(G * qcap))) ||
+            (rc = ensure(c, c->d_qoffs, (size_t)(G * kBucketMax * nseg_max))))
+            return rc;
     }
     // zeroed by call_prologue_kernel (the first launch of the sequence below)
     const bool zero_q = (variant & 16) || kmax > kMaxL;
@@ -3146,7 +3293,10 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     if (use_graph) {
         gkey.assign({(uint64_t)nv, (uint64_t)max_parents, (uint64_t)variant, (uint64_t)G, (uint64_t)Ls,
                      (uint64_t)c->score_xcd, (uint64_t)n, (uint64_t)c->N, dbits(c->lambda), (uint64_t)c->prof,
-                     (uint64_t)c->walk_small_sets, (uint64_t)c->walk_k6, (uint64_t)c->walk_lane,
+                     (uint64_t)c->walk_small_sets, (uint64_t)c->walk_k6,
+                     (uint64_t)c->walk_bucket, (uint64_t)(uintptr_t)c->d_qaux.p, (uint64_t)(uintptr_t)c->d_qsidx.p,
+                     (uint64_t)(uintptr_t)c->d_qkey.p,
+                     (uint64_t)(uintptr_t)c->d_qoffs.p,
                      (uint64_t)(uintptr_t)c->table.p, (uint64_t)(uintptr_t)c->d_work.p,
                      (uint64_t)(uintptr_t)c->d_workg.p, (uint64_t)(uintptr_t)c->d_queue.p,
                      (uint64_t)(uintptr_t)c->d_qcount.p, (uint64_t)(uintptr_t)c->d_qseg.p, (uint64_t)(uintptr_t)c->d_cand.p,
@@ -3249,6 +3399,8 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                     (variant & 16) ? c->d_qseg.p + segoff[(size_t)g * 2 * (kmax + 1) + (size_t)L * 2 + ph] : nullptr;
                 sa.queue = (variant & 16) ? c->d_queue.p + (size_t)g * qwords : nullptr;
                 sa.qcount = qc;
+                const bool bk = bucket && (L == 5 || L == 6);
+                sa.qkey = bk ? c->d_qkey.p + (size_t)g * qcap : nullptr;
                 // nothing reads the subset maxima of the top layer's second phase
                 sa.hsub_out = !(L == kmax && ph == 1);
                 const uint64_t blocks = (cnt + kBlock - 1) / kBlock;
@@ -3279,16 +3431,24 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
                 if (variant & 16) {
                     // the undecided lanes of this launch, densely packed
                     const int wk = sliced_k(L, cnt, (uint64_t)c->walk_small_sets, c->walk_k6);
-                    if ((variant & 32) && c->walk_lane && !wck && lane_fn(L, ph)) {
-                        // one set per lane: 64-entry chunks, a grid-stride loop of
-                        // at most kLaneWaves waves
+                    if (bk) {
+                        // counting sort of the queue by walk key, then the table's waves
                         const uint64_t nseg = seg_count(blocks);
-                        const uint64_t items = nseg * (kSegEntries / 64);
-                        const uint64_t lb = std::min<uint64_t>(items, (uint64_t)kLaneWaves);
+                        const int kl = L == 6 ? (wk >= 8 ? 8 : 4) : (wk >= 4 ? 4 : 2);
+                        uint32_t *kbase = c->d_qoffs.p + (size_t)g * kBucketMax * nseg_max;
+                        uint32_t *sidx = c->d_qsidx.p + (size_t)g * qcap;
+                        uint32_t *qaux = c->d_qaux.p + (size_t)g * qcap;
+                        const unsigned int *hdr = reinterpret_cast<const unsigned int *>(qc + nseg * kSegStride);
+                        // the profiled walk time includes the sort (count + scatter)
                         prof_begin_s(c, kWalkNames[ph][L], st);
-                        hipLaunchKernelGGL(lane_fn(L, ph), dim3((unsigned)lb), dim3(64), 0, st, sa.queue, qc,
-                                           c->table.p, sa.hsub_out ? sa.hsub : nullptr, total_slots, sa.err,
-                                           (uint32_t)nseg);
+                        walk_bucket_count_kernel<<<(unsigned)((nseg + kBucketSegs - 1) / kBucketSegs), 256, 0, st>>>(
+                            qc, (uint32_t)nseg, L, sa.qkey, qaux, kbase);
+                        const uint64_t items = nseg * (kSegEntries / 256);
+                        walk_bucket_scatter_kernel<<<(unsigned)std::min<uint64_t>(items, 2048), 256, 0, st>>>(
+                            qc, qaux, kbase, (uint32_t)nseg, L, sidx);
+                        hipLaunchKernelGGL(bucket_fn(L, ph, kl), dim3((unsigned)std::min<uint64_t>(wave_cap, 4096)),
+                                           dim3(64), 0, st, (const uint64_t *)sa.queue, (const uint32_t *)sidx, hdr,
+                                           c->table.p, sa.hsub_out ? sa.hsub : nullptr, total_slots, sa.err);
                         prof_end_s(c, st);
                     } else if ((variant & 32) && sliced_fn(L, ph, wk)) {
                         // one wave per (queue segment, chunk of 64 * K entries)

@@ -165,6 +165,7 @@ void ulg_destroy(ulg_ctx *c) {
     release(c->raw); release(c->z); release(c->gram); release(c->partials); release(c->colstat);
     release(c->table); release(c->d_tbl_off); release(c->d_work); release(c->d_blk);
     release(c->d_cand); release(c->d_meta); release(c->d_binom); release(c->d_binom64); release(c->d_wqueue); release(c->d_wbits); release(c->d_stats); release(c->d_dump); release(c->d_queue); release(c->d_qcount); release(c->d_workg); release(c->d_vwork); release(c->d_hq); release(c->d_hqc); release(c->d_hmax); release(c->d_hoff); release(c->d_hmeta); release(c->d_scount); release(c->d_hsub); release(c->d_qseg);
+    release(c->d_qaux); release(c->d_qsidx); release(c->d_qoffs); release(c->d_qkey);
     release(c->out_sets); release(c->out_scores); release(c->out_offsets);
     release(c->qbuf_in); release(c->qbuf_out);
     pss_release(c);
@@ -224,9 +225,9 @@ int ulg_set_option(ulg_ctx *c, const char *name, int64_t value) {
         c->walk_k6 = (int)value;
         return ULG_OK;
     }
-    if (std::strcmp(name, "walk_lane") == 0) {
-        if (value != 0 && value != 1) return set_err(c, ULG_ERR_ARG, "walk_lane must be 0 or 1");
-        c->walk_lane = (int)value;
+    if (std::strcmp(name, "walk_bucket") == 0) {
+        if (value != 0 && value != 1) return set_err(c, ULG_ERR_ARG, "walk_bucket must be 0 or 1");
+        c->walk_bucket = (int)value;
         return ULG_OK;
     }
     if (std::strcmp(name, "walk_small_sets") == 0) {

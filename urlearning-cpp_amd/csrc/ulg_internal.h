@@ -69,8 +69,8 @@ struct ulg_ctx {
     int64_t total_stored = 0;
     int64_t total_scored = 0;
     bool scored = false;
-    int score_variant = 113;
-    int walk_lane = 0;  // layers <= 6: one queued set per lane (walk_lane_kernel) instead of the bit-sliced union walk
+    int score_variant = 241;
+    int walk_bucket = 1;  // layers 5, 6: walk the queue sorted by walk key (walk_bucket_kernel)
     int score_streams = 3;                  // scorer variable groups on concurrent streams
     int score_small_layers = 4;             // layers <= this run one-pass on one stream (two-pass variants)
     int score_fused = 3;                    // ... and layers <= this (<= small layers) in one launch, a workgroup per variable
@@ -110,6 +110,8 @@ struct ulg_ctx {
     ulg::DevBuf<unsigned long long> d_stats;  // score_variant 13 statistics
     ulg::DevBuf<uint64_t> d_dump;
     ulg::DevBuf<uint64_t> d_queue;                // score_variant bit 4: undecided lanes
+    ulg::DevBuf<uint32_t> d_qaux, d_qsidx, d_qoffs;  // walk_bucket: key/rank, sorted index, key bases
+    ulg::DevBuf<uint8_t> d_qkey;                            // walk_bucket: each queue entry's walk key
     ulg::DevBuf<unsigned long long> d_qseg;       // ... their per-segment counters (cbic.hip kSegBlocks)
     ulg::DevBuf<unsigned long long> d_qcount;
     ulg::DevBuf<uint64_t> d_workg;                // per stream-group work prefixes
@@ -174,7 +176,9 @@ int ensure(ulg_ctx *c, DevBuf<T> &b, size_t elems) {
     if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
     b.cap = 0;
-    hipError_t e = hipMalloc(&b.p, elems * sizeof(T));
+    // 16 bytes of slack: kernels copy whole 16-byte chunks (fill_lds), so the
+    // last chunk of an array may read up to 15 bytes past its end
+    hipError_t e = hipMalloc(&b.p, elems * sizeof(T) + 16);
     if (e != hipSuccess)
         return set_err(c, ULG_ERR_HIP, std::string("hipMalloc failed: ") + hipGetErrorString(e));
     b.cap = elems;
