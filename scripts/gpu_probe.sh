@@ -23,6 +23,11 @@
 #   slots       bench steps in flight: SLOTS x KS, two rounds   -> slots_*.json
 #   wclock      scripts/walk_clock.py --case c3 per build in LIBS -> wc_<lib>/
 #   c4          scripts/c4_probe.py 29 (VARS)                   -> c4.log
+#   pmc_c4      two SQ passes of C4's wide-layer replays (c4_probe.py 29
+#               VARS, default 23, ULG_WALK_STATS) for c4_replay_summary.py
+#   exact       scripts/probe_exact.py c3 per ULG_EXACT_PF mode in PF_MODES
+#               (default "6"), two alternating rounds -> exact_<mode>_<rep>.json
+# (round 5's scripts/r5_*.sh and r4_probe.sh are these steps now)
 set -eu
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -113,6 +118,20 @@ for step in ${STEPS:-suite smoke bench}; do
     c4)
       timeout -k 10 300 python3 scripts/c4_probe.py 29 ${VARS:-} > "$OUT/c4.log" 2>&1
       tail -n 3 "$OUT/c4.log" ;;
+    pmc_c4)
+      i=0
+      for ctrs in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD" \
+          "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_LDS_BANK_CONFLICT"; do
+        i=$((i+1))
+        ULG_WALK_STATS=1 timeout -s KILL 150 rocprofv3 --pmc $ctrs --kernel-trace --output-format csv -d "$OUT/c4p$i" -o run -- \
+          python3 scripts/c4_probe.py 29 ${VARS:-23} > "$OUT/c4p$i.log" 2>&1
+        echo "c4 pmc pass $i ok"
+      done ;;
+    exact)
+      for rep in 1 2; do for pf in ${PF_MODES:-6}; do
+        ULG_EXACT_PF=$pf timeout -k 10 240 python3 scripts/probe_exact.py c3 > "$OUT/exact_${pf}_$rep.json" 2> "$OUT/exact_${pf}_$rep.err"
+        echo "exact pf=$pf rep=$rep $(cat "$OUT/exact_${pf}_$rep.json")"
+      done; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

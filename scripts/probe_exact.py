@@ -1,4 +1,9 @@
-"""Times the exact-order A* (host replay over GPU tables) at C2 and C3."""
+"""Times the exact-order A* (host replay over GPU tables) at C2 and C3, with
+the replay thread's host counters per expansion (ulg_get_info exact_*), and
+checks C3's goal cost and expansion count against tests/golden/c3_oracle.json.
+ULG_EXACT_PF selects the heap layout / prefetch mode (search_host.cpp):
+    python scripts/probe_exact.py [c2] [c3]"""
+import json
 import os
 import sys
 import time
@@ -18,7 +23,18 @@ for name in (sys.argv[1:] or ["c2", "c3"]):
     ctx.score(list(range(n)), full, k)
     ctx.search_from_scores()
     t = time.perf_counter()
-    r = ctx.astar(edges=full, mode=0, net_text=False)
+    r = ctx.astar(edges=full, mode=0, net_text=(name == "c3"))
     dt = time.perf_counter() - t
-    print(name, "exact A*:", r["expanded"], "expansions in %.3f s = %.3g /s" % (dt, r["expanded"] / dt),
-          "cost", r["cost"], flush=True)
+    e = max(r["expanded"], 1)
+    pmu = {kk: ctx.info("exact_" + kk) for kk in ("cycles", "instructions", "cache_misses")}
+    out = {"case": name, "pf": os.environ.get("ULG_EXACT_PF", "6"), "expanded": r["expanded"], "seconds": dt,
+           "expansions_per_s": r["expanded"] / dt, "cost": r["cost"],
+           "ns_per_expansion": 1e9 * dt / e,
+           "cycles_per_expansion": pmu["cycles"] / e if pmu["cycles"] >= 0 else None,
+           "cache_misses_per_expansion": pmu["cache_misses"] / e if pmu["cache_misses"] >= 0 else None}
+    if name == "c3":
+        ref = json.load(open(os.path.join(ROOT, "tests", "golden", "c3_oracle.json")))
+        out["oracle_expanded"] = ref.get("expanded")
+        out["equal_to_oracle"] = (r["expanded"] == ref["expanded"] and r["cost"] == ref["goal_cost"]
+                                  and r["net_text"] == ref["net_file"])
+    print(json.dumps(out), flush=True)

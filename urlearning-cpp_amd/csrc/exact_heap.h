@@ -200,20 +200,60 @@ struct DEnt {
     inline uint32_t layer() const { return key >> 27; }
 };
 
-struct DenseHeap {
-    DEnt *a = nullptr;  // buffer (grows to at most 2^m + 1 entries; never shrinks)
-    bool pf5 = false;   // pop: prefetch five levels ahead as well as four
+// Physical layouts of the dense heap's logical positions p (the reference's
+// implicit binary heap: children 2p+1, 2p+2).  The algorithms read and write
+// logical positions only, so a layout changes where an entry lives, never
+// which entry a position holds: the pop order and the pqPos values are the
+// reference's in every layout.
+//
+// FlatLayout: position p at a[p] (the buffer starts 8 B into a line, so two
+// siblings share 16 aligned bytes).
+struct FlatLayout {
+    static constexpr bool kBlocked = false;
+    static inline int64_t phys(int64_t p) { return p; }
+};
+// PairBlockLayout (round 6, review item 7): every node q at an even depth
+// owns one 64-B line holding its two children and four grandchildren (slots
+// 0-1 and 2-5; 6-7 unused), the lines in BFS order of their owners; the root
+// is alone in line 0.  A descent then reads one line per two levels instead
+// of one per level, and the line it needs next is known one block ahead:
+// the block of the even-depth node it stands on.
+struct PairBlockLayout {
+    static constexpr bool kBlocked = true;
+    // the line of the block owned by even-depth node i (1-based)
+    static inline int64_t block_line(uint64_t i) {
+        const int dq = 63 - __builtin_clzll(i);  // even
+        return 1 + (int64_t)((((uint64_t)1 << dq) - 1) / 3 + (i - ((uint64_t)1 << dq)));
+    }
+    static inline int64_t phys(int64_t p) {
+        const uint64_t i = (uint64_t)p + 1;
+        if (i == 1) return 0;
+        const int d = 63 - __builtin_clzll(i);
+        if (d & 1) return 8 * block_line(i >> 1) + (int64_t)(i & 1);
+        return 8 * block_line(i >> 2) + 2 + (int64_t)(i & 3);
+    }
+    // physical entries for logical positions [0, n)
+    static inline int64_t capacity(int64_t n) { return n <= 1 ? 8 : phys(n - 1) + 8; }
+};
+
+template <class Lay>
+struct DenseHeapT {
+    using Layout = Lay;
+    DEnt *a = nullptr;  // buffer (grows to at most 2^m + 1 logical entries; never shrinks)
+    bool pf5 = false;   // pop: prefetch five levels ahead as well as four (flat layout)
+    bool pfdeep = false;  // blocked layout: also the grandchildren's blocks (two more levels)
     int64_t len = 0, hwm = 0;
     DenseRec *recs = nullptr;
     bool hang = false;
     int64_t scans = 0;
 
+    inline DEnt &A(int64_t p) const { return a[Lay::phys(p)]; }
     // CompareNodeStar, evaluated without branches: the heap descent picks a
     // child per level on it, and that choice is a coin flip for a predictor
-    static inline bool cns(const DEnt &A, const DEnt &B) {
-        const float diff = A.f - B.f;
+    static inline bool cns(const DEnt &X, const DEnt &Y) {
+        const float diff = X.f - Y.f;
         const bool tie = std::fabs(diff) < FLT_EPSILON;
-        const bool deeper = B.layer() > A.layer();
+        const bool deeper = Y.layer() > X.layer();
         const bool worse = diff > 0.0f;
         return (tie & deeper) | (!tie & worse);
     }
@@ -223,29 +263,24 @@ struct DenseHeap {
     inline void setpos(const DEnt &e, int64_t p) { recs[e.slot()].pq = (int32_t)(p + 1); }
     void push_hole(int64_t hole, int64_t top, DEnt value) {
         int64_t parent = (hole - 1) / 2;
-        while (hole > top && cns(a[parent], value)) {
-            a[hole] = a[parent];
-            setpos(a[hole], hole);
+        while (hole > top && cns(A(parent), value)) {
+            A(hole) = A(parent);
+            setpos(A(hole), hole);
             hole = parent;
             parent = (hole - 1) / 2;
         }
-        a[hole] = value;
+        A(hole) = value;
         setpos(value, hole);
     }
     void push(uint32_t x) {
         const DEnt e = ent(x);
-        a[len] = e;
+        A(len) = e;
         ++len;
         hwm = std::max(hwm, len);
         push_hole(len - 1, 0, e);
     }
-    void adjust(int64_t hole, int64_t n, DEnt value) {
-        const int64_t top = hole;
-        int64_t second = hole;
-        uint32_t mv_slot[64];
-        int64_t mv_pos[64];
-        int nm = 0;
-        while (second < (n - 1) / 2) {
+    inline void prefetch_descent(int64_t second, int64_t n) const {
+        if constexpr (!Lay::kBlocked) {
             // four levels ahead: the 16 great-great-grandchildren of the hole
             // are 128 contiguous bytes
             const int64_t g4 = 16 * second + 15;
@@ -262,18 +297,37 @@ struct DenseHeap {
                     __builtin_prefetch(&a[g5 + 31]);
                 }
             }
+        } else {
+            // the hole at an even depth owns the next block (its children and
+            // grandchildren): the one line the next two levels read
+            const uint64_t i = (uint64_t)second + 1;
+            if (!((63 - __builtin_clzll(i)) & 1) && 2 * second + 1 < n) {
+                __builtin_prefetch(&a[8 * Lay::block_line(i)]);
+                if (pfdeep && 8 * second + 7 < n)  // the four grandchildren own the blocks after it
+                    for (uint64_t gc = 4 * i; gc < 4 * i + 4; ++gc) __builtin_prefetch(&a[8 * Lay::block_line(gc)]);
+            }
+        }
+    }
+    void adjust(int64_t hole, int64_t n, DEnt value) {
+        const int64_t top = hole;
+        int64_t second = hole;
+        uint32_t mv_slot[64];
+        int64_t mv_pos[64];
+        int nm = 0;
+        while (second < (n - 1) / 2) {
+            prefetch_descent(second, n);
             second = 2 * (second + 1);
-            second -= (int64_t)cns(a[second], a[second - 1]);
-            a[hole] = a[second];
-            __builtin_prefetch(&recs[a[hole].slot()], 1);
-            mv_slot[nm] = a[hole].slot();
+            second -= (int64_t)cns(A(second), A(second - 1));
+            A(hole) = A(second);
+            __builtin_prefetch(&recs[A(hole).slot()], 1);
+            mv_slot[nm] = A(hole).slot();
             mv_pos[nm++] = hole;
             hole = second;
         }
         if ((n & 1) == 0 && second == (n - 2) / 2) {
             second = 2 * (second + 1);
-            a[hole] = a[second - 1];
-            mv_slot[nm] = a[hole].slot();
+            A(hole) = A(second - 1);
+            mv_slot[nm] = A(hole).slot();
             mv_pos[nm++] = hole;
             hole = second - 1;
         }
@@ -281,10 +335,10 @@ struct DenseHeap {
         push_hole(hole, top, value);
     }
     uint32_t pop() {
-        const uint32_t ret = a[0].slot();
+        const uint32_t ret = A(0).slot();
         const int64_t last = len - 1;
-        const DEnt value = a[last];
-        a[last] = a[0];
+        const DEnt value = A(last);
+        A(last) = A(0);
         adjust(0, last, value);
         --len;
         return ret;
@@ -296,48 +350,50 @@ struct DenseHeap {
             hang = true;  // cannot happen: a pqPos only names a slot the heap has held
             return;
         }
-        DEnt value = a[pos];
+        DEnt value = A(pos);
         if (value.slot() == x && pos < len) {
             value.f = fx;
-            a[pos].f = fx;
+            A(pos).f = fx;
         } else {
             ++scans;
             for (int64_t i = 0; i < len; ++i)
-                if (a[i].slot() == x) a[i].f = fx;
+                if (A(i).slot() == x) A(i).f = fx;
             value.f = recs[value.slot()].g + recs[value.slot()].h;
         }
         const int64_t parent = (pos - 1) / 2;
-        if (pos > 0 && cns(a[parent], value)) {
+        if (pos > 0 && cns(A(parent), value)) {
             int64_t par = (pos - 1) / 2, index = pos;
-            while (index > 0 && cns(a[par], value)) {
-                a[index] = a[par];
-                setpos(a[index], index);
+            while (index > 0 && cns(A(par), value)) {
+                A(index) = A(par);
+                setpos(A(index), index);
                 index = par;
                 par = (par - 1) / 2;
             }
             if (pos != index) {
-                a[index] = value;
+                A(index) = value;
                 setpos(value, index);
             }
         } else {
             // __down_heap as written (priority_queue-inl.h:176-208)
             int64_t index = pos, left = 2 * index + 1, right = 2 * index + 2, largest = len, guard = 0;
             while (index < len) {
-                if ((right >= len) || ((left < len) && cns(a[right], a[left]))) largest = left;
-                if (largest < len && cns(value, a[largest])) {
+                if ((right >= len) || ((left < len) && cns(A(right), A(left)))) largest = left;
+                if (largest < len && cns(value, A(largest))) {
                     if (largest == index || ++guard > 128) { hang = true; break; }
-                    a[index] = a[largest];
-                    setpos(a[largest], index);
+                    A(index) = A(largest);
+                    setpos(A(largest), index);
                     index = largest;
                     left = index * 2 + 1;
                     right = index * 2 + 2;
                 } else
                     break;
             }
-            if (pos != index) a[index] = value;
+            if (pos != index) A(index) = value;
         }
     }
 };
+using DenseHeap = DenseHeapT<FlatLayout>;
+using BlockedHeap = DenseHeapT<PairBlockLayout>;
 
 }  // namespace exact
 }  // namespace ulg

@@ -207,9 +207,12 @@ inline bool dense_eligible(uint64_t scope, uint64_t scc) {
     return m <= kDenseScopeBits && ((1ull << m) * (uint64_t)__builtin_popcountll(scc) * 4) <= kDenseRowsMaxBytes;
 }
 
-// run_astar_on_one_scc (astar_main.cpp:216-546) over dense node homes
-int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool skeleton_good, uint64_t ancestors,
-                uint64_t the_scc, int64_t *expanded, bool *hang, ExactResult &res, const Clock::time_point *deadline) {
+// run_astar_on_one_scc (astar_main.cpp:216-546) over dense node homes; HeapT:
+// the reference's heap in the flat (DenseHeap) or pair-block (BlockedHeap,
+// ULG_EXACT_PF bit 8) physical layout -- same pops, same pqPos
+template <class HeapT>
+int astar_dense_t(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool skeleton_good, uint64_t ancestors,
+                  uint64_t the_scc, int64_t *expanded, bool *hang, ExactResult &res, const Clock::time_point *deadline) {
     SearchState &s = *c->search;
     const int n = T.n;
     const uint64_t scope = ancestors | the_scc;
@@ -222,12 +225,16 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
     // the heap's buffer starts 8 B into a line, so a node's two children
     // (2i+1, 2i+2) share 16 aligned bytes and its 16 great-great-grandchildren
     // two lines
-    if (!recmem.reserve(nslots * sizeof(DenseRec), false) || !heapmem.reserve((nslots + 16) * sizeof(DEnt), false))
+    constexpr bool kBlocked = HeapT::Layout::kBlocked;
+    const uint64_t heap_entries =
+        kBlocked ? (uint64_t)PairBlockLayout::capacity((int64_t)nslots + 16) : nslots + 16;
+    if (!recmem.reserve(nslots * sizeof(DenseRec), false) || !heapmem.reserve(heap_entries * sizeof(DEnt), false))
         return set_err(c, ULG_ERR_HIP, "cannot map the dense search arrays");
     DenseRec *recs = static_cast<DenseRec *>(recmem.p);
-    DenseHeap open;
+    HeapT open;
     open.recs = recs;
-    open.a = static_cast<DEnt *>(heapmem.p) + 1;
+    // flat: 8 B into a line (siblings share 16 aligned bytes); blocked: line-aligned blocks
+    open.a = static_cast<DEnt *>(heapmem.p) + (kBlocked ? 0 : 1);
     // Prefetch modes (ULG_EXACT_PF, default 6, A/B only): bit 1, the pop also
     // prefetches 5 heap levels ahead (C3 17.6 -> 16.8 s on the box's EPYC
     // 9575F); bit 2, the heap top's successor records and cost row are
@@ -236,6 +243,7 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
     // or prefetch tried was no faster and is gone.
     const int pfmode = std::getenv("ULG_EXACT_PF") ? std::atoi(std::getenv("ULG_EXACT_PF")) : 6;
     open.pf5 = (pfmode & 2) != 0;
+    open.pfdeep = (pfmode & 512) != 0;  // blocked layout: the grandchildren's blocks too
 
     // slot bit of each variable, and its column in the row table
     uint32_t sbit[64] = {0};
@@ -270,7 +278,7 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
             // the node about to be popped is already known (the heap top):
             // its successor records and cost row are fetched while the pop
             // descends the heap, instead of after it
-            const uint32_t top = open.a[0].slot();
+            const uint32_t top = open.A(0).slot();
             const uint64_t tv = g_have_bmi2 ? pdep_bmi2(top, scope) : pdep64(top, scope);
             const float *trow = rows + (uint64_t)top * W;
             __builtin_prefetch(trow);
@@ -383,6 +391,15 @@ int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool ske
     res.found = true;
     res.goal_g = recs[goal].g;
     return ULG_OK;
+}
+
+int astar_dense(ulg_ctx *c, const HostTables &T, const uint64_t *edges, bool skeleton_good, uint64_t ancestors,
+                uint64_t the_scc, int64_t *expanded, bool *hang, ExactResult &res, const Clock::time_point *deadline) {
+    const int pfmode = std::getenv("ULG_EXACT_PF") ? std::atoi(std::getenv("ULG_EXACT_PF")) : 6;
+    if (pfmode & 256)
+        return astar_dense_t<BlockedHeap>(c, T, edges, skeleton_good, ancestors, the_scc, expanded, hang, res,
+                                          deadline);
+    return astar_dense_t<DenseHeap>(c, T, edges, skeleton_good, ancestors, the_scc, expanded, hang, res, deadline);
 }
 
 uint64_t all_vars(int n) { return (n >= 64) ? ~0ull : ((1ull << n) - 1ull); }

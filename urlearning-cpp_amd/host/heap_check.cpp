@@ -1,7 +1,8 @@
 // heap_check -- differential check of the two replays of the reference's
 // priority queue (csrc/exact_heap.h): Heap (node records in generation order,
 // used by the indexed exact search and triplet_astar) and DenseHeap (node
-// homes at pext(S, scope), used by the dense exact search).  Both must make
+// homes at pext(S, scope), used by the dense exact search), the latter in its
+// flat and its pair-block physical layout (BlockedHeap).  All must make
 // the same moves on the same push / pop / decrease-key sequence, including
 // the float ties the CompareNodeStar epsilon rule (base/node.h:124-135) and
 // the left-child-only __down_heap (priority_queue-inl.h:176-208) act on.
@@ -38,6 +39,13 @@ int main(int argc, char **argv) {
         DenseHeap d;
         d.recs = recs.data();
         d.a = buf.data() + 1;
+        // the blocked layout on its own records (the same values, its own pqPos)
+        std::vector<DenseRec> recs2(nslots, DenseRec{0.0f, 0.0f, 0, 0, {0, 0, 0}});
+        std::vector<DEnt> buf2((size_t)PairBlockLayout::capacity((int64_t)nslots + 2));
+        BlockedHeap bl;
+        bl.recs = recs2.data();
+        bl.a = buf2.data();
+        bl.pfdeep = (seed & 1) != 0;
 
         std::unordered_map<uint32_t, uint32_t> idx_of;  // slot -> index into nodes
         std::vector<uint32_t> open_slots;
@@ -63,6 +71,9 @@ int main(int argc, char **argv) {
                 recs[x].g = g;
                 recs[x].h = hh;
                 d.push(x);
+                recs2[x].g = g;
+                recs2[x].h = hh;
+                bl.push(x);
                 state[x] = 1;
                 open_slots.push_back(x);
                 ++pushes;
@@ -70,12 +81,14 @@ int main(int argc, char **argv) {
                 if (h.len == 0) continue;
                 const uint32_t a = nodes[h.pop()].sub;
                 const uint32_t b = d.pop();
-                if (a != b) {
-                    std::printf("FAIL op %ld: pop %u vs %u\n", op, a, b);
+                const uint32_t b2 = bl.pop();
+                if (a != b || b != b2) {
+                    std::printf("FAIL op %ld: pop %u vs %u vs %u (blocked)\n", op, a, b, b2);
                     return 1;
                 }
                 nodes[idx_of[a]].pq = -2;
                 recs[b].pq = -1;
+                recs2[b].pq = -1;
                 state[a] = 2;
                 ++closed;
                 ++pops;
@@ -91,11 +104,13 @@ int main(int argc, char **argv) {
                 const float g = recs[x].g - (cluster ? 5e-8f : 0.5f) * (float)(1 + rng() % 4);
                 nodes[idx_of[x]].g = g;
                 recs[x].g = g;
+                recs2[x].g = g;
                 h.update(idx_of[x]);
                 d.update(x);
+                bl.update(x);
                 ++updates;
             }
-            if (h.hang != d.hang) {
+            if (h.hang != d.hang || d.hang != bl.hang || d.len != bl.len) {
                 std::printf("FAIL op %ld: hang flags differ\n", op);
                 return 1;
             }
@@ -106,13 +121,14 @@ int main(int argc, char **argv) {
             }
             if (op % 97 == 0)
                 for (int64_t i = 0; i < h.len; ++i)
-                    if (nodes[h.a[i].idx].sub != d.a[i].slot() || h.a[i].f != d.a[i].f) {
+                    if (nodes[h.a[i].idx].sub != d.a[i].slot() || h.a[i].f != d.a[i].f ||
+                        bl.A(i).slot() != d.a[i].slot() || bl.A(i).f != d.a[i].f) {
                         std::printf("FAIL op %ld: heap slot %lld differs\n", op, (long long)i);
                         return 1;
                     }
         }
         for (uint32_t x = 0; x < nslots; ++x)
-            if (state[x] == 1 && nodes[idx_of[x]].pq + 1 != recs[x].pq) {
+            if (state[x] == 1 && (nodes[idx_of[x]].pq + 1 != recs[x].pq || recs2[x].pq != recs[x].pq)) {
                 std::printf("FAIL: pqPos of %u: %d vs %d\n", x, nodes[idx_of[x]].pq, recs[x].pq - 1);
                 return 1;
             }
