@@ -537,6 +537,82 @@ int main(int argc, char **argv) {
             }
         }
     }
+    // 12. the all-open key split by a secondary key (64 per wave): (a) the
+    //     var-0 toggles of the first-level nodes, (b) 6 of the second-level
+    //     nodes, (c) the full open words
+    {
+        const uint32_t root = PH_ == 0 ? ((1u << L_) - 1u) : (((1u << L_) - 1u) << 1);
+        std::vector<uint32_t> first;
+        for (int b2 = (PH_ == 0 ? 0 : 1); b2 <= (PH_ == 0 ? L_ - 1 : L_); ++b2) first.push_back(root ^ (1u << b2));
+        std::vector<Set *> heavy;
+        for (Set *x : all) {
+            bool allopen = true;
+            for (uint32_t t : first) allopen &= tb(x->open, t);
+            if (allopen) heavy.push_back(x);
+        }
+        auto keyA = [&](const Set *x) {
+            uint32_t k = 0;
+            for (uint32_t t : first) k = (k << 1) | (uint32_t)tb(x->open, t ^ 1u);
+            return k;
+        };
+        auto keyB = [&](const Set *x) {
+            uint32_t k = 0;
+            int nb = 0;
+            for (size_t i = 0; i < first.size() && nb < 6; ++i)
+                for (size_t j = i + 1; j < first.size() && nb < 6; ++j, ++nb)
+                    k = (k << 1) | (uint32_t)tb(x->open, first[i] & first[j]);
+            return k;
+        };
+        auto keyAB = [&](const Set *x) { return (keyA(x) << 6) | keyB(x); };
+        for (int mode = 0; mode < 4; ++mode) {
+            std::vector<Set *> o = heavy;
+            if (mode == 1) std::stable_sort(o.begin(), o.end(), [&](Set *a, Set *b) { return keyA(a) < keyA(b); });
+            if (mode == 2) std::stable_sort(o.begin(), o.end(), [&](Set *a, Set *b) { return keyB(a) < keyB(b); });
+            if (mode == 3) std::stable_sort(o.begin(), o.end(), [&](Set *a, Set *b) { return keyAB(a) < keyAB(b); });
+            long sum;
+            const long m = sched_max(o, 64, &sum);
+            const char *nm[] = {"queue order", "var-0 toggles", "6 second-level", "both (12 bits)"};
+            std::printf("all-open key (%zu sets), 64/wave, secondary key %s: max %ld sum %ld\n", heavy.size(), nm[mode],
+                        m, sum);
+        }
+    }
+    // 13. the other keys: by the first-level pattern only, or also by six
+    //     second-level nodes; 128 / 256 sets per wave
+    {
+        const uint32_t root = PH_ == 0 ? ((1u << L_) - 1u) : (((1u << L_) - 1u) << 1);
+        std::vector<uint32_t> first;
+        for (int b2 = (PH_ == 0 ? 0 : 1); b2 <= (PH_ == 0 ? L_ - 1 : L_); ++b2) first.push_back(root ^ (1u << b2));
+        auto k1 = [&](const Set *x) {
+            uint32_t k = 0;
+            for (size_t i = 0; i < first.size(); ++i) k |= (uint32_t)tb(x->open, first[i]) << i;
+            return k;
+        };
+        auto k2 = [&](const Set *x) {
+            uint32_t k = 0;
+            int nb = 0;
+            for (size_t i = 0; i < first.size() && nb < 6; ++i)
+                for (size_t j = i + 1; j < first.size() && nb < 6; ++j, ++nb)
+                    k = (k << 1) | (uint32_t)tb(x->open, first[i] & first[j]);
+            return k;
+        };
+        const uint32_t full = (1u << first.size()) - 1u;
+        std::vector<Set *> light;
+        for (Set *x : all)
+            if (k1(x) != full) light.push_back(x);
+        for (int two = 0; two < 2; ++two) {
+            std::vector<Set *> o = light;
+            std::stable_sort(o.begin(), o.end(), [&](Set *a, Set *b) {
+                const uint32_t ka = (k1(a) << 6) | (two ? k2(a) : 0u), kb = (k1(b) << 6) | (two ? k2(b) : 0u);
+                return ka < kb;
+            });
+            for (int per : {128, 256, 512}) {
+                long sum;
+                const long m = sched_max(o, per, &sum);
+                std::printf("not-all-open keys (%zu sets) by first-level%s, %d/wave: max %ld sum %ld\n", light.size(),
+                            two ? " + six second-level bits" : "", per, m, sum);
+            }
+        }
+    }
     // 5. oracle schedule: by true length
     {
         std::vector<size_t> ix(all.size());

@@ -216,8 +216,8 @@ constexpr int kSegBlocks = 32;
 constexpr uint64_t kSegEntries = (uint64_t)kSegBlocks * kBlock;
 constexpr int kSegStride = 16;  // counters 128 B apart
 // A bucketed launch's header after its segment counters (zeroed with them):
-// every key's set total (u32 64..127).
-constexpr int kBucketHdrWords = 64;
+// every key's set total (u32 64..191).
+constexpr int kBucketHdrWords = 128;
 // Bits of the call's error word (d_qcount[nqc - 1], zeroed by the prologue,
 // copied beside the stored count by scan_kernel): a wide walk over its cap;
 // a queue position past its segment (nothing is written there); a walk entry
@@ -234,15 +234,34 @@ __device__ __forceinline__ uint64_t walk_segment() { return blockIdx.x % seg_cou
 // nodes (P minus one member, the top call's tests) it may expand, one bit per
 // member -- sets with the same key start the same union walk, so a launch
 // sorted by key walks ~3x fewer union points (scripts/walk_sched_study.cpp).
+// When every first-level node is open (the longest, least alike walks), the
+// key is 64 + the open bits of six second-level nodes (P minus two members,
+// the first six pairs in order): those sets then split further (C3 layer 6
+// with variable 0: the longest wave 432 -> 294 union points).
 template <int L, int PHASE, int W>
 __device__ __forceinline__ uint32_t walk_key(const uint64_t (&ow)[W]) {
     constexpr uint32_t root = PHASE == 0 ? ((1u << L) - 1u) : (((1u << L) - 1u) << 1);
+    constexpr int off = PHASE == 0 ? 0 : 1;
     uint32_t key = 0;
 #pragma unroll
     for (int a = 0; a < L; ++a) {
-        constexpr int off = PHASE == 0 ? 0 : 1;
         const uint32_t t = root ^ (1u << (a + off));
         key |= (uint32_t)((ow[t >> 6] >> (t & 63u)) & 1ull) << a;
+    }
+    if (key == (1u << L) - 1u) {
+        uint32_t sec = 0;
+        int nb = 0;
+#pragma unroll
+        for (int a = 0; a < L; ++a)
+#pragma unroll
+            for (int b = a + 1; b < L; ++b) {
+                if (nb < 6) {
+                    const uint32_t t = root ^ (1u << (a + off)) ^ (1u << (b + off));
+                    sec |= (uint32_t)((ow[t >> 6] >> (t & 63u)) & 1ull) << nb;
+                }
+                ++nb;
+            }
+        key = 64u + sec;
     }
     return key;
 }
@@ -976,9 +995,8 @@ __global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, 
 // ~465 points and the launch's union points from 311 K to ~100 K
 // (scripts/walk_sched_study.cpp on the dumped queues).  Same walks, same
 // decisions: only which sets share a wave changes.
-constexpr int kBucketMax = 64;  // walk keys (L <= 6 first-level nodes)
+constexpr int kBucketMax = 128;  // walk keys: 64 first-level patterns, the all-open one split 64 ways
 
-__device__ __forceinline__ uint32_t bucket_order(uint32_t key, uint32_t full) { return key == full ? 0u : key + 1u; }
 
 // One block per kBucketSegs segments: the segments' key histogram in LDS
 // (16 keys per 16-byte load), each entry's rank among the block's sets of its
@@ -999,7 +1017,6 @@ __global__ void __launch_bounds__(256) walk_bucket_count_kernel(const unsigned l
     __shared__ unsigned int qnl[kBucketSegs];
     const uint32_t seg0 = blockIdx.x * kBucketSegs;
     const uint32_t nsb = nseg - seg0 < (uint32_t)kBucketSegs ? nseg - seg0 : (uint32_t)kBucketSegs;
-    const uint32_t nk = 1u << L;
     unsigned int *hdr = reinterpret_cast<unsigned int *>(const_cast<unsigned long long *>(qseg) + (uint64_t)nseg * kSegStride);
     if (threadIdx.x < kBucketMax) lh[threadIdx.x] = 0u;
     if (threadIdx.x < 64) {
@@ -1040,28 +1057,35 @@ __global__ void __launch_bounds__(256) walk_bucket_count_kernel(const unsigned l
         }
     }
     __syncthreads();
-    if (threadIdx.x < nk) {
+    if (threadIdx.x < kBucketMax) {
         const unsigned int c = lh[threadIdx.x];
         kbase[(uint64_t)blockIdx.x * kBucketMax + threadIdx.x] = c ? atomicAdd(hdr + 64 + threadIdx.x, c) : 0u;
     }
+    (void)L;
 }
 
-// The keys in walk order (the all-open key first) as one wave's lanes: lane kk
-// holds key order kk's set count, its first sorted position, and its wave
-// range [wbeg, wend) in the launch's wave list (64 sets per wave for the
-// all-open key, per_light for the others).  hdr: the launch's key totals.
+// The keys in walk order as one wave's lanes, two per lane: order kk = 2 lane
+// + h (h = 0, 1); orders 0..63 are the all-open sub-keys 64..127 (64 sets
+// per wave, one per lane), orders 64..127 the other first-level patterns
+// 0..63 (per_light sets per wave).  Per half: the key's set count, its first
+// sorted position and its wave range [wbeg, wend) in the launch's wave list.
 struct BucketLanes {
-    unsigned int tot, st, wbeg, wend, pk;
+    unsigned int tot[2], st[2], wbeg[2], wend[2], pk[2];
 };
-__device__ __forceinline__ BucketLanes bucket_lanes(const unsigned int *hdr, int L, uint32_t per_light) {
-    const uint32_t nk = 1u << L, full = nk - 1u;
+__device__ __forceinline__ uint32_t bucket_key(uint32_t kk) { return kk < 64 ? 64u + kk : kk - 64u; }
+__device__ __forceinline__ BucketLanes bucket_lanes(const unsigned int *hdr, uint32_t per_light) {
     const int lane = threadIdx.x & 63;
-    const uint32_t kk = (uint32_t)lane;
     BucketLanes b;
-    b.tot = kk < nk ? hdr[64 + (kk == 0 ? full : kk - 1u)] : 0u;
-    b.pk = kk == 0 ? 64u : per_light;
-    const unsigned int nwk = (b.tot + b.pk - 1) / b.pk;
-    unsigned int st = b.tot, wi = nwk;
+    unsigned int nw[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t kk = 2u * (uint32_t)lane + (uint32_t)h;
+        b.tot[h] = hdr[64 + bucket_key(kk)];
+        b.pk[h] = kk < 64 ? 64u : per_light;
+        nw[h] = (b.tot[h] + b.pk[h] - 1) / b.pk[h];
+    }
+    const unsigned int t2 = b.tot[0] + b.tot[1], w2 = nw[0] + nw[1];
+    unsigned int st = t2, wi = w2;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const unsigned int t = __shfl_up(st, o), u = __shfl_up(wi, o);
@@ -1070,9 +1094,12 @@ __device__ __forceinline__ BucketLanes bucket_lanes(const unsigned int *hdr, int
             wi += u;
         }
     }
-    b.st = st - b.tot;
-    b.wend = wi;
-    b.wbeg = wi - nwk;
+    b.st[0] = st - t2;
+    b.st[1] = b.st[0] + b.tot[0];
+    b.wbeg[0] = wi - w2;
+    b.wend[0] = b.wbeg[0] + nw[0];
+    b.wbeg[1] = b.wend[0];
+    b.wend[1] = wi;
     return b;
 }
 
@@ -1086,11 +1113,12 @@ __global__ void __launch_bounds__(256) walk_bucket_scatter_kernel(const unsigned
         reinterpret_cast<const unsigned int *>(qseg + (uint64_t)nseg * kSegStride);
     __shared__ unsigned int kst[kBucketMax];
     if (threadIdx.x < 64) {
-        const BucketLanes b = bucket_lanes(hdr, L, 64u);
-        const uint32_t nk = 1u << L, kk = threadIdx.x;
-        if (kk < nk) kst[kk == 0 ? nk - 1u : kk - 1u] = b.st;
+        const BucketLanes b = bucket_lanes(hdr, 64u);
+        kst[bucket_key(2 * threadIdx.x)] = b.st[0];
+        kst[bucket_key(2 * threadIdx.x + 1)] = b.st[1];
     }
     __syncthreads();
+    (void)L;
     const uint64_t items = (uint64_t)nseg * (kSegEntries / 256);
     for (uint64_t item = blockIdx.x; item < items; item += gridDim.x) {
         const uint32_t seg = (uint32_t)(item % nseg);
@@ -1198,17 +1226,21 @@ __global__ void __launch_bounds__(64) walk_bucket_kernel(const uint64_t *queue, 
                                                          uint64_t nslots, unsigned long long *err) {
     constexpr int NVMAX = Sliced<L, KL>::NV > Sliced<L, 1>::NV ? Sliced<L, KL>::NV : Sliced<L, 1>::NV;
     __shared__ uint32_t open_lds[NVMAX * 64];
-    const BucketLanes b = bucket_lanes(hdr, L, 64u * KL);
-    const uint32_t nw = __shfl(b.wend, 63);
+    const BucketLanes b = bucket_lanes(hdr, 64u * KL);
+    const uint32_t nw = __shfl(b.wend[1], 63);
     for (uint32_t w = blockIdx.x; w < nw; w += gridDim.x) {
-        // the key order kk holding wave w: the first lane whose range ends past w
-        const unsigned long long past = __ballot(b.wend > w);
-        const int kk = __ffsll((long long)past) - 1;
-        const uint32_t wbeg = __shfl(b.wbeg, kk), st = __shfl(b.st, kk), tot = __shfl(b.tot, kk),
-                       pk = __shfl(b.pk, kk);
+        // the lane holding wave w: the first whose range ends past w; then its half
+        const unsigned long long past = __ballot(b.wend[1] > w);
+        const int ln = __ffsll((long long)past) - 1;
+        const bool h1 = __shfl(b.wend[0], ln) <= w;
+        const uint32_t wbeg = h1 ? __shfl(b.wbeg[1], ln) : __shfl(b.wbeg[0], ln);
+        const uint32_t st = h1 ? __shfl(b.st[1], ln) : __shfl(b.st[0], ln);
+        const uint32_t tot = h1 ? __shfl(b.tot[1], ln) : __shfl(b.tot[0], ln);
+        const uint32_t pk = h1 ? __shfl(b.pk[1], ln) : __shfl(b.pk[0], ln);
+        const uint32_t kk = 2u * (uint32_t)ln + (h1 ? 1u : 0u);
         const uint32_t off = (w - wbeg) * pk;
         const uint32_t cw = tot - off < pk ? tot - off : pk;
-        if (kk == 0)
+        if (kk < 64)
             walk_group<L, PHASE, 1, NVMAX>(queue, sidx, st + off, cw, open_lds, table, hsub, nslots, err);
         else
             walk_group<L, PHASE, KL, NVMAX>(queue, sidx, st + off, cw, open_lds, table, hsub, nslots, err);
