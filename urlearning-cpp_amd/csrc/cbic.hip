@@ -988,11 +988,12 @@ __global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, 
 // writes each set's key, walk_bucket_count_kernel ranks the sets of each
 // segment by key and, in its last block, lays out the keys and a table of walk
 // waves, walk_bucket_scatter_kernel writes each set's queue index at its place -- and
-// walk_bucket_kernel walks the table.  The key whose every first-level node is
-// open holds the longest, least alike walks: it comes first in the table, 64
-// sets per wave (one per lane); every other key 64 x K per wave.  At C3's
-// layer 6 without variable 0 the longest wave's union walk drops from 811 to
-// ~465 points and the launch's union points from 311 K to ~100 K
+// walk_bucket_kernel walks the table.  The sets whose every first-level node
+// is open hold the longest, least alike walks: split 64 ways by six
+// second-level nodes (keys 64..127), they come first in the table, 64 sets per
+// wave (one per lane); every other key 64 x K per wave.  At C3's layer 6
+// without variable 0 the longest wave's union walk drops from 811 to ~465
+// points and the launch's union points from 311 K to ~100 K
 // (scripts/walk_sched_study.cpp on the dumped queues).  Same walks, same
 // decisions: only which sets share a wave changes.
 constexpr int kBucketMax = 128;  // walk keys: 64 first-level patterns, the all-open one split 64 ways
