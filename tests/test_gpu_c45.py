@@ -10,8 +10,8 @@ C5: n=32, N=50k, full skeleton.  As specified it is degenerate:
     (triplet_astar.cpp:837-844) and the MEC is empty.  The scorer runs the
     k = 6 variant: 30,164,768 parent sets.
 
-tests/golden/c45_oracle.json (make_c45_fixture.py) holds, for a few
-variables of each config, the oracle's stored-set count, a SHA-256 of the
+tests/golden/c45_oracle.json (make_c45_fixture.py) holds, for every C4
+variable (30) and 8 C5 variables, the oracle's stored-set count, a SHA-256 of the
 sorted masks, the score sum and every 512th (set, score).  The GPU must store
 exactly those sets, with every sampled score within 1e-6 relative.  On every
 variable of C5 the lists must also have the shape the reference produces

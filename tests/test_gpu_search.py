@@ -311,12 +311,13 @@ def test_exact_astar_dense_and_indexed_forms_agree(ulg_ctx, oracle_built, monkey
     assert out[0] == out[1]
 
 
-@pytest.mark.parametrize("pf", ["0", "2", "4"])
+@pytest.mark.parametrize("pf", ["0", "2", "4", "260", "772"])
 def test_exact_astar_prefetch_modes_identical(ulg_ctx, oracle_built, monkeypatch, pf):
     """ULG_EXACT_PF only moves prefetches (bit 1: five heap levels ahead in a
-    pop; bit 2: the heap top's records and cost row before its pop): the
-    dense replay's DAG, order, cost and expansion count stay the oracle's in
-    every mode."""
+    pop; bit 2: the heap top's records and cost row before its pop) or, with
+    value 256, the heap's physical layout (PairBlockLayout, exact_heap.h;
+    512: its deeper prefetch): the dense replay's DAG, order, cost and
+    expansion count stay the oracle's in every mode."""
     import ulg
     o = oracle_built
     n, k = 18, 4
