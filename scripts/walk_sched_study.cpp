@@ -22,6 +22,7 @@ struct Set {
 };
 
 static int L_, PH_, W_;
+static const bool clear_early = std::getenv("STUDY_CLEAR_EARLY") != nullptr;
 
 static inline bool tb(const uint64_t *w, uint32_t t) { return (w[t >> 6] >> (t & 63)) & 1ull; }
 static inline void cb(uint64_t *w, uint32_t t) { w[t >> 6] &= ~(1ull << (t & 63)); }
@@ -58,6 +59,11 @@ struct Group {
                     anyx |= x[k];
                 }
                 if (!anyx) continue;
+                // STUDY_CLEAR_EARLY: checked.insert(T2) once, before the
+                // calls (nothing below T2 reads T2's open bit)
+                if (clear_early)
+                    for (size_t k = 0; k < s.size(); ++k)
+                        if (x[k]) cb(&open[k * 8], T2);
                 uint32_t npv = 0;
                 int j = 0;
                 for (int i = 0; i < M; ++i) {
@@ -68,7 +74,7 @@ struct Group {
                     walk(T2, npv, x, M - 1, j == 1 ? 0 : j - 1, j == 1 ? (M - 1 < 2 ? M - 1 : 2) : j);
                     bool any2 = false;
                     for (size_t k = 0; k < s.size(); ++k) {
-                        if (x[k]) cb(&open[k * 8], T2);
+                        if (x[k] && !clear_early) cb(&open[k * 8], T2);
                         x[k] &= alive[k];
                         any2 |= x[k];
                     }

@@ -709,7 +709,14 @@ __device__ __forceinline__ void walk_sliced(uint32_t T, uint32_t pv, uint32_t ac
                 // twice, 2^(L-1) copies of the deepest one (a ~40 KB kernel)
                 walk_sliced<L, K, M - 1, DIAG, OV, PH>(T2, npv, x, hiV, openV, alive, dom, pts, j == 1 ? 0 : j - 1,
                                                        j == 1 ? (M - 1 < 2 ? M - 1 : 2) : j);
-                sl_clear<L, K>(openV, T2, x);  // checked.insert(T2) for the sets that ran the call
+                // checked.insert(T2) for the sets that ran the call.  Not
+                // once before the first call: the recursion can re-enter T2
+                // through two variable-0 toggles (zero padding), where the
+                // reference expands it again, and marking it early changes
+                // decisions (0.2 % of random bitsets,
+                // scripts/walk_mark_order_check.cpp).  After call 1 the
+                // later inserts are no-ops; skipping them measured no faster.
+                sl_clear<L, K>(openV, T2, x);
                 x &= alive;
                 if (!wave_any(x)) break;
             }
