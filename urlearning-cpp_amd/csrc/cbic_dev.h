@@ -689,6 +689,7 @@ __device__ __forceinline__ void walk_sliced(uint32_t T, uint32_t pv, uint32_t ac
             // zero (if any) and the padding: a few scalar operations per
             // expanded node instead of a compare per entry and call.  (Round
             // 6: the walk launches ~20 % shorter, C3 call 0.72 -> 0.67 ms.)
+            if (!wave_any(x)) continue;
             uint32_t rest;
             int cnt;
             if (u != 0u) {
@@ -701,7 +702,30 @@ __device__ __forceinline__ void walk_sliced(uint32_t T, uint32_t pv, uint32_t ac
                 cnt = __builtin_popcount(nz);
                 rest = (pv & 15u) == 0u ? (pv >> 4) : pv;
             }
-            if (!wave_any(x)) continue;
+            if constexpr (M == 2) {
+                // the callees (M = 1) only test: the j-th tests T2 minus
+                // entry j-1 for the sets still running.  Inlined as one loop;
+                // nothing below reads T2's open bit, so one insert at the end
+                // does what the insert after each call did -- when a call
+                // ran: a node whose list is empty is never inserted
+                // (scripts/walk_mark_order_check.cpp checks this form).
+                const uint32_t x0 = x;
+#pragma nounroll
+                for (int j = 1; j <= cnt; ++j) {
+                    x &= alive;
+                    if (!wave_any(x)) break;
+                    if constexpr (DIAG) ++pts;
+                    const uint32_t T3 = T2 ^ (1u << ((rest >> (4 * (j - 1))) & 15u));
+                    const uint32_t h3 = sl_get<L, K>(hiV, T3) & x;
+#ifdef ULG_GATHER_STATS
+                    if (h3) atomicAdd(&g_wstats[(L * 2 + PH) * 16 + (L - 1)], (unsigned long long)__builtin_popcount(h3));
+#endif
+                    dom |= h3;
+                    alive &= ~h3;
+                }
+                if (cnt > 0) sl_clear<L, K>(openV, T2, x0);
+                continue;
+            }
 #pragma nounroll
             for (int j = 1; j <= cnt; ++j) {
                 const uint32_t npv = j >= 8 ? rest : (rest & ((1u << (4 * j)) - 1u));
