@@ -964,10 +964,13 @@ __global__ void __launch_bounds__(64) walk_sliced_kernel(const uint64_t *queue, 
     for (int i = 0; i < L; ++i) pvtop |= (uint32_t)(i + (v0inP ? 0 : 1)) << (4 * i);
     uint32_t dom = 0u, pts = 0u;
     // the open bits in LDS (OpenLds): no vector copies per recursion level
-    __shared__ uint32_t open_lds[S::NV * 64];
+    __shared__ uint32_t open_lds[2 * S::NV * 64];
     OpenLds<L, K> ol{open_lds + threadIdx.x};
 #pragma unroll
-    for (int r = 0; r < S::NV; ++r) ol.base[r * 64] = openV[r];
+    for (int r = 0; r < S::NV; ++r) {
+        ol.base[r * 64] = openV[r];
+        ol.base[r * 64 + S::NV * 64] = hiV[r];
+    }
     if (wclock) walk_sliced<L, K, L, true, OpenLds<L, K>, PHASE>(Plocal, pvtop, alive, hiV, ol, alive, dom, pts);
     else walk_sliced<L, K, L, false, OpenLds<L, K>, PHASE>(Plocal, pvtop, alive, hiV, ol, alive, dom, pts);
 #ifdef ULG_GATHER_STATS
@@ -1199,10 +1202,13 @@ __device__ __forceinline__ void walk_group(const uint64_t *queue, const uint32_t
 #pragma unroll
     for (int i = 0; i < L; ++i) pvtop |= (uint32_t)(i + (v0inP ? 0 : 1)) << (4 * i);
     uint32_t dom = 0u, pts = 0u;
-    OpenLds<L, K> ol{open_lds + lane};
+    OpenLds<L, K, NVMAX * 64> ol{open_lds + lane};
 #pragma unroll
-    for (int r = 0; r < S::NV; ++r) ol.base[r * 64] = openV[r];
-    walk_sliced<L, K, L, false, OpenLds<L, K>, PHASE>(Plocal, pvtop, alive, hiV, ol, alive, dom, pts);
+    for (int r = 0; r < S::NV; ++r) {
+        ol.base[r * 64] = openV[r];
+        ol.base[r * 64 + NVMAX * 64] = hiV[r];
+    }
+    walk_sliced<L, K, L, false, OpenLds<L, K, NVMAX * 64>, PHASE>(Plocal, pvtop, alive, hiV, ol, alive, dom, pts);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         if (ent[k] == 0xFFFFFFFFu) continue;
@@ -1226,7 +1232,7 @@ __global__ void __launch_bounds__(64) walk_bucket_kernel(const uint64_t *queue, 
                                                          const unsigned int *hdr, float *table, float *hsub,
                                                          uint64_t nslots, unsigned long long *err) {
     constexpr int NVMAX = Sliced<L, KL>::NV > Sliced<L, 1>::NV ? Sliced<L, KL>::NV : Sliced<L, 1>::NV;
-    __shared__ uint32_t open_lds[NVMAX * 64];
+    __shared__ uint32_t open_lds[2 * NVMAX * 64];  // open bits, then the hi copy
     const BucketLanes b = bucket_lanes(hdr, 64u * KL);
     const uint32_t nw = __shfl(b.wend[1], 63);
     for (uint32_t w = blockIdx.x; w < nw; w += gridDim.x) {

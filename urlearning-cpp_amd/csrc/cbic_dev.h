@@ -631,20 +631,40 @@ __device__ __forceinline__ bool wave_any(uint32_t x) { return __ballot(x != 0u) 
 // offset and a clear one ds_and, where the register form's indexed write
 // makes the compiler copy the whole vector at every recursion level (16
 // v_mov_b64 per expanded node at layer 6).
-template <int L, int K>
+// A copy of the hi bits sits HOFF words further (read-only): a node's open
+// and hi words then come from one address, two LDS reads in flight together,
+// instead of an indexed register read (s_set_gpr_idx) beside the LDS read.
+template <int L, int K, int HOFF = Sliced<L, K>::NV * 64>
 struct OpenLds {
     uint32_t *base;  // this lane's word 0
 };
-template <int L, int K>
-__device__ __forceinline__ uint32_t sl_get(const OpenLds<L, K> &v, uint32_t t) {
+template <int L, int K, int HOFF>
+__device__ __forceinline__ uint32_t sl_get(const OpenLds<L, K, HOFF> &v, uint32_t t) {
     using S = Sliced<L, K>;
     return (v.base[(t / S::E) * 64] >> (S::K * (t % S::E))) & S::KM;
 }
-template <int L, int K>
-__device__ __forceinline__ void sl_clear(OpenLds<L, K> &v, uint32_t t, uint32_t m) {
+template <int L, int K, int HOFF>
+__device__ __forceinline__ void sl_clear(OpenLds<L, K, HOFF> &v, uint32_t t, uint32_t m) {
     using S = Sliced<L, K>;
     __hip_atomic_fetch_and(v.base + (t / S::E) * 64, ~(m << (S::K * (t % S::E))), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+template <class OV>
+struct HiOffset {
+    static constexpr int value = -1;  // no LDS copy: the registers
+};
+template <int L, int K, int HOFF>
+struct HiOffset<OpenLds<L, K, HOFF>> {
+    static constexpr int value = HOFF;
+};
+// the hi bits of t: from the LDS copy beside an OpenLds, else the registers
+template <int L, int K, class OV>
+__device__ __forceinline__ uint32_t sl_get_hi(const OV &v, const typename Sliced<L, K>::Vec &hiV, uint32_t t) {
+    using S = Sliced<L, K>;
+    if constexpr (HiOffset<OV>::value >= 0)
+        return (v.base[(t / S::E) * 64 + HiOffset<OV>::value] >> (S::K * (t % S::E))) & S::KM;
+    else
+        return sl_get<L, K>(hiV, t);
 }
 
 // [idx_lo, idx_hi): the positions this call can change anything at.  The
@@ -670,7 +690,7 @@ __device__ __forceinline__ void walk_sliced(uint32_t T, uint32_t pv, uint32_t ac
         const uint32_t u = (pv >> (4 * idx)) & 15u;
         const uint32_t T2 = T ^ (1u << u);
         // a hit ends that set's walk (the reference returns up the recursion)
-        const uint32_t h = sl_get<L, K>(hiV, T2) & act;
+        const uint32_t h = (M > 1 ? sl_get_hi<L, K>(openV, hiV, T2) : sl_get<L, K>(hiV, T2)) & act;
         dom |= h;
 #ifdef ULG_GATHER_STATS
         if (h) atomicAdd(&g_wstats[(L * 2 + PH) * 16 + (L - M)], (unsigned long long)__builtin_popcount(h));
