@@ -443,7 +443,7 @@ __device__ __forceinline__ void one_pass_set(const ScoreArgs &a, unsigned char *
         constexpr int W = bits_words(L);
         using BS = std::conditional_t<(W >= 4), BitsLds<W>, Bits<W>>;
         uint64_t *lds_bits = reinterpret_cast<uint64_t *>(smem + lay.bits) + threadIdx.x;
-        const LocalSet<L> ls = local_set<L>(cm, z);
+        const LocalSet<L> ls = local_set<L, PHASE>(cm, z);
         const uint64_t cpack = ls.cpack;
         const uint32_t Plocal = ls.Plocal;
         const uint32_t pvtop = ls.pvtop;
@@ -728,7 +728,7 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
         const uint64_t cmk = a1 ? ecm[k] : 1ull;
         const float hk1 = a1 ? ehch[k] : absent_f();
         uint64_t *lds_bits = reinterpret_cast<uint64_t *>(smem + lay.bits) + threadIdx.x;
-        const LocalSet<L> ls = local_set<L>(cmk, zk);
+        const LocalSet<L> ls = local_set<L, PHASE>(cmk, zk);
         BS present = make_bits<BS>(lds_bits);
         BS hib = make_bits<BS>(lds_bits + (size_t)W * kBlock);
         present.clear();
@@ -793,7 +793,7 @@ __global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
             const float tq = ets[k];
             const uint64_t sq = eslot[k];
             const float hq = ehch[k];
-            const LocalSet<L> lq = local_set<L>(ecm[k], zq);
+            const LocalSet<L> lq = local_set<L, PHASE>(ecm[k], zq);
             BS pq = make_bits<BS>(lds_bits), hq_bits = make_bits<BS>(lds_bits);
 #pragma unroll
             for (int j = 0; j < W; ++j) {

@@ -344,11 +344,15 @@ struct LocalSet {
     uint32_t pvtop;   // the top-level parent vector: P's local bits, 4 bits each
     bool v0inP;
 };
-template <int L>
+// PHASE (N4): phase-0 sets hold variable 0 and exist only when it is a
+// candidate (z; the host counts no phase-0 sets otherwise), phase-1 sets never
+// hold it -- so the root and the top list are constants of the phase and the
+// rule tests on them compile to fixed bit positions.
+template <int L, int PHASE>
 __device__ __forceinline__ LocalSet<L> local_set(uint64_t cm, bool z) {
     LocalSet<L> s;
-    s.v0inP = z && (cm & 1ull);
-    const uint64_t E = z ? (cm & ~1ull) : cm;
+    s.v0inP = PHASE == 0;
+    const uint64_t E = (PHASE == 0 || z) ? (cm & ~1ull) : cm;
     s.cpack = 0;
     uint64_t rem = E;
 #pragma unroll
