@@ -42,30 +42,34 @@ __device__ __forceinline__ uint32_t B(const uint32_t *binom, int a, int k) { ret
 // answer lies in [e - 3, e] for e = floor((r i!)^(1/i) + (i-1)/2) + 1, and
 // one round of four independent reads (e + 1 as the guard) settles it; the
 // scan remains as the fallback should the float estimate ever land low.
-__device__ __forceinline__ uint64_t unrank_colex(uint64_t r, int l, int U, const uint32_t *binom) {
+// Ranks of the unrolled layers fit 32 bits (C(63, 8) < 2^32, and the table
+// clamps C(a, b) to 32 bits anyway), so the arithmetic stays in 32-bit
+// registers: the callers are the layer kernels (L <= 8) and the list write.
+__device__ __forceinline__ uint64_t unrank_colex(uint64_t r64, int l, int U, const uint32_t *binom) {
     constexpr float kFact[9] = {1.f, 1.f, 2.f, 6.f, 24.f, 120.f, 720.f, 5040.f, 40320.f};
     constexpr float kInv[9] = {1.f, 1.f, 0.5f, 1.f / 3.f, 0.25f, 0.2f, 1.f / 6.f, 1.f / 7.f, 0.125f};
+    uint32_t r = (uint32_t)r64;
     uint64_t mask = 0;
     int c = U - 1;
     for (int i = l; i >= 1; --i) {
         int e;
         if (i == 1 || i > 8) {
-            e = i == 1 ? (int)(r < (uint64_t)c ? r : (uint64_t)c) : c;
+            e = i == 1 ? (int)(r < (uint32_t)c ? r : (uint32_t)c) : c;
         } else {
             const float g = exp2f(log2f((float)r * kFact[i]) * kInv[i]);  // r = 0: 0
             e = (int)(g + 0.5f * (float)(i - 1)) + 1;
             e = e < c ? e : c;
             e = e > i - 1 ? e : i - 1;  // C(i - 1, i) = 0 <= r
         }
-        const bool low = e < c && (uint64_t)B(binom, e + 1, i) <= r;  // the estimate fell short
-        const uint64_t b0 = B(binom, e, i);
-        const uint64_t b1 = e >= 1 ? B(binom, e - 1, i) : 0ull;
-        const uint64_t b2 = e >= 2 ? B(binom, e - 2, i) : 0ull;
+        const bool low = e < c && B(binom, e + 1, i) <= r;  // the estimate fell short
+        const uint32_t b0 = B(binom, e, i);
+        const uint32_t b1 = e >= 1 ? B(binom, e - 1, i) : 0u;
+        const uint32_t b2 = e >= 2 ? B(binom, e - 2, i) : 0u;
         int cc = b0 <= r ? e : (b1 <= r ? e - 1 : (b2 <= r ? e - 2 : -1));
-        uint64_t bc = b0 <= r ? b0 : (b1 <= r ? b1 : b2);
+        uint32_t bc = b0 <= r ? b0 : (b1 <= r ? b1 : b2);
         if (low || cc < 0) {
             cc = low ? c : e - 3;
-            while (cc >= 0 && (uint64_t)B(binom, cc, i) > r) --cc;
+            while (cc >= 0 && B(binom, cc, i) > r) --cc;
             bc = B(binom, cc, i);
         }
         mask |= 1ull << cc;
@@ -76,7 +80,7 @@ __device__ __forceinline__ uint64_t unrank_colex(uint64_t r, int l, int U, const
 }
 
 __device__ __forceinline__ uint64_t rank_colex(uint64_t mask, const uint32_t *binom) {
-    uint64_t r = 0;
+    uint32_t r = 0;
     int j = 0;
     while (mask) {
         const int a = __builtin_ctzll(mask);
@@ -514,10 +518,10 @@ __device__ __forceinline__ void child_ranks(uint64_t cm, const uint32_t *binom, 
         d[j] = B(binom, aj, j);
         f[j] = WITH0 ? B(binom, aj, j + 2) : 0u;
     }
-    uint64_t pe = 0, pf = 0;
+    uint32_t pe = 0, pf = 0;  // ranks of the unrolled layers fit 32 bits
 #pragma unroll
     for (int i = 0; i < L; ++i) {
-        uint64_t sd = 0, se = 0;
+        uint32_t sd = 0, se = 0;
 #pragma unroll
         for (int j = i + 1; j < L; ++j) {
             sd += d[j];
@@ -784,12 +788,15 @@ __device__ __forceinline__ float cbic_set_score(const double *g, int n, int v, c
                                                 double lambda) {
     double Lm[L][L];
     double y[L];
+    int ro[L];  // row offsets gv[i] * n (< 2^24: a full-rate 24-bit multiply)
+#pragma unroll
+    for (int i = 0; i < L; ++i) ro[i] = __mul24(gv[i], n);
 #pragma unroll
     for (int i = 0; i < L; ++i)
 #pragma unroll
-        for (int j = 0; j <= i; ++j) Lm[i][j] = g[gv[i] * n + gv[j]];
+        for (int j = 0; j <= i; ++j) Lm[i][j] = g[ro[i] + gv[j]];
 #pragma unroll
-    for (int i = 0; i < L; ++i) y[i] = g[gv[i] * n + v];
+    for (int i = 0; i < L; ++i) y[i] = g[ro[i] + v];
     const double cvv = g[v * n + v];
 #pragma unroll
     for (int j = 0; j < L; ++j) {
