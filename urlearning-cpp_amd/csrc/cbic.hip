@@ -181,8 +181,35 @@ struct LdsLayout {
 };
 constexpr int kCmpEntryBytes = 8 + 4 + 4 + 4 + 4;
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
+#ifndef ULG_LDS_ALIAS
+#define ULG_LDS_ALIAS 1
+#endif
 __host__ __device__ inline LdsLayout lds_layout(int n, int nv, int S, int L, int V) {
     LdsLayout l;
+    if (ULG_LDS_ALIAS && (V & 208) == 208 && bits_words(L) < 4) {
+        // the two-pass kernels with the second compaction (variant bit 7):
+        // the Gram matrix, the work prefixes and the candidate lists are
+        // read only before the block's first barrier (the scores and the
+        // subset-maxima settle), and the compaction entries and their words
+        // are written only after it -- so they share one region.  The
+        // counters, the binomials, the slab offsets and the metadata, read
+        // throughout, sit in front of it.  C3 layer 6: 26.7 -> 19 KB per
+        // block, 6 -> 8 blocks per CU (C5: 5 -> 8).
+        const int W = bits_words(L);
+        l.binom = 0;
+        l.toff = align16(l.binom + 64 * kBinomK * 4);
+        l.meta = align16(l.toff + (nv * S + 1) * 8);
+        l.cmp = align16(l.meta + nv * 4 * 4);  // 16 bytes of counters, then the entries
+        const int ra = l.cmp + 16;             // the shared region
+        l.gram = ra;
+        l.work = align16(l.gram + n * n * 8);
+        l.cand = align16(l.work + (nv + 1) * 8);
+        l.stack = l.bits = align16(l.cand + nv * 64);
+        l.cmp2 = align16(ra + kBlock * kCmpEntryBytes);
+        const int endc = l.cmp2 + 2 * W * kBlock * 8;
+        l.total = l.stack > endc ? l.stack : endc;
+        return l;
+    }
     l.gram = 0;
     l.binom = align16(l.gram + n * n * 8);
     l.work = align16(l.binom + 64 * kBinomK * 4);
@@ -563,7 +590,10 @@ __device__ __forceinline__ void walk_or_store(const ScoreArgs &a, BS &present, B
 // ulg_set_option "score_variant"), compile-time so each form gets its own
 // register allocation.
 template <int L, int PHASE, int V>
-__global__ void __launch_bounds__(kBlock) score_layer_kernel(ScoreArgs a) {
+#ifndef ULG_SCORE_MINBLOCKS
+#define ULG_SCORE_MINBLOCKS 1
+#endif
+__global__ void __launch_bounds__(kBlock, ULG_SCORE_MINBLOCKS) score_layer_kernel(ScoreArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const LdsLayout lay = lds_layout(a.n, a.nv, a.S, L, V);
     double *g = reinterpret_cast<double *>(smem + lay.gram);
