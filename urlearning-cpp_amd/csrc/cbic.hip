@@ -586,14 +586,20 @@ __device__ __forceinline__ void walk_or_store(const ScoreArgs &a, BS &present, B
     }
 }
 
+// Minimum waves per SIMD for the register allocator (the second argument of
+// __launch_bounds__): the layer-6 two-pass launch without variable 0, the
+// largest, at 6 (80 VGPRs instead of 82, which left 5 waves per SIMD): C3
+// 188 -> 178 us, C5 1,405 -> 1,323 us.  8 (64 VGPRs) spills more and slowed
+// the phase-0 launch 210 -> 269 us; the other kernels keep their allocation.
+template <int L, int PHASE, int V>
+constexpr int score_min_waves() {
+    return (L == 6 && PHASE == 1 && (V & 16) != 0) ? 6 : 1;
+}
 // PHASE 0: sets containing variable 0; 1: the rest.  V = variant bits (see
 // ulg_set_option "score_variant"), compile-time so each form gets its own
 // register allocation.
 template <int L, int PHASE, int V>
-#ifndef ULG_SCORE_MINBLOCKS
-#define ULG_SCORE_MINBLOCKS 1
-#endif
-__global__ void __launch_bounds__(kBlock, ULG_SCORE_MINBLOCKS) score_layer_kernel(ScoreArgs a) {
+__global__ void __launch_bounds__(kBlock, (score_min_waves<L, PHASE, V>())) score_layer_kernel(ScoreArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const LdsLayout lay = lds_layout(a.n, a.nv, a.S, L, V);
     double *g = reinterpret_cast<double *>(smem + lay.gram);
