@@ -591,9 +591,12 @@ __device__ __forceinline__ void walk_or_store(const ScoreArgs &a, BS &present, B
 // largest, at 6 (80 VGPRs instead of 82, which left 5 waves per SIMD): C3
 // 188 -> 178 us, C5 1,405 -> 1,323 us.  8 (64 VGPRs) spills more and slowed
 // the phase-0 launch 210 -> 269 us; the other kernels keep their allocation.
+#ifndef ULG_L6_REST_WAVES
+#define ULG_L6_REST_WAVES 6
+#endif
 template <int L, int PHASE, int V>
 constexpr int score_min_waves() {
-    return (L == 6 && PHASE == 1 && (V & 16) != 0) ? 6 : 1;
+    return (L == 6 && PHASE == 1 && (V & 16) != 0) ? ULG_L6_REST_WAVES : 1;
 }
 // PHASE 0: sets containing variable 0; 1: the rest.  V = variant bits (see
 // ulg_set_option "score_variant"), compile-time so each form gets its own
