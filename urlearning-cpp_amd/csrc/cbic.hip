@@ -588,11 +588,12 @@ __device__ __forceinline__ void walk_or_store(const ScoreArgs &a, BS &present, B
 
 // Minimum waves per SIMD for the register allocator (the second argument of
 // __launch_bounds__): the layer-6 two-pass launch without variable 0, the
-// largest, at 6 (80 VGPRs instead of 82, which left 5 waves per SIMD): C3
-// 188 -> 178 us, C5 1,405 -> 1,323 us.  8 (64 VGPRs) spills more and slowed
-// the phase-0 launch 210 -> 269 us; the other kernels keep their allocation.
+// largest, at 7 (72 VGPRs; 82 had left 5 waves per SIMD): C3 188 -> 175 us,
+// C5 1,405 -> 1,293 us (6: 178 / 1,302 us).  8 for every kernel (64 VGPRs)
+// spilled more and slowed the phase-0 launch 210 -> 269 us; the other
+// kernels keep their allocation.
 #ifndef ULG_L6_REST_WAVES
-#define ULG_L6_REST_WAVES 6
+#define ULG_L6_REST_WAVES 7
 #endif
 template <int L, int PHASE, int V>
 constexpr int score_min_waves() {
