@@ -595,9 +595,16 @@ __device__ __forceinline__ void walk_or_store(const ScoreArgs &a, BS &present, B
 #ifndef ULG_L6_REST_WAVES
 #define ULG_L6_REST_WAVES 7
 #endif
+#ifndef ULG_L6_VAR0_WAVES
+#define ULG_L6_VAR0_WAVES 1
+#endif
+#ifndef ULG_L4_WAVES
+#define ULG_L4_WAVES 1
+#endif
 template <int L, int PHASE, int V>
 constexpr int score_min_waves() {
-    return (L == 6 && PHASE == 1 && (V & 16) != 0) ? ULG_L6_REST_WAVES : 1;
+    return (L == 6 && (V & 16) != 0) ? (PHASE == 1 ? ULG_L6_REST_WAVES : ULG_L6_VAR0_WAVES)
+                                     : (L == 4 ? ULG_L4_WAVES : 1);
 }
 // PHASE 0: sets containing variable 0; 1: the rest.  V = variant bits (see
 // ulg_set_option "score_variant"), compile-time so each form gets its own
