@@ -590,16 +590,18 @@ __device__ __forceinline__ void walk_or_store(const ScoreArgs &a, BS &present, B
 // __launch_bounds__): the layer-6 two-pass launch without variable 0, the
 // largest, at 7 (72 VGPRs; 82 had left 5 waves per SIMD): C3 188 -> 175 us,
 // C5 1,405 -> 1,293 us (6: 178 / 1,302 us).  8 for every kernel (64 VGPRs)
-// spilled more and slowed the phase-0 launch 210 -> 269 us; the other
-// kernels keep their allocation.
+// spilled more and slowed the phase-0 launch 210 -> 269 us.  The phase-0
+// launch at 7 (72 VGPRs): 215 -> 208 us at C5; the layer-4 one-pass kernels
+// at 8 (60 VGPRs, no spills): C5 81 -> 79 us.  The others keep their
+// allocation.
 #ifndef ULG_L6_REST_WAVES
 #define ULG_L6_REST_WAVES 7
 #endif
 #ifndef ULG_L6_VAR0_WAVES
-#define ULG_L6_VAR0_WAVES 1
+#define ULG_L6_VAR0_WAVES 7
 #endif
 #ifndef ULG_L4_WAVES
-#define ULG_L4_WAVES 1
+#define ULG_L4_WAVES 8
 #endif
 template <int L, int PHASE, int V>
 constexpr int score_min_waves() {
