@@ -2197,10 +2197,13 @@ constexpr int kWriteLdsSegs = 2048;  // slab offsets staged in LDS up to this ma
 // locates its first slot's (variable, layer) segment and unranks it once;
 // every later slot is the colex successor (Gosper's hack, typedefs.h:692-697)
 // inside the segment, or the first set (1 << L) - 1 of the next one.
-__global__ void __launch_bounds__(kBlock) write_kernel(WriteArgs a) {
+// 8 waves per SIMD (<= 64 VGPRs) and the slab offsets in dynamic LDS sized
+// to the call ((nv * S + 1) * 8 bytes, 1.6 KB at C3, instead of a fixed 16 KB):
+// the kernel waits on its loads, so resident waves are what it needs.
+__global__ void __launch_bounds__(kBlock, 8) write_kernel(WriteArgs a) {
     __shared__ uint32_t pre[kBlock / 64];
     __shared__ uint32_t binom[64 * kBinomK];
-    __shared__ uint64_t toff_s[kWriteLdsSegs + 1];
+    extern __shared__ uint64_t toff_s[];  // (nv * S + 1) entries when nv * S <= kWriteLdsSegs
     __shared__ uint32_t cand_s[64 * 16];  // the candidate lists (64 bytes per variable, nv <= 64)
     const int nseg = a.nv * a.S;
     const bool lds_off = nseg <= kWriteLdsSegs;
@@ -2244,6 +2247,10 @@ __global__ void __launch_bounds__(kBlock) write_kernel(WriteArgs a) {
                              : unrank_colex64(s0 - toff[seg], L, m, a.binom64);
     for (int j = first; j < kSlotsPerThread; ++j) {
         const uint64_t s = base + j;
+        // the last block's slots past the table hold nothing, and the
+        // segment search below must not run past the last offset
+        // (toff[nseg] = total): it read toff[nseg + 1]
+        if (s >= a.total) break;
         if (j > first) {
             if (s >= toff[seg + 1]) {
                 while (s >= toff[seg + 1]) ++seg;
@@ -3613,7 +3620,11 @@ static int cbic_score(ulg_ctx *c, const int *vars, int nv, const uint64_t *candi
     wa.scores = c->out_scores.p;
     wa.offsets = c->out_offsets.p;
     prof_begin(c, "write_stored");
-    write_kernel<<<(unsigned)nb, kBlock, 0, c->stream>>>(wa);
+    {
+        const size_t nseg = (size_t)nv * (size_t)S;
+        const size_t toff_bytes = nseg <= (size_t)kWriteLdsSegs ? (nseg + 1) * sizeof(uint64_t) : 0;
+        write_kernel<<<(unsigned)nb, kBlock, toff_bytes, c->stream>>>(wa);
+    }
     prof_end(c);
     ULG_HIP(c, hipGetLastError());
     if (use_graph) {
